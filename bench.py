@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""bench.py — Msamples/s of the MI355X path tracer on the canonical RTIOW scene (BASELINE.json).
+
+One step = one frame of the hot path: every pixel of the 1920x1080 image traced at `--spp`
+samples, depth 50, on the canonical scene (generateRandomScene(t=0): 488 spheres, camera
+(13,11,-3) -> origin), i.e. BASELINE.json config 2's input. For N > 1 the step also includes the
+RCCL gather of every rank's row strips to rank 0 and the on-device reassembly (strong scaling:
+the image is fixed, each GPU renders 1/N of its rows).
+
+Launch: python bench.py [--gpus 1 --steps 5 --warmup 2]
+        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+Rank 0 prints one JSON line (DESIGN.md §6 explains every field).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "ray-tracing-gpu-vulkan_amd"))
+
+VALU_FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, vector FP32 (256 CU x 2.4 GHz)
+HBM_PEAK_GBPS = 8000.0
+FLOP_PER_SPHERE_TEST = 23
+FLOP_PER_BOX_TEST = 20
+
+
+def host_cores() -> int:
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, 16))    # the GPU box grants a 16-CPU share
+
+
+def cpu_baseline(width: int, height: int) -> dict:
+    """The CPU oracle (C++ restatement of the shaders, brute-force closest hit) on config 1:
+    one full 1920x1080 frame at 1 spp, timed on this host's cores."""
+    from oracle import oracle
+    oracle.build()
+    sc = oracle.generate_scene(0.0)
+    rci = oracle.render_call_info(1, width, height)
+    threads = host_cores()
+    t0 = time.perf_counter()
+    _, _, st = oracle.render(sc, rci, width, height, threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(width * height / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads,
+            "kind": "port",
+            "sample": f"config 1: {width}x{height} at 1 spp, depth 50, brute-force closest hit, "
+                      f"{threads} threads, {dt:.2f} s, {st[0] / st[1]:.3f} segments/sample"}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--spp", type=int, default=100)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--accel", choices=["lbvh", "brute"], default="lbvh")
+    ap.add_argument("--grid", type=int, default=11, help="scene grid half extent (11: 488 spheres)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-brute-line", action="store_true", help="skip the brute-force side measurement")
+    ap.add_argument("--profile", action="store_true", help="short run for rocprofv3 (no side legs)")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import rtvk
+    from rtvk import abi
+    from rtvk.dist import DistributedRenderer, hip_assembler, hip_band_renderer
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    W, H, spp = args.width, args.height, args.spp
+    accel = abi.RT_ACCEL_BRUTE if args.accel == "brute" else abi.RT_ACCEL_LBVH
+    renderer = rtvk.Renderer(local)
+    scene = rtvk.generateRandomScene(0.0, args.grid)
+    renderer.set_scene(scene)
+    rci = rtvk.canonical_render_call_info(spp, W, H)
+    opts = rtvk.make_options(accel=accel)
+    stream = torch.cuda.current_stream()
+    ev = []
+
+    base_render = hip_band_renderer(renderer, rci, opts)
+
+    def timed_render(rows, accum, out):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        base_render(rows, accum, out)
+        e1.record(stream)
+        ev.append((e0, e1))
+
+    dr = DistributedRenderer(W, H, dev, timed_render, hip_assembler(renderer))
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        dr.step()
+    barrier()
+    ev.clear()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        dr.step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / max(1, len(ev))
+    st = renderer.stats()   # last frame's counters on this rank
+
+    samples_per_step = W * H * spp
+    value = samples_per_step * args.steps / elapsed / 1e6
+
+    # Algorithmic work of one launch on this rank, counted by the instrumented build of the same
+    # kernel (identical image, same traversal; outside the timed region).
+    local_rows = len(dr.rows_np)
+    cnt_opts = rtvk.make_options(accel=accel, count_tests=True)
+    if local_rows:
+        acc = torch.zeros((local_rows, W, 4), dtype=torch.float32, device=dev)
+        out = torch.zeros((local_rows, W, 4), dtype=torch.uint8, device=dev)
+        renderer.render_device(rci, acc, out, rows=dr.rows, options=cnt_opts)
+        torch.cuda.synchronize()
+        cs = renderer.stats()
+        del acc, out
+    else:
+        cs = rtvk.Stats()
+    flops = cs.box_tests * FLOP_PER_BOX_TEST + cs.sphere_tests * FLOP_PER_SPHERE_TEST
+    achieved = flops / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
+
+    result = None
+    if rank == 0:
+        traffic = None
+        tf = ROOT / "profiles" / "pmc_traffic.json"
+        if tf.exists():
+            try:
+                tj = json.loads(tf.read_text())
+                key = f"{args.accel}-{W}x{H}-{spp}spp-grid{args.grid}-n{world}"
+                traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
+            except (ValueError, OSError):
+                traffic = None
+        roof = {"bound": "valu-fp32", "achieved": round(achieved, 3), "peak": VALU_FP32_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved / VALU_FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+                "kernel": f"rt_trace_kernel<{'ACCEL_LBVH' if accel == 2 else 'ACCEL_BRUTE'},false>",
+                "kernel_ms": round(kernel_ms, 4),
+                "flop_per_launch": int(flops), "box_tests": int(cs.box_tests),
+                "sphere_tests": int(cs.sphere_tests),
+                "flop_model": "20/box test + 23/sphere test (SURVEY.md 8(d)); counts from the "
+                              "instrumented build of the same kernel"}
+        result = {
+            "metric": "Msamples/s (1920x1080 RTIOW scene, depth 50)",
+            "value": round(value, 2),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": f"synthetic: canonical scene generateRandomScene(t=0), {len(scene)} spheres, "
+                    "camera (13,11,-3) -> origin, global per-pixel seeds TEA(TEA(x,y),0)",
+            "config": {"workload": f"rtiow-{W}x{H}-{spp}spp-depth50 (BASELINE config 2 input)",
+                       "width": W, "height": H, "spp": spp, "depth": 50, "spheres": len(scene),
+                       "accel": args.accel, "parallelism": f"row-strips x{world} + rccl gather"},
+            "segments_per_sample": round(st.segments / max(1, st.samples), 4),
+            "msegments_per_s": round(st.segments * world / max(1, st.samples) * value, 2)
+            if world == 1 else None,
+            "roofline": roof,
+            "context": {"reference_rx6800xt_vulkan_rt_msamples": 1658.9,
+                        "source": "README.md:57,61 via BASELINE.md (different GPU, HW RT cores)"},
+        }
+    # Side measurement: brute force (BASELINE config 2 as specified: no BVH), N = 1 only.
+    if world == 1 and not args.no_brute_line and not args.profile and accel != abi.RT_ACCEL_BRUTE:
+        bopts = rtvk.make_options(accel=abi.RT_ACCEL_BRUTE)
+        acc = torch.zeros((H, W, 4), dtype=torch.float32, device=dev)
+        out = torch.zeros((H, W, 4), dtype=torch.uint8, device=dev)
+        renderer.render_device(rci, acc, out, options=bopts)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 2
+        e0.record(stream)
+        for _ in range(reps):
+            renderer.render_device(rci, acc, out, options=bopts)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        bms = e0.elapsed_time(e1) / reps
+        bst = renderer.stats()
+        bflops = bst.segments * len(scene) * FLOP_PER_SPHERE_TEST
+        result["brute_force"] = {
+            "value": round(samples_per_step / (bms * 1e-3) / 1e6, 2), "unit": "Msamples/s",
+            "kernel_ms": round(bms, 3),
+            "roofline": {"bound": "valu-fp32", "achieved": round(bflops / (bms * 1e-3) / 1e12, 3),
+                         "peak": VALU_FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(bflops / (bms * 1e-3) / 1e12 / VALU_FP32_PEAK_TFLOPS, 4)}}
+        del acc, out
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile:
+        result["cpu_baseline"] = cpu_baseline(W, H)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    renderer.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,166 @@
+/*
+ * rt_mi355x.h — C-ABI boundary of the MI355X path tracer (librt_mi355x.so).
+ *
+ * Plain C: pointers, sizes and the byte-exact structs of rt_abi.h. No torch, no
+ * HIP types in the signatures (streams travel as void*).
+ *
+ * What each entry point replaces in the reference (water-chika/ray-tracing-gpu-vulkan):
+ *
+ *   ray_trace()              src/ray_trace.h:5-15 / src/ray_trace.cpp:922-972 — same symbol and
+ *                            signature; headless, renders once, honours `storeRenderResult`
+ *                            (the reference accepts but ignores it, src/ray_trace.cpp:928) and
+ *                            RETURNS (the reference loops until its window closes, :88/:567).
+ *   rt_generate_scene()      src/scene.h:79-157 generateRandomScene(), with the wall-clock time
+ *                            (:82-83) made an explicit argument and the 22x22 grid generalised to
+ *                            a (2K)x(2K) grid (K = 11 is the reference scene; K = 158 is config 5).
+ *   rt_canonical_render_call_info()
+ *                            the RenderCallInfo the reference fills per frame,
+ *                            src/ray_trace.cpp:660-676 (number 0, camera (13,11,-3) -> origin).
+ *   rt_context_create() + rt_set_scene()
+ *                            the per-frame scene upload + acceleration-structure build:
+ *                            AABBs src/ray_trace.cpp:583-599, BLAS src/vulkan.h:395-453,
+ *                            TLAS src/vulkan.h:463-554, rebuild src/vulkan.h:1020-1059,
+ *                            UBO upload src/vulkan.h:1239-1254.
+ *   rt_render_device()       the per-frame GPU work of one device: clear accumulator
+ *                            (src/vulkan.h:1061-1106) + vkCmdTraceRaysKHR(W, band_h, 1)
+ *                            (src/vulkan.h:994-995) executing shaders/shader.{rgen,rint,rchit,rmiss}.
+ *                            Device pointers, caller's stream, asynchronous.
+ *   rt_render()              host-pointer convenience wrapper (one call = one frame); rci_count > 1
+ *                            renders one band per GPU like src/ray_trace.cpp:74-93.
+ *
+ * Error model: every rt_* call returns RT_OK (0) or a negative rt_status; the message of the
+ * calling thread's last failure is rt_last_error(). Exceptions never cross this boundary (the
+ * reference lets C++ exceptions escape its extern "C" function). ray_trace() has
+ * no return value in the reference; it prints the error to stderr, as src/main.cpp:61-63 does.
+ *
+ * Threading: a context is thread-compatible (one call at a time per context); distinct contexts
+ * may be used concurrently from distinct threads.
+ */
+#ifndef RT_MI355X_H
+#define RT_MI355X_H
+
+#include <stdbool.h>
+#include <stdint.h>
+#include "rt_abi.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1u
+
+typedef enum rt_status {
+    RT_OK = 0,
+    RT_ERR_INVALID_ARGUMENT = -1,
+    RT_ERR_DEVICE = -2,       /* a HIP runtime call failed                         */
+    RT_ERR_OUT_OF_MEMORY = -3,
+    RT_ERR_NO_SCENE = -4,     /* rt_render_device() before rt_set_scene()          */
+    RT_ERR_IO = -5,           /* image store failed                                */
+    RT_ERR_NO_DEVICE = -6     /* no HIP device visible                             */
+} rt_status;
+
+/* Per-pixel seed coordinates. */
+typedef enum rt_seed_mode {
+    RT_SEED_GLOBAL = 0,        /* seed = TEA(TEA(x_global, y_global), number): image independent of GPU count */
+    RT_SEED_LAUNCH_LOCAL = 1   /* seed = TEA(TEA(launchID.x, launchID.y), number): shader.rgen:40 verbatim  */
+} rt_seed_mode;
+
+/* Random stream layout. */
+typedef enum rt_rng_mode {
+    RT_RNG_PIXEL_STREAM = 0,   /* reference: one LCG stream per pixel runs through every sample (random.glsl)   */
+    RT_RNG_SAMPLE_COUNTER = 1  /* counter-based: sample s of a pixel starts at TEA(pixel_seed, s): samples of a
+                                  pixel are independent and may be split across launches / devices             */
+} rt_rng_mode;
+
+/* Closest-hit search structure (the reference uses the driver's BVH, src/vulkan.h:395-554). */
+typedef enum rt_accel {
+    RT_ACCEL_AUTO = 0,         /* LBVH                                                   */
+    RT_ACCEL_BRUTE = 1,        /* every sphere per segment, sphere list from the scalar cache */
+    RT_ACCEL_LBVH = 2          /* linear BVH (Morton order, Karras hierarchy)            */
+} rt_accel;
+
+typedef struct rt_options {
+    uint32_t max_depth;   /* segments per sample; 0 -> 50 (shader.rgen:27)                       */
+    uint32_t seed_mode;   /* rt_seed_mode                                                        */
+    uint32_t rng_mode;    /* rt_rng_mode                                                         */
+    uint32_t accel;       /* rt_accel                                                            */
+    uint32_t accumulate;  /* 0: clear the accumulator first (src/vulkan.h:1081-1086); 1: add on top */
+    uint32_t sample_base; /* RT_RNG_SAMPLE_COUNTER only: index of this launch's first sample       */
+    uint32_t reserved[2];
+} rt_options;
+
+/* Statistics of the last rt_render_device() on a context (valid after its stream completes). */
+typedef struct rt_stats {
+    uint64_t segments;      /* traced segments (one traceRayEXT each, shader.rgen:75)              */
+    uint64_t samples;       /* camera samples                                                     */
+    uint64_t box_tests;     /* LBVH node-box tests (0 for brute force)                             */
+    uint64_t sphere_tests;  /* ray-sphere tests (shader.rint:44-60 evaluations)                    */
+} rt_stats;
+
+typedef struct rt_context rt_context;
+
+/* ---- library ---------------------------------------------------------------------- */
+uint32_t    rt_abi_version(void);
+const char* rt_last_error(void);
+int         rt_device_count(int* count);
+
+/* ---- host data API (scene.h / render_call_info.h) --------------------------------- */
+/* generateRandomScene(t) with a (2K)x(2K) grid: writes 4 + 4K^2 spheres (488 for K = 11). */
+int rt_generate_scene(float t, uint32_t grid_half_extent, Sphere* out, uint32_t capacity,
+                      uint32_t* count);
+int rt_canonical_render_call_info(uint32_t spp, uint32_t width, uint32_t height,
+                                  RenderCallInfo* out);
+
+/* ---- device API ------------------------------------------------------------------- */
+int rt_context_create(int device, rt_context** out);
+int rt_context_destroy(rt_context* ctx);
+/* Uploads `count` spheres (host memory) and builds the acceleration structures on the device. */
+int rt_set_scene(rt_context* ctx, const Sphere* spheres, uint32_t count, void* stream);
+/*
+ * Render one band on ctx's device, asynchronously on `stream` (hipStream_t; NULL = default).
+ *   rci          host pointer; rci->offset / rci->image_size / camera / spp / number as in the UBO.
+ *   rows         optional DEVICE array of band_height global row indices (strip tiling across
+ *                GPUs); NULL means rows rci->offset.y + [0, band_height).
+ *   accum_rgba32f / out_rgba8   DEVICE arrays of band_width * band_height texels, row-major by
+ *                band row (the reference's per-band storage images, bindings 3 and 0).
+ */
+int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t* rows,
+                     uint32_t band_width, uint32_t band_height, float* accum_rgba32f,
+                     uint8_t* out_rgba8, const rt_options* opt, void* stream);
+/* Statistics of the last completed rt_render_device (synchronises ctx's last stream). */
+int rt_get_stats(rt_context* ctx, rt_stats* out);
+/*
+ * Scatter band rows into a full image on the device: dst_row[rows[i]] = src_row[i]
+ * (the host-side reorder after the multi-GPU gather).
+ */
+int rt_scatter_rows(rt_context* ctx, const float* src_accum, const uint8_t* src_rgba8,
+                    const uint32_t* rows, uint32_t n_rows, uint32_t width, float* dst_accum,
+                    uint8_t* dst_rgba8, void* stream);
+
+/* ---- host-pointer convenience ------------------------------------------------------ */
+/*
+ * One frame over the full image rci[0].image_size with host buffers. rci_count bands, band i
+ * spanning rows [rci[i].offset.y, rci[i+1].offset.y) (last band to image height), band i on
+ * device i % device_count. accum_rgba32f: W*H*4 floats, out_rgba8: W*H*4 bytes (full image).
+ */
+int rt_render(const Sphere* spheres, uint32_t sphere_count, const RenderCallInfo* rci,
+              uint32_t rci_count, float* accum_rgba32f, uint8_t* out_rgba8,
+              const rt_options* opt, rt_stats* stats);
+
+/* Writes an rgba8 image as binary PPM (P6, alpha dropped). */
+int rt_store_ppm(const char* path, const uint8_t* rgba8, uint32_t width, uint32_t height);
+
+/* Diagnostic (tests only): evaluates one arithmetic-contract primitive on `device` for n
+ * (x, y) pairs: op 0 sqrt(x), 1 x/y, 2 sin(x), 3 fma(x,y,1), 4 normalize(x,y,0.5).x, 5 pow(x,5). */
+int rt_debug_math(int device, int op, const float* in_pairs, float* out, uint32_t n);
+
+/* src/ray_trace.h:9-15 — identical symbol and parameter list. Renders the canonical scene once
+ * (t = 0), prints the frame time, stores `render.ppm` when storeRenderResult, and returns. */
+void ray_trace(uint32_t samples, bool storeRenderResult, uint32_t width, uint32_t height,
+               uint32_t gpu_count);
+
+#ifdef __cplusplus
+}  /* extern "C" */
+#endif
+
+#endif /* RT_MI355X_H */

@@ -1,0 +1,562 @@
+// rt_api.cpp — host runtime behind the C-ABI (include/rt_mi355x.h).
+//
+// Replaces the reference's host orchestration for the hot path (src/ray_trace.cpp:42-972,
+// src/vulkan.h): device contexts instead of Vulkan devices, one HBM-resident scene + LBVH per
+// context instead of UBO + BLAS/TLAS, one fused persistent kernel launch per band instead of
+// clear + vkCmdTraceRaysKHR, and a headless ray_trace() that renders once and returns.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <exception>
+#include <memory>
+#include <random>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/rt_abi.h"
+#include "../../include/rt_mi355x.h"
+#include "rt_bvh.h"
+#include "rt_internal.h"
+
+namespace rt {
+hipError_t launch_trace(const TraceParams& P, uint32_t accel, bool count, int grid, hipStream_t st);
+hipError_t trace_occupancy(uint32_t accel, bool count, int* blocks_per_cu);
+hipError_t launch_scatter_rows(const float* src_acc, const uint8_t* src_px, const uint32_t* rows,
+                               uint32_t n_rows, uint32_t width, float* dst_acc, uint8_t* dst_px,
+                               hipStream_t st);
+hipError_t launch_debug_math(int op, const float* in, float* out, uint32_t n, hipStream_t st);
+}  // namespace rt
+
+struct rt_context {
+    int device = 0;
+    int cu_count = 0;
+    rt::DeviceScene scene;
+    std::vector<void*> scene_allocs;
+    rt::Counters* counters = nullptr;   // device
+    hipStream_t last_stream = nullptr;
+    int occ[2][2] = {{0, 0}, {0, 0}};   // [accel-1][count]
+};
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define RT_HIP(call)                                                                        \
+    do {                                                                                    \
+        hipError_t e_ = (call);                                                             \
+        if (e_ != hipSuccess)                                                               \
+            return fail(e_ == hipErrorOutOfMemory ? RT_ERR_OUT_OF_MEMORY : RT_ERR_DEVICE,   \
+                        std::string(#call) + ": " + hipGetErrorString(e_));                  \
+    } while (0)
+
+// RAII device selection: restores the caller's current device.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+void free_scene(rt_context* ctx) {
+    for (void* p : ctx->scene_allocs) (void)hipFree(p);
+    ctx->scene_allocs.clear();
+    ctx->scene = rt::DeviceScene{};
+}
+
+template <typename T>
+int upload(rt_context* ctx, const std::vector<T>& v, T** dst, hipStream_t st) {
+    *dst = nullptr;
+    if (v.empty()) return RT_OK;
+    void* p = nullptr;
+    RT_HIP(hipMalloc(&p, v.size() * sizeof(T)));
+    ctx->scene_allocs.push_back(p);
+    RT_HIP(hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st));
+    *dst = static_cast<T*>(p);
+    return RT_OK;
+}
+
+// ---- shader.rgen:29, 48-49, 92-105: camera + viewport, once per launch ------------------
+struct F3 { float x, y, z; };
+inline F3 f3(float x, float y, float z) { return F3{x, y, z}; }
+inline F3 operator+(F3 a, F3 b) { return f3(a.x + b.x, a.y + b.y, a.z + b.z); }
+inline F3 operator-(F3 a, F3 b) { return f3(a.x - b.x, a.y - b.y, a.z - b.z); }
+inline float dot3(F3 a, F3 b) { return std::fma(a.z, b.z, std::fma(a.y, b.y, a.x * b.x)); }
+inline F3 unit(F3 v) {
+    float len = std::sqrt(dot3(v, v));
+    float inv = 1.0f / len;
+    return f3(v.x * inv, v.y * inv, v.z * inv);
+}
+inline F3 cross3(F3 a, F3 b) {
+    return f3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+
+void fill_camera(const RenderCallInfo& rci, rt::TraceParams& P) {
+    const float fov = 25.0f, aperture = 0.0f, focus = 10.0f;  // shader.rgen:29
+    const F3 up = f3(0.0f, 1.0f, 0.0f);
+    const F3 from = f3(rci.camera_pos.x, rci.camera_pos.y, rci.camera_pos.z);
+    const F3 at = from + f3(rci.camera_dir.x, rci.camera_dir.y, rci.camera_dir.z);
+    const float sx = float(rci.image_size.x), sy = float(rci.image_size.y);
+    const float aspect = sx / sy;
+    const float half = (fov * 0.017453292519943295f) / 2.0f;
+    const float vh = float(std::tan(double(half))) * 2.0f;
+    const float vw = aspect * vh;
+    const F3 fwd = unit(at - from);
+    const F3 right = unit(cross3(up, fwd));
+    const F3 cup = unit(cross3(fwd, right));
+    const F3 hor = f3(vw * right.x * focus, vw * right.y * focus, vw * right.z * focus);
+    const F3 ver = f3(vh * cup.x * focus, vh * cup.y * focus, vh * cup.z * focus);
+    const F3 ulc = ((from - f3(hor.x / 2.0f, hor.y / 2.0f, hor.z / 2.0f)) +
+                    f3(ver.x / 2.0f, ver.y / 2.0f, ver.z / 2.0f)) +
+                   f3(fwd.x * focus, fwd.y * focus, fwd.z * focus);
+    auto put = [](float* d, F3 v) { d[0] = v.x; d[1] = v.y; d[2] = v.z; };
+    put(P.lf, from); put(P.hor, hor); put(P.ver, ver); put(P.ulc, ulc); put(P.cup, cup); put(P.crt, right);
+    P.half_aperture = aperture / 2.0f;
+    P.size_x = sx;
+    P.size_y = sy;
+}
+
+// ---- scene.h:37-157 -------------------------------------------------------------------------
+inline float uniform(std::mt19937& e, float lo, float hi) {
+    std::uniform_real_distribution<float> d(lo, hi);
+    return d(e);
+}
+rt_vec4 hsv_color(std::mt19937& e) {
+    const float h = std::floor(uniform(e, 0.0f, 360.0f));
+    const float s = 0.75f, v = 0.45f, C = s * v;
+    const float X = C * (1.0f - std::fabs(std::fmod(h / 60.0f, 2.0f) - 1.0f));
+    const float m = v - C;
+    float r, g, b;
+    if (h >= 0 && h < 60) { r = C; g = X; b = 0; }
+    else if (h >= 60 && h < 120) { r = X; g = C; b = 0; }
+    else if (h >= 120 && h < 180) { r = 0; g = C; b = X; }
+    else if (h >= 180 && h < 240) { r = 0; g = X; b = C; }
+    else if (h >= 240 && h < 300) { r = X; g = 0; b = C; }
+    else { r = C; g = 0; b = X; }
+    return rt_vec4{r + m, g + m, b + m, 1.0f};
+}
+Sphere make_sphere(rt_vec4 g, uint32_t mat, uint32_t tex, rt_vec4 c0, rt_vec4 c1, float attr) {
+    Sphere s;
+    std::memset(&s, 0, sizeof(s));
+    s.geometry = g;
+    s.materialType = mat;
+    s.textureType = tex;
+    s.colors[0] = c0;
+    s.colors[1] = c1;
+    s.materialSpecificAttribute = attr;
+    return s;
+}
+
+int current_device_count(int* n) {
+    hipError_t e = hipGetDeviceCount(n);
+    if (e != hipSuccess || *n <= 0) {
+        *n = 0;
+        return fail(RT_ERR_NO_DEVICE, "no HIP device visible");
+    }
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t rt_abi_version(void) { return RT_ABI_VERSION; }
+
+const char* rt_last_error(void) { return g_last_error.c_str(); }
+
+int rt_device_count(int* count) {
+    if (!count) return fail(RT_ERR_INVALID_ARGUMENT, "count is NULL");
+    return current_device_count(count);
+}
+
+int rt_generate_scene(float t, uint32_t K, Sphere* out, uint32_t capacity, uint32_t* count) {
+    const uint64_t need = 4ull + 4ull * K * K;
+    if (count) *count = uint32_t(need);
+    if (need > 0xffffffffull) return fail(RT_ERR_INVALID_ARGUMENT, "grid too large");
+    if (!out) return count ? RT_OK : fail(RT_ERR_INVALID_ARGUMENT, "out is NULL");
+    if (capacity < need) return fail(RT_ERR_INVALID_ARGUMENT, "capacity too small");
+    const rt_vec4 z = {0, 0, 0, 0};
+    // scene.h:85-116; cos of the float time argument in double, rounded to float.
+    out[0] = make_sphere({0.0f, -1000.0f, 1.0f, 1000.0f}, RT_DIFFUSE, RT_CHECKERED,
+                         {0.05f, 0.05f, 0.05f, 1.0f}, {0.95f, 0.95f, 0.95f, 1.0f}, 0.0f);
+    out[1] = make_sphere({-4.0f, 1.0f, float(std::cos(double(2 * t))), 1.0f}, RT_DIFFUSE, RT_SOLID,
+                         {0.6f, 0.3f, 0.1f, 1.0f}, z, 0.0f);
+    out[2] = make_sphere({4.0f, 1.0f, float(std::cos(double(3 * t))), 1.0f}, RT_METAL, RT_SOLID,
+                         {0.8f, 0.8f, 0.8f, 1.0f}, z, 0.0f);
+    out[3] = make_sphere({0.0f, 1.0f, float(std::cos(double(t))), 1.0f}, RT_REFRACTIVE, RT_SOLID,
+                         {1.0f, 1.0f, 1.0f, 1.0f}, z, 1.5f);
+    std::mt19937 e{};  // scene.h:120
+    uint32_t i = 4;
+    const int k = int(K);
+    for (int a = -k; a < k; a++) {
+        for (int b = -k; b < k; b++) {
+            // g++ (the reference's compiler) evaluates the vec4 arguments right to left:
+            // the z offset is drawn before the x offset (scene.h:124-125).
+            const float dz = uniform(e, 0.0f, 1.0f);
+            const float dx = uniform(e, 0.0f, 1.0f);
+            const rt_vec4 g = {float(a) + 0.9f * dx, 0.2f, float(b) + 0.9f * dz, 0.2f};
+            const float pm = uniform(e, 0.0f, 1.0f);
+            if (double(pm) < 0.7) {
+                out[i] = make_sphere(g, RT_DIFFUSE, RT_SOLID, hsv_color(e), z, 0.0f);
+            } else if (double(pm) < 0.85) {
+                const float cb = uniform(e, 0.5f, 1.0f);
+                const float cg = uniform(e, 0.5f, 1.0f);
+                const float cr = uniform(e, 0.5f, 1.0f);
+                out[i] = make_sphere(g, RT_METAL, RT_SOLID, {cr, cg, cb, 1.0f}, z, 0.0f);
+            } else {
+                out[i] = make_sphere(g, RT_REFRACTIVE, RT_SOLID, {1.0f, 1.0f, 1.0f, 1.0f}, z, 1.5f);
+            }
+            i++;
+        }
+    }
+    return RT_OK;
+}
+
+int rt_canonical_render_call_info(uint32_t spp, uint32_t width, uint32_t height, RenderCallInfo* out) {
+    if (!out) return fail(RT_ERR_INVALID_ARGUMENT, "out is NULL");
+    std::memset(out, 0, sizeof(*out));
+    out->number = 0;                                   // src/ray_trace.cpp:665
+    out->samplesPerRenderCall = spp;                   // :666
+    out->offset = rt_uvec2{0, 0};
+    out->image_size = rt_uvec2{width, height};         // :668
+    out->camera_pos = rt_vec4{13.0f, 11.0f, -3.0f, 0.0f};   // :669
+    out->camera_dir = rt_vec4{-13.0f, -11.0f, 3.0f, 0.0f};  // :670
+    return RT_OK;
+}
+
+int rt_context_create(int device, rt_context** out) {
+    if (!out) return fail(RT_ERR_INVALID_ARGUMENT, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    if (int rc = current_device_count(&n)) return rc;
+    if (device < 0 || device >= n) return fail(RT_ERR_INVALID_ARGUMENT, "device index out of range");
+    DeviceGuard g(device);
+    std::unique_ptr<rt_context> ctx(new rt_context());
+    ctx->device = device;
+    RT_HIP(hipDeviceGetAttribute(&ctx->cu_count, hipDeviceAttributeMultiprocessorCount, device));
+    void* c = nullptr;
+    RT_HIP(hipMalloc(&c, sizeof(rt::Counters)));
+    RT_HIP(hipMemset(c, 0, sizeof(rt::Counters)));
+    ctx->counters = static_cast<rt::Counters*>(c);
+    for (uint32_t acc = 1; acc <= 2; acc++)
+        for (int cnt = 0; cnt < 2; cnt++) {
+            int b = 0;
+            RT_HIP(rt::trace_occupancy(acc, cnt != 0, &b));
+            ctx->occ[acc - 1][cnt] = std::max(1, b);
+        }
+    *out = ctx.release();
+    return RT_OK;
+}
+
+int rt_context_destroy(rt_context* ctx) {
+    if (!ctx) return RT_OK;
+    DeviceGuard g(ctx->device);
+    (void)hipDeviceSynchronize();
+    free_scene(ctx);
+    if (ctx->counters) (void)hipFree(ctx->counters);
+    delete ctx;
+    return RT_OK;
+}
+
+int rt_set_scene(rt_context* ctx, const Sphere* spheres, uint32_t count, void* stream) {
+    if (!ctx) return fail(RT_ERR_INVALID_ARGUMENT, "ctx is NULL");
+    if (!spheres && count) return fail(RT_ERR_INVALID_ARGUMENT, "spheres is NULL");
+    if (count >= (1u << 27)) return fail(RT_ERR_INVALID_ARGUMENT, "too many spheres");
+    try {
+        DeviceGuard g(ctx->device);
+        hipStream_t st = static_cast<hipStream_t>(stream);
+        RT_HIP(hipStreamSynchronize(st));  // previous launches may still read the old scene
+        free_scene(ctx);
+        std::vector<rt::GeomRec> geom(count);
+        std::vector<float> radius(count);
+        std::vector<rt::MatRec> mat(count);
+        for (uint32_t i = 0; i < count; i++) {
+            const Sphere& s = spheres[i];
+            const float r = s.geometry.w;
+            geom[i] = rt::GeomRec{s.geometry.x, s.geometry.y, s.geometry.z, r * r};
+            radius[i] = r;
+            rt::MatRec m;
+            m.c0x = s.colors[0].x; m.c0y = s.colors[0].y; m.c0z = s.colors[0].z;
+            m.attr = s.materialSpecificAttribute;
+            m.c1x = s.colors[1].x; m.c1y = s.colors[1].y; m.c1z = s.colors[1].z;
+            m.type_tex = (s.materialType & 0xffu) | ((s.textureType & 0xffu) << 8);
+            mat[i] = m;
+        }
+        // Brute-force padding: whole batches of 8; the pad spheres sit 1e19 away with
+        // radius^2 = -1e38, so D = b^2 - a(|oc|^2 + 1e38) < 0 for every ray.
+        while (geom.size() % 8) geom.push_back(rt::GeomRec{0.0f, 1e19f, 0.0f, -1e38f});
+        rt::HostBvh bvh;
+        rt::build_lbvh_host(spheres, count, bvh);
+        rt::DeviceScene& d = ctx->scene;
+        d.n_spheres = count;
+        if (int rc = upload(ctx, geom, &d.geom, st)) return rc;
+        if (int rc = upload(ctx, radius, &d.radius, st)) return rc;
+        d.small_rmax = bvh.small_rmax;
+        if (int rc = upload(ctx, mat, &d.mat, st)) return rc;
+        d.n_big = uint32_t(bvh.big_ids.size());
+        if (int rc = upload(ctx, bvh.big_ids, &d.big_ids, st)) return rc;
+        d.n_nodes = uint32_t(bvh.nodes.size());
+        if (int rc = upload(ctx, bvh.nodes, &d.nodes, st)) return rc;
+        if (int rc = upload(ctx, bvh.leaf_geom, &d.leaf_geom, st)) return rc;
+        if (int rc = upload(ctx, bvh.leaf_ids, &d.leaf_ids, st)) return rc;
+        RT_HIP(hipStreamSynchronize(st));  // host vectors die at return
+        return RT_OK;
+    } catch (const std::exception& e) {
+        return fail(RT_ERR_OUT_OF_MEMORY, e.what());
+    }
+}
+
+int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t* rows,
+                     uint32_t band_width, uint32_t band_height, float* accum, uint8_t* out,
+                     const rt_options* opt, void* stream) {
+    if (!ctx || !rci) return fail(RT_ERR_INVALID_ARGUMENT, "ctx or rci is NULL");
+    if (!ctx->scene.geom && ctx->scene.n_spheres) return fail(RT_ERR_NO_SCENE, "no scene set");
+    if (band_width == 0 || band_height == 0) return RT_OK;
+    if (!accum || !out) return fail(RT_ERR_INVALID_ARGUMENT, "accum or out is NULL");
+    if (rci->image_size.x == 0 || rci->image_size.y == 0)
+        return fail(RT_ERR_INVALID_ARGUMENT, "image_size is zero");
+    const uint64_t tiles_x = (band_width + 7u) / 8u, tiles_y = (band_height + 7u) / 8u;
+    if (tiles_x * tiles_y * 64u >= (1ull << 32)) return fail(RT_ERR_INVALID_ARGUMENT, "band too large");
+    rt_options o;
+    std::memset(&o, 0, sizeof(o));
+    if (opt) o = *opt;
+    uint32_t accel = o.accel == RT_ACCEL_BRUTE ? rt::ACCEL_BRUTE : rt::ACCEL_LBVH;
+    if (o.accel > RT_ACCEL_LBVH) return fail(RT_ERR_INVALID_ARGUMENT, "unknown accel");
+    if (o.seed_mode > RT_SEED_LAUNCH_LOCAL) return fail(RT_ERR_INVALID_ARGUMENT, "unknown seed_mode");
+    if (o.rng_mode > RT_RNG_SAMPLE_COUNTER) return fail(RT_ERR_INVALID_ARGUMENT, "unknown rng_mode");
+    const bool count = (o.reserved[0] & 1u) != 0;  // internal: count box / sphere tests
+
+    rt::TraceParams P;
+    std::memset(&P, 0, sizeof(P));
+    fill_camera(*rci, P);
+    P.number = rci->number;
+    P.spp = rci->samplesPerRenderCall;
+    P.max_depth = o.max_depth ? o.max_depth : 50u;
+    P.seed_local = o.seed_mode == RT_SEED_LAUNCH_LOCAL;
+    P.rng_counter = o.rng_mode == RT_RNG_SAMPLE_COUNTER;
+    P.sample_base = o.sample_base;
+    P.accumulate = o.accumulate ? 1u : 0u;
+    P.off_x = rci->offset.x;
+    P.off_y = rci->offset.y;
+    P.band_w = band_width;
+    P.band_h = band_height;
+    P.tiles_x = uint32_t(tiles_x);
+    P.n_units = uint32_t(tiles_x * tiles_y * 64u);
+    P.rows = rows;
+    const rt::DeviceScene& d = ctx->scene;
+    P.n_spheres = d.n_spheres;
+    P.geom = d.geom;
+    P.radius = d.radius;
+    P.mat = d.mat;
+    P.n_big = d.n_big;
+    P.big_ids = d.big_ids;
+    P.nodes = d.n_nodes ? d.nodes : nullptr;
+    P.leaf_geom = d.leaf_geom;
+    P.leaf_ids = d.leaf_ids;
+    // Node-cull slack: a candidate's AABB entry lies at most
+    // 2.75 r + 1.15e-3 t beyond its reported t.
+    P.cull_abs = 3.0f * d.small_rmax + 1e-3f;
+    P.cull_rel = 2e-3f;
+    P.accum = accum;
+    P.out = reinterpret_cast<uint32_t*>(out);
+    P.counters = ctx->counters;
+
+    DeviceGuard g(ctx->device);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    RT_HIP(hipMemsetAsync(ctx->counters, 0, sizeof(rt::Counters), st));
+    const uint64_t lanes_needed = P.n_units;
+    const uint64_t full = uint64_t(ctx->cu_count) * ctx->occ[accel - 1][count ? 1 : 0];
+    const uint64_t by_work = (lanes_needed + 255u) / 256u;
+    const int grid = int(std::max<uint64_t>(1, std::min(full, by_work)));
+    RT_HIP(rt::launch_trace(P, accel, count, grid, st));
+    ctx->last_stream = st;
+    return RT_OK;
+}
+
+int rt_get_stats(rt_context* ctx, rt_stats* out) {
+    if (!ctx || !out) return fail(RT_ERR_INVALID_ARGUMENT, "ctx or out is NULL");
+    DeviceGuard g(ctx->device);
+    RT_HIP(hipStreamSynchronize(ctx->last_stream));
+    rt::Counters c;
+    RT_HIP(hipMemcpy(&c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
+    out->segments = c.segments;
+    out->samples = c.samples;
+    out->box_tests = c.box_tests;
+    out->sphere_tests = c.sphere_tests;
+    return RT_OK;
+}
+
+int rt_scatter_rows(rt_context* ctx, const float* src_accum, const uint8_t* src_rgba8,
+                    const uint32_t* rows, uint32_t n_rows, uint32_t width, float* dst_accum,
+                    uint8_t* dst_rgba8, void* stream) {
+    if (!ctx || !rows) return fail(RT_ERR_INVALID_ARGUMENT, "ctx or rows is NULL");
+    if ((dst_accum && !src_accum) || (dst_rgba8 && !src_rgba8))
+        return fail(RT_ERR_INVALID_ARGUMENT, "source missing for a destination");
+    DeviceGuard g(ctx->device);
+    RT_HIP(rt::launch_scatter_rows(src_accum, src_rgba8, rows, n_rows, width, dst_accum, dst_rgba8,
+                                   static_cast<hipStream_t>(stream)));
+    return RT_OK;
+}
+
+// Diagnostic export for the parity tests: evaluates a contract primitive on the device.
+int rt_debug_math(int device, int op, const float* in_pairs, float* out, uint32_t n) {
+    if (!in_pairs || !out) return fail(RT_ERR_INVALID_ARGUMENT, "NULL buffer");
+    int nd = 0;
+    if (int rc = current_device_count(&nd)) return rc;
+    DeviceGuard g(device);
+    float *din = nullptr, *dout = nullptr;
+    RT_HIP(hipMalloc(&din, size_t(n) * 2 * sizeof(float) + 16));
+    RT_HIP(hipMalloc(&dout, size_t(n) * sizeof(float) + 16));
+    RT_HIP(hipMemcpy(din, in_pairs, size_t(n) * 2 * sizeof(float), hipMemcpyHostToDevice));
+    RT_HIP(rt::launch_debug_math(op, din, dout, n, nullptr));
+    RT_HIP(hipMemcpy(out, dout, size_t(n) * sizeof(float), hipMemcpyDeviceToHost));
+    (void)hipFree(din);
+    (void)hipFree(dout);
+    return RT_OK;
+}
+
+int rt_render(const Sphere* spheres, uint32_t sphere_count, const RenderCallInfo* rci,
+              uint32_t rci_count, float* accum, uint8_t* out, const rt_options* opt,
+              rt_stats* stats) {
+    if (!rci || rci_count == 0) return fail(RT_ERR_INVALID_ARGUMENT, "no RenderCallInfo");
+    if (!accum || !out) return fail(RT_ERR_INVALID_ARGUMENT, "accum or out is NULL");
+    const uint32_t W = rci[0].image_size.x, H = rci[0].image_size.y;
+    if (W == 0 || H == 0) return fail(RT_ERR_INVALID_ARGUMENT, "image_size is zero");
+    for (uint32_t i = 0; i < rci_count; i++) {
+        const uint32_t y0 = rci[i].offset.y;
+        const uint32_t y1 = (i + 1 < rci_count) ? rci[i + 1].offset.y : H;
+        if (rci[i].image_size.x != W || rci[i].image_size.y != H || rci[i].offset.x != 0 || y1 < y0 || y1 > H)
+            return fail(RT_ERR_INVALID_ARGUMENT, "bands must tile the image top to bottom");
+    }
+    int nd = 0;
+    if (int rc = current_device_count(&nd)) return rc;
+    std::vector<int> rcs(rci_count, RT_OK);
+    std::vector<std::string> errs(rci_count);
+    std::vector<rt_stats> st(rci_count);
+    // One host thread per band, as the reference fans out per device (src/ray_trace.cpp:687).
+    auto band = [&](uint32_t i) {
+        const uint32_t y0 = rci[i].offset.y;
+        const uint32_t y1 = (i + 1 < rci_count) ? rci[i + 1].offset.y : H;
+        const uint32_t bh = y1 - y0;
+        std::memset(&st[i], 0, sizeof(rt_stats));
+        if (bh == 0) return;
+        rt_context* ctx = nullptr;
+        int rc = rt_context_create(int(i % uint32_t(nd)), &ctx);
+        float* dacc = nullptr;
+        uint8_t* dout = nullptr;
+        const size_t texels = size_t(W) * bh;
+        auto run = [&]() -> int {
+            if (rc) return rc;
+            DeviceGuard g(ctx->device);
+            if (int r = rt_set_scene(ctx, spheres, sphere_count, nullptr)) return r;
+            RT_HIP(hipMalloc(&dacc, texels * 16));
+            RT_HIP(hipMalloc(&dout, texels * 4));
+            float* hacc = accum + size_t(y0) * W * 4;
+            uint8_t* hout = out + size_t(y0) * W * 4;
+            if (opt && opt->accumulate) RT_HIP(hipMemcpy(dacc, hacc, texels * 16, hipMemcpyHostToDevice));
+            if (int r = rt_render_device(ctx, &rci[i], nullptr, W, bh, dacc, dout, opt, nullptr)) return r;
+            RT_HIP(hipMemcpy(hacc, dacc, texels * 16, hipMemcpyDeviceToHost));
+            RT_HIP(hipMemcpy(hout, dout, texels * 4, hipMemcpyDeviceToHost));
+            return rt_get_stats(ctx, &st[i]);
+        };
+        rcs[i] = run();
+        if (rcs[i]) errs[i] = g_last_error;
+        if (ctx) {
+            DeviceGuard g(ctx->device);
+            if (dacc) (void)hipFree(dacc);
+            if (dout) (void)hipFree(dout);
+        }
+        rt_context_destroy(ctx);
+    };
+    std::vector<std::thread> pool;
+    for (uint32_t i = 1; i < rci_count; i++) pool.emplace_back(band, i);
+    band(0);
+    for (auto& t : pool) t.join();
+    rt_stats total;
+    std::memset(&total, 0, sizeof(total));
+    for (uint32_t i = 0; i < rci_count; i++) {
+        if (rcs[i]) return fail(rcs[i], errs[i]);
+        total.segments += st[i].segments;
+        total.samples += st[i].samples;
+        total.box_tests += st[i].box_tests;
+        total.sphere_tests += st[i].sphere_tests;
+    }
+    if (stats) *stats = total;
+    return RT_OK;
+}
+
+int rt_store_ppm(const char* path, const uint8_t* rgba8, uint32_t width, uint32_t height) {
+    if (!path || !rgba8) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return fail(RT_ERR_IO, std::string("cannot open ") + path);
+    std::fprintf(f, "P6\n%u %u\n255\n", width, height);
+    std::vector<uint8_t> row(size_t(width) * 3);
+    bool ok = true;
+    for (uint32_t y = 0; y < height && ok; y++) {
+        for (uint32_t x = 0; x < width; x++)
+            for (int c = 0; c < 3; c++) row[size_t(x) * 3 + c] = rgba8[(size_t(y) * width + x) * 4 + c];
+        ok = std::fwrite(row.data(), 1, row.size(), f) == row.size();
+    }
+    ok = (std::fclose(f) == 0) && ok;
+    return ok ? RT_OK : fail(RT_ERR_IO, std::string("write failed: ") + path);
+}
+
+// src/ray_trace.h:9-15. Headless: one frame of the canonical scene (t = 0), split into
+// gpu_count row bands like src/ray_trace.cpp:74-93 (the first band takes the remainder).
+void ray_trace(uint32_t samples, bool storeRenderResult, uint32_t width, uint32_t height,
+               uint32_t gpu_count) {
+    try {
+        int nd = 0;
+        if (current_device_count(&nd)) {
+            std::fprintf(stderr, "ray_trace: %s\n", g_last_error.c_str());
+            return;
+        }
+        uint32_t n = std::max(1u, std::min(gpu_count, uint32_t(nd)));
+        n = std::min(n, std::max(1u, height));
+        std::vector<Sphere> scene(488);
+        uint32_t cnt = 0;
+        rt_generate_scene(0.0f, 11, scene.data(), uint32_t(scene.size()), &cnt);
+        std::vector<RenderCallInfo> rci(n);
+        const uint32_t base = height / n, rem = height % n;
+        uint32_t y = 0;
+        for (uint32_t i = 0; i < n; i++) {
+            rt_canonical_render_call_info(samples, width, height, &rci[i]);
+            rci[i].offset = rt_uvec2{0, y};
+            y += base + (i == 0 ? rem : 0);
+        }
+        std::vector<float> acc(size_t(width) * height * 4);
+        std::vector<uint8_t> img(size_t(width) * height * 4);
+        rt_stats st;
+        const auto t0 = std::chrono::steady_clock::now();
+        int rc = rt_render(scene.data(), cnt, rci.data(), n, acc.data(), img.data(), nullptr, &st);
+        const auto t1 = std::chrono::steady_clock::now();
+        if (rc) {
+            std::fprintf(stderr, "ray_trace: %s\n", g_last_error.c_str());
+            return;
+        }
+        const double sec = std::chrono::duration<double>(t1 - t0).count();
+        std::printf("duration_per_frame: %.3f ms (%u GPU, %llu samples, %.1f Msamples/s incl. setup)\n",
+                    sec * 1e3, n, (unsigned long long)st.samples, double(st.samples) / sec / 1e6);
+        if (storeRenderResult) {
+            if (rt_store_ppm("render.ppm", img.data(), width, height))
+                std::fprintf(stderr, "ray_trace: %s\n", g_last_error.c_str());
+        }
+    } catch (const std::exception& e) {
+        std::fprintf(stderr, "ray_trace: %s\n", e.what());
+    }
+}
+
+}  // extern "C"

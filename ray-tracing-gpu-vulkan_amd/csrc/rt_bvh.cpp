@@ -1,0 +1,157 @@
+// rt_bvh.cpp — LBVH over the scene's spheres (replaces the driver BLAS/TLAS built at
+// src/vulkan.h:395-554 from the per-sphere AABBs of src/ray_trace.cpp:583-599).
+//
+// Layout (rt_internal.h BvhNode): nodes in depth-first order with escape links, so the device
+// walk needs no stack: hit inner node -> index + 1, miss or leaf done -> escape.
+//
+// Construction (Karras-style binary radix tree over Morton codes):
+//   1. "big" spheres (radius > 2 x median radius; at most 64, largest first) are kept out of the
+//      tree and tested exhaustively: the reference ground sphere (r = 1000) would otherwise
+//      inflate every ancestor box up to the root.
+//   2. small-sphere centers quantised to 10 bits per axis inside their bounds, 30-bit Morton
+//      codes, stable sort by (code, index).
+//   3. recursive split at the highest differing Morton bit (the radix-tree split; equal codes
+//      split in the middle), leaves of at most kLeafMax spheres.
+//   4. node bounds = exact float min/max of the member spheres' AABBs (center -/+ radius), so
+//      every node box contains its spheres' AABBs bit-exactly (the traversal's exactness
+//      argument, DESIGN.md §4.3, needs this).
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <vector>
+
+#include "rt_bvh.h"
+
+namespace rt {
+
+namespace {
+
+constexpr uint32_t kLeafMax = 4;
+constexpr uint32_t kBigMax = 64;
+
+inline uint32_t expand_bits(uint32_t v) {  // 10 bits -> every third bit of 30
+    v = (v * 0x00010001u) & 0xFF0000FFu;
+    v = (v * 0x00000101u) & 0x0F00F00Fu;
+    v = (v * 0x00000011u) & 0xC30C30C3u;
+    v = (v * 0x00000005u) & 0x49249249u;
+    return v;
+}
+
+struct Prim {
+    uint32_t code;
+    uint32_t id;
+};
+
+struct Builder {
+    const Sphere* sph;
+    const std::vector<Prim>& prims;
+    HostBvh& out;
+
+    void bounds(uint32_t lo, uint32_t hi, float* bmin, float* bmax) const {
+        bmin[0] = bmin[1] = bmin[2] = INFINITY;
+        bmax[0] = bmax[1] = bmax[2] = -INFINITY;
+        for (uint32_t i = lo; i < hi; i++) {
+            const rt_vec4& g = sph[prims[i].id].geometry;
+            const float c[3] = {g.x, g.y, g.z};
+            for (int k = 0; k < 3; k++) {
+                bmin[k] = std::min(bmin[k], c[k] - g.w);
+                bmax[k] = std::max(bmax[k], c[k] + g.w);
+            }
+        }
+    }
+
+    uint32_t split(uint32_t lo, uint32_t hi) const {  // [lo, hi), hi - lo >= 2
+        const uint32_t a = prims[lo].code, b = prims[hi - 1].code;
+        if (a == b) return (lo + hi) / 2;
+        const int common = __builtin_clz(a ^ b);
+        uint32_t s = lo, step = hi - 1 - lo;
+        do {  // binary search for the last index sharing more than `common` prefix bits with a
+            step = (step + 1) >> 1;
+            const uint32_t ns = s + step;
+            if (ns < hi - 1 && __builtin_clz(a ^ prims[ns].code) > common) s = ns;
+        } while (step > 1);
+        return s + 1;
+    }
+
+    void build(uint32_t lo, uint32_t hi) {
+        const uint32_t me = uint32_t(out.nodes.size());
+        out.nodes.push_back(BvhNode{});
+        float bmin[3], bmax[3];
+        bounds(lo, hi, bmin, bmax);
+        BvhNode n;
+        n.lox = bmin[0]; n.loy = bmin[1]; n.loz = bmin[2];
+        n.hix = bmax[0]; n.hiy = bmax[1]; n.hiz = bmax[2];
+        if (hi - lo <= kLeafMax) {
+            const uint32_t first = uint32_t(out.leaf_geom.size());
+            for (uint32_t i = lo; i < hi; i++) {
+                const rt_vec4& g = sph[prims[i].id].geometry;
+                out.leaf_geom.push_back(GeomRec{g.x, g.y, g.z, g.w * g.w});
+                out.leaf_ids.push_back(prims[i].id);
+            }
+            n.first_count = (first << 4) | (hi - lo);
+        } else {
+            const uint32_t s = split(lo, hi);
+            build(lo, s);
+            build(s, hi);
+            n.first_count = 0;
+        }
+        n.escape = uint32_t(out.nodes.size());  // first node after this subtree
+        out.nodes[me] = n;
+    }
+};
+
+}  // namespace
+
+void build_lbvh_host(const Sphere* sph, uint32_t n, HostBvh& out) {
+    out = HostBvh{};
+    if (n == 0) return;
+    // 1. big spheres
+    std::vector<float> radii(n);
+    for (uint32_t i = 0; i < n; i++) radii[i] = sph[i].geometry.w;
+    std::vector<float> sorted = radii;
+    std::nth_element(sorted.begin(), sorted.begin() + n / 2, sorted.end());
+    const float median = sorted[n / 2];
+    std::vector<uint32_t> big;
+    for (uint32_t i = 0; i < n; i++)
+        if (radii[i] > 2.0f * median) big.push_back(i);
+    if (big.size() > kBigMax) {
+        std::stable_sort(big.begin(), big.end(), [&](uint32_t a, uint32_t b) { return radii[a] > radii[b]; });
+        big.resize(kBigMax);
+    }
+    std::sort(big.begin(), big.end());
+    out.big_ids = big;
+    std::vector<char> is_big(n, 0);
+    for (uint32_t i : big) is_big[i] = 1;
+    // 2. Morton codes of the small spheres
+    std::vector<Prim> prims;
+    prims.reserve(n - big.size());
+    float cmin[3] = {INFINITY, INFINITY, INFINITY}, cmax[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (uint32_t i = 0; i < n; i++) {
+        if (is_big[i]) continue;
+        const float c[3] = {sph[i].geometry.x, sph[i].geometry.y, sph[i].geometry.z};
+        for (int k = 0; k < 3; k++) { cmin[k] = std::min(cmin[k], c[k]); cmax[k] = std::max(cmax[k], c[k]); }
+        out.small_rmax = std::max(out.small_rmax, radii[i]);
+        prims.push_back(Prim{0, i});
+    }
+    if (prims.empty()) return;
+    for (Prim& p : prims) {
+        const float c[3] = {sph[p.id].geometry.x, sph[p.id].geometry.y, sph[p.id].geometry.z};
+        uint32_t q[3];
+        for (int k = 0; k < 3; k++) {
+            const float ext = cmax[k] - cmin[k];
+            float f = ext > 0.0f ? (c[k] - cmin[k]) / ext : 0.5f;
+            f = std::min(std::max(f, 0.0f), 1.0f);
+            q[k] = std::min(1023u, uint32_t(f * 1024.0f));
+        }
+        p.code = (expand_bits(q[0]) << 2) | (expand_bits(q[1]) << 1) | expand_bits(q[2]);
+    }
+    std::stable_sort(prims.begin(), prims.end(), [](const Prim& a, const Prim& b) { return a.code < b.code; });
+    // 3-4. hierarchy in depth-first order
+    out.nodes.reserve(2 * prims.size());
+    Builder b{sph, prims, out};
+    b.build(0, uint32_t(prims.size()));
+    for (BvhNode& nd : out.nodes)
+        if (nd.escape >= out.nodes.size()) nd.escape = 0xffffffffu;
+}
+
+}  // namespace rt

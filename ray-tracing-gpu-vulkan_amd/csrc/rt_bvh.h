@@ -1,0 +1,22 @@
+// rt_bvh.h — host-side LBVH build interface (rt_bvh.cpp).
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include "../../include/rt_abi.h"
+#include "rt_internal.h"
+
+namespace rt {
+
+struct HostBvh {
+    std::vector<uint32_t> big_ids;    // spheres tested exhaustively, ascending index
+    std::vector<BvhNode> nodes;       // depth-first, escape links
+    std::vector<GeomRec> leaf_geom;   // small spheres in leaf order
+    std::vector<uint32_t> leaf_ids;   // original index per leaf slot
+    float small_rmax = 0.0f;          // largest radius inside the tree (traversal slack)
+};
+
+void build_lbvh_host(const Sphere* spheres, uint32_t n, HostBvh& out);
+
+}  // namespace rt

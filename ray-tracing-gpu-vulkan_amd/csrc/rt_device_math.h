@@ -1,0 +1,108 @@
+// rt_device_math.h — device side of the arithmetic contract.
+//
+// Every operation here is an IEEE binary32 operation with one rounding (the library is built
+// with -ffp-contract=off; fmas are written out where the contract names them), so results are
+// bit-identical to the CPU oracle (oracle/rt_oracle.cpp), which implements the same contract
+// independently. Correctly rounded divide and sqrt are hipcc's defaults for f32 on gfx950
+// (-fhip-fp32-correctly-rounded-divide-sqrt); this file must never be built with -ffast-math.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rtd {
+
+struct V3 { float x, y, z; };
+
+__device__ __forceinline__ V3 v3(float x, float y, float z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 add(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 sub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 mul(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ V3 scale(float s, V3 a) { return v3(s * a.x, s * a.y, s * a.z); }
+__device__ __forceinline__ V3 neg(V3 a) { return v3(-a.x, -a.y, -a.z); }
+
+// dot(a,b) = fma(a.z,b.z, fma(a.y,b.y, a.x*b.x))
+__device__ __forceinline__ float dot(V3 a, V3 b) {
+    return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x));
+}
+// normalize(v) = v * (1 / sqrt(dot(v,v)))
+__device__ __forceinline__ V3 normalize(V3 v) {
+    float len = __builtin_sqrtf(dot(v, v));
+    float inv = 1.0f / len;
+    return v3(v.x * inv, v.y * inv, v.z * inv);
+}
+// GLSL reflect(I, N) = I - 2.0 * dot(N, I) * N
+__device__ __forceinline__ V3 reflect(V3 i, V3 n) {
+    float k = 2.0f * dot(n, i);
+    return sub(i, scale(k, n));
+}
+// GLSL refract(I, N, eta)
+__device__ __forceinline__ V3 refract(V3 i, V3 n, float eta) {
+    float d = dot(n, i);
+    float k = 1.0f - eta * eta * (1.0f - d * d);
+    if (k < 0.0f) return v3(0.0f, 0.0f, 0.0f);
+    float s = eta * d + __builtin_sqrtf(k);
+    return sub(scale(eta, i), scale(s, n));
+}
+
+// random.glsl:1-13 — 16-round TEA.
+__device__ __forceinline__ uint32_t tea(uint32_t v0, uint32_t v1) {
+    uint32_t s0 = 0;
+#pragma unroll
+    for (uint32_t n = 0; n < 16; n++) {
+        s0 += 0x9e3779b9u;
+        v0 += ((v1 << 4) + 0xa341316cu) ^ (v1 + s0) ^ ((v1 >> 5) + 0xc8013ea4u);
+        v1 += ((v0 << 4) + 0xad90777du) ^ (v0 + s0) ^ ((v0 >> 5) + 0x7e95761eu);
+    }
+    return v0;
+}
+// random.glsl:15-22 — LCG step and 24-bit float (exact: integer * 2^-24).
+__device__ __forceinline__ float rnd(uint32_t& seed) {
+    seed = 1664525u * seed + 1013904223u;
+    return float(seed & 0x00FFFFFFu) * (1.0f / 16777216.0f);
+}
+// random.glsl:24-34 with [min,max] = [-1,1]: r*2 - 1 (exact in binary32 for 24-bit r).
+__device__ __forceinline__ float rnd_pm1(uint32_t& seed) {
+    float r = rnd(seed);
+    return r * 2.0f + -1.0f;
+}
+__device__ __forceinline__ V3 random_unit_vector(uint32_t& seed) {
+    float x = rnd_pm1(seed);
+    float y = rnd_pm1(seed);
+    float z = rnd_pm1(seed);
+    return normalize(v3(x, y, z));
+}
+
+// sin for the checker texture (shader.rchit:59): 3-part Cody-Waite + fdlibm float kernels.
+__device__ __forceinline__ float sinf_det(float x) {
+    float k = __builtin_rintf(x * 0.636619772f);
+    float r = __builtin_fmaf(-k, 1.5707962513e+00f, x);
+    r = __builtin_fmaf(-k, 7.5497894159e-08f, r);
+    r = __builtin_fmaf(-k, 5.3903029534e-15f, r);
+    int q = int(k) & 3;
+    float r2 = r * r;
+    float ps = __builtin_fmaf(r2, -1.9515295891e-04f, 8.3321608736e-03f);
+    ps = __builtin_fmaf(r2, ps, -1.6666654611e-01f);
+    float s = __builtin_fmaf(r * r2, ps, r);
+    float pc = __builtin_fmaf(r2, 2.4433157118e-05f, -1.3887316255e-03f);
+    pc = __builtin_fmaf(r2, pc, 4.1666645683e-02f);
+    float r4 = r2 * r2;
+    float c = __builtin_fmaf(r4, pc, __builtin_fmaf(-0.5f, r2, 1.0f));
+    float v = (q & 1) ? c : s;
+    return (q & 2) ? -v : v;
+}
+
+// pow(x, 5.0) with GLSL's undefined negative base mapped to NaN.
+__device__ __forceinline__ float pow5(float x) {
+    float x2 = x * x;
+    float p = x2 * x2 * x;
+    return (x < 0.0f) ? __builtin_nanf("") : p;
+}
+
+// Vulkan UNORM8 store: clamp to [0,1] (NaN -> 0), round to nearest.
+__device__ __forceinline__ uint32_t unorm8(float x) {
+    float v = (x > 0.0f) ? ((x < 1.0f) ? x : 1.0f) : 0.0f;
+    return uint32_t(__builtin_fmaf(v, 255.0f, 0.5f));
+}
+
+}  // namespace rtd

@@ -1,0 +1,97 @@
+// rt_internal.h — device data layout and launch parameters shared by the HIP kernels
+// (rt_kernels.hip) and the host runtime (rt_api.cpp). Not part of the public C-ABI.
+#pragma once
+
+#include <stdint.h>
+
+namespace rt {
+
+// Per-sphere geometry record read by the closest-hit search (shader.rint:28-30):
+// center.xyz and radius^2 (rounded once, as shader.rint:48 computes radius * radius).
+struct alignas(16) GeomRec {
+    float cx, cy, cz, rr;
+};
+
+// Per-sphere material record read once per hit (shader.rchit:39): 32 B instead of the
+// reference's 80-B std140 Sphere, so one hit costs two 16-B loads.
+struct alignas(16) MatRec {
+    float c0x, c0y, c0z, attr;   // colors[0].rgb, materialSpecificAttribute
+    float c1x, c1y, c1z;         // colors[1].rgb (checker)
+    uint32_t type_tex;           // materialType | textureType << 8
+};
+
+// LBVH node, 32 B. Stackless "escape-link" layout: nodes are stored in depth-first order, so a
+// hit on an inner node continues at index+1 and a miss (or a finished leaf) jumps to `escape`.
+//   inner node: lo/hi = bounds of the subtree, count = 0
+//   leaf:       lo/hi = bounds, first = first slot in the leaf-sphere permutation, count >= 1
+struct alignas(16) BvhNode {
+    float lox, loy, loz;
+    uint32_t escape;             // next node index when the box is missed / leaf done; ~0u = end
+    float hix, hiy, hiz;
+    uint32_t first_count;        // leaf: first << 4 | count (count 1..15); inner: 0
+};
+
+// Scene as resident in HBM (one allocation per context, rebuilt by rt_set_scene).
+struct DeviceScene {
+    uint32_t n_spheres = 0;
+    GeomRec* geom = nullptr;       // n_spheres, original sphere order (brute force + shading)
+    float* radius = nullptr;       // n_spheres, for the AABB test (center -/+ radius)
+    MatRec* mat = nullptr;         // n_spheres
+    // LBVH over the "small" spheres; "big" spheres (radius above a scene-relative threshold,
+    // e.g. the ground sphere r = 1000) are tested exhaustively before the tree walk.
+    uint32_t n_big = 0;
+    uint32_t* big_ids = nullptr;   // n_big sphere indices, ascending
+    uint32_t n_nodes = 0;
+    BvhNode* nodes = nullptr;      // 2 * n_leaf_spheres - 1 at most
+    GeomRec* leaf_geom = nullptr;  // spheres permuted into leaf order (contiguous per leaf)
+    uint32_t* leaf_ids = nullptr;  // original index of each leaf slot
+    float small_rmax = 0.0f;       // largest radius in the tree
+};
+
+enum : uint32_t { ACCEL_BRUTE = 1, ACCEL_LBVH = 2 };
+
+// Counters block (device memory, zeroed before each launch by the host).
+struct Counters {
+    uint32_t work_head;            // next unit (pixel) to hand out
+    uint32_t _pad;
+    unsigned long long segments;
+    unsigned long long samples;
+    unsigned long long box_tests;
+    unsigned long long sphere_tests;
+};
+
+// Kernel launch parameters (passed by value as the kernel argument).
+struct TraceParams {
+    // Camera / viewport (shader.rgen:92-115), computed once per launch on the host.
+    float lf[3], hor[3], ver[3], ulc[3], cup[3], crt[3];
+    float half_aperture;
+    float size_x, size_y;          // full image size as float (shader.rgen:42)
+    uint32_t number, spp, max_depth;
+    uint32_t seed_local;           // 1: seed from launch-local ids (shader.rgen:40 verbatim)
+    uint32_t rng_counter;          // 1: RT_RNG_SAMPLE_COUNTER
+    uint32_t sample_base;
+    uint32_t accumulate;
+    uint32_t off_x, off_y;         // band offset (rows == nullptr)
+    uint32_t band_w, band_h;
+    uint32_t tiles_x;              // ceil(band_w / 8)
+    uint32_t n_units;              // tiles_x * ceil(band_h / 8) * 64
+    const uint32_t* rows;          // optional global row per band row
+    // scene
+    uint32_t n_spheres;
+    const GeomRec* geom;
+    const float* radius;
+    const MatRec* mat;
+    uint32_t n_big;
+    const uint32_t* big_ids;
+    const BvhNode* nodes;
+    const GeomRec* leaf_geom;
+    const uint32_t* leaf_ids;
+    float cull_abs;                // LBVH node-cull slack: best + cull_abs + cull_rel * best
+    float cull_rel;
+    // outputs
+    float* accum;                  // band_w * band_h * 4 floats
+    uint32_t* out;                 // band_w * band_h packed rgba8
+    Counters* counters;
+};
+
+}  // namespace rt

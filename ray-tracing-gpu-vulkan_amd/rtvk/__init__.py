@@ -1,0 +1,192 @@
+"""rtvk — host-side mirror of the reference's hot-path API over librt_mi355x.so.
+
+Names follow the reference:
+  generateRandomScene(t)           src/scene.h:79-157 (t explicit instead of the wall clock)
+  RenderCallInfo / Sphere / Scene  src/render_call_info.h:5-13, src/scene.h:16-29
+  ray_trace(samples, storeRenderResult, width, height, gpu_count)
+                                   src/ray_trace.h:9-15 (headless; renders once and returns)
+and the per-frame device work of src/ray_trace.cpp:567-739 is ``Renderer.render_device``.
+
+Everything computes in the HIP library; this module only marshals arguments. Device buffers are
+torch tensors (memory + stream plumbing only).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Iterable, Optional, Sequence
+
+import numpy as np
+
+from . import abi
+from .abi import (CHECKERED, DIFFUSE, METAL, REFRACTIVE, SOLID, Options, RenderCallInfo, RtError,
+                  Scene, Sphere, Stats, check, load_library)
+
+__all__ = [
+    "DIFFUSE", "METAL", "REFRACTIVE", "SOLID", "CHECKERED", "Sphere", "Scene", "RenderCallInfo",
+    "Options", "Stats", "RtError", "generateRandomScene", "canonical_render_call_info",
+    "make_options", "Renderer", "render", "ray_trace", "store_ppm", "spheres_to_numpy",
+    "load_library",
+]
+
+MAX_DEPTH = 50  # shader.rgen:27
+
+
+def generateRandomScene(t: float = 0.0, grid_half_extent: int = 11):
+    """src/scene.h:79-157: ground + 3 big spheres + (2K)^2 grid; K = 11 gives the 488-sphere scene.
+
+    Returns a ctypes array of ``Sphere`` (length 4 + 4K^2)."""
+    lib = load_library()
+    n = ctypes.c_uint32()
+    check(lib.rt_generate_scene(ctypes.c_float(t), grid_half_extent, None, 0, ctypes.byref(n)))
+    arr = (Sphere * n.value)()
+    check(lib.rt_generate_scene(ctypes.c_float(t), grid_half_extent, ctypes.addressof(arr), n.value,
+                                ctypes.byref(n)))
+    return arr
+
+
+def spheres_to_numpy(spheres) -> np.ndarray:
+    """Raw 80-byte records as a (n, 80) uint8 array (for hashing / fixtures)."""
+    return np.frombuffer(bytes(spheres), dtype=np.uint8).reshape(-1, 80)
+
+
+def canonical_render_call_info(spp: int, width: int = 1920, height: int = 1080) -> RenderCallInfo:
+    """The RenderCallInfo the reference fills every frame (src/ray_trace.cpp:660-676)."""
+    rci = RenderCallInfo()
+    check(load_library().rt_canonical_render_call_info(spp, width, height, ctypes.byref(rci)))
+    return rci
+
+
+def make_options(max_depth: int = MAX_DEPTH, seed_mode: int = abi.RT_SEED_GLOBAL,
+                 rng_mode: int = abi.RT_RNG_PIXEL_STREAM, accel: int = abi.RT_ACCEL_AUTO,
+                 accumulate: bool = False, sample_base: int = 0, count_tests: bool = False) -> Options:
+    o = Options()
+    o.max_depth, o.seed_mode, o.rng_mode, o.accel = max_depth, seed_mode, rng_mode, accel
+    o.accumulate, o.sample_base = int(bool(accumulate)), sample_base
+    o.reserved[0] = 1 if count_tests else 0
+    return o
+
+
+def _stream_ptr(stream) -> Optional[int]:
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    return getattr(stream, "cuda_stream", stream)
+
+
+def _check_dev_tensor(t, dtype_name: str, shape: Sequence[int]):
+    import torch
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise TypeError("expected a device (cuda) torch.Tensor")
+    if str(t.dtype) != dtype_name or not t.is_contiguous() or tuple(t.shape) != tuple(shape):
+        raise ValueError(f"expected contiguous {dtype_name} tensor of shape {tuple(shape)}, "
+                         f"got {t.dtype} {tuple(t.shape)}")
+
+
+class Renderer:
+    """One device context: HBM-resident scene + LBVH, and the fused trace kernel.
+
+    Replaces, per GPU, the reference's descriptor set / BLAS / TLAS / pipeline
+    (src/ray_trace.cpp:315-527) and its per-frame command buffer (src/vulkan.h:998-1204)."""
+
+    def __init__(self, device: int = 0):
+        self._lib = load_library()
+        self._ctx = ctypes.c_void_p()
+        check(self._lib.rt_context_create(device, ctypes.byref(self._ctx)))
+        self.device = device
+        self.sphere_count = 0
+
+    def close(self) -> None:
+        if self._ctx:
+            self._lib.rt_context_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_scene(self, spheres, stream=None) -> None:
+        """Upload spheres (ctypes Sphere array or (n,80) uint8 records) and build the LBVH."""
+        buf = spheres if not isinstance(spheres, np.ndarray) else np.ascontiguousarray(spheres, np.uint8)
+        n = len(spheres)
+        ptr = ctypes.addressof(buf) if not isinstance(buf, np.ndarray) else buf.ctypes.data
+        st = 0 if stream is None else _stream_ptr(stream)
+        check(self._lib.rt_set_scene(self._ctx, ptr if n else None, n, st))
+        self.sphere_count = n
+
+    def render_device(self, rci: RenderCallInfo, accum, out, rows=None,
+                      options: Optional[Options] = None, stream=None) -> None:
+        """One band on this device, asynchronous on `stream` (torch current stream by default).
+
+        accum: float32 cuda tensor [band_h, band_w, 4]; out: uint8 cuda tensor [band_h, band_w, 4];
+        rows: optional int32/uint32 cuda tensor [band_h] of global row indices (strip tiling)."""
+        bh, bw = int(accum.shape[0]), int(accum.shape[1])
+        _check_dev_tensor(accum, "torch.float32", (bh, bw, 4))
+        _check_dev_tensor(out, "torch.uint8", (bh, bw, 4))
+        rows_ptr = None
+        if rows is not None:
+            if rows.numel() != bh or not rows.is_cuda or rows.element_size() != 4 or not rows.is_contiguous():
+                raise ValueError("rows must be a contiguous 4-byte cuda tensor of band_h entries")
+            rows_ptr = rows.data_ptr()
+        check(self._lib.rt_render_device(self._ctx, ctypes.byref(rci), rows_ptr, bw, bh,
+                                         accum.data_ptr(), out.data_ptr(),
+                                         ctypes.byref(options) if options is not None else None,
+                                         _stream_ptr(stream)))
+
+    def stats(self) -> Stats:
+        st = Stats()
+        check(self._lib.rt_get_stats(self._ctx, ctypes.byref(st)))
+        return st
+
+    def scatter_rows(self, src_accum, src_rgba8, rows, dst_accum, dst_rgba8, stream=None) -> None:
+        """dst[rows[i]] = src[i] (device), the reorder after a multi-GPU gather."""
+        n, w = int(src_rgba8.shape[0]), int(src_rgba8.shape[1])
+        check(self._lib.rt_scatter_rows(self._ctx, src_accum.data_ptr() if src_accum is not None else None,
+                                        src_rgba8.data_ptr(), rows.data_ptr(), n, w,
+                                        dst_accum.data_ptr() if dst_accum is not None else None,
+                                        dst_rgba8.data_ptr(), _stream_ptr(stream)))
+
+
+@dataclass
+class RenderResult:
+    accum: np.ndarray   # float32 [H, W, 4] — the rgba32f sum image (binding 3)
+    rgba8: np.ndarray   # uint8   [H, W, 4] — the tonemapped image (binding 0)
+    stats: Stats
+
+
+def render(spheres, rci: RenderCallInfo | Sequence[RenderCallInfo], options: Optional[Options] = None,
+           accum: Optional[np.ndarray] = None) -> RenderResult:
+    """Host-buffer frame (rt_render): one band per RenderCallInfo, band i on device i % ndev."""
+    lib = load_library()
+    rcis = [rci] if isinstance(rci, RenderCallInfo) else list(rci)
+    arr = (RenderCallInfo * len(rcis))(*rcis)
+    W, H = rcis[0].image_size.x, rcis[0].image_size.y
+    acc = np.zeros((H, W, 4), np.float32) if accum is None else np.ascontiguousarray(accum, np.float32)
+    out = np.zeros((H, W, 4), np.uint8)
+    st = Stats()
+    sp = spheres if not isinstance(spheres, np.ndarray) else np.ascontiguousarray(spheres, np.uint8)
+    sptr = ctypes.addressof(sp) if not isinstance(sp, np.ndarray) else sp.ctypes.data
+    check(lib.rt_render(sptr, len(spheres), ctypes.addressof(arr), len(rcis), acc.ctypes.data,
+                        out.ctypes.data, ctypes.byref(options) if options is not None else None,
+                        ctypes.byref(st)))
+    return RenderResult(acc, out, st)
+
+
+def store_ppm(path: str, rgba8: np.ndarray) -> None:
+    h, w = rgba8.shape[:2]
+    img = np.ascontiguousarray(rgba8, np.uint8)
+    check(load_library().rt_store_ppm(str(path).encode(), img.ctypes.data, w, h))
+
+
+def ray_trace(samples: int = 10, storeRenderResult: bool = False, width: int = 1920,
+              height: int = 1080, gpu_count: int = 1) -> None:
+    """src/ray_trace.h:9-15, same parameters and defaults (the C symbol, called through ctypes)."""
+    load_library().ray_trace(samples, storeRenderResult, width, height, gpu_count)

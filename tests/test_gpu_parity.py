@@ -1,0 +1,228 @@
+"""GPU parity: librt_mi355x.so (through its C-ABI) against the CPU oracle on the same inputs.
+
+Bar: bit-exact. Both sides implement the arithmetic contract of DESIGN.md §3 (IEEE binary32,
+explicit fmas, correctly rounded divide/sqrt, deterministic sin), so every accumulator float and
+every rgba8 byte must be identical, and the traced-segment counts must agree. Full-size cases
+use size-independent properties (LBVH == brute force, band-split invariance) plus one full-frame
+oracle comparison at 1 spp.
+"""
+import ctypes
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLDEN = Path(__file__).resolve().parent / "golden"
+BRUTE, LBVH = 1, 2
+
+
+@pytest.fixture(scope="module")
+def torch():
+    import torch as t
+    if not t.cuda.is_available():
+        pytest.skip("no GPU")
+    return t
+
+
+@pytest.fixture(scope="module")
+def rtvk(torch):
+    import rtvk as m
+    return m
+
+
+@pytest.fixture(scope="module")
+def renderer(rtvk):
+    r = rtvk.Renderer(0)
+    yield r
+    r.close()
+
+
+def gpu_render(rtvk, renderer, torch, spheres, rci_u32, band_w, band_h, rows=None, accel=LBVH,
+               max_depth=50, seed_mode=0, rng_mode=0, accumulate=False, sample_base=0, accum=None,
+               count=False):
+    renderer.set_scene(np.ascontiguousarray(spheres, np.uint8).reshape(-1, 80))
+    rci = rtvk.RenderCallInfo.from_buffer_copy(np.ascontiguousarray(rci_u32).tobytes())
+    acc = (torch.zeros((band_h, band_w, 4), dtype=torch.float32, device="cuda") if accum is None
+           else torch.from_numpy(np.ascontiguousarray(accum, np.float32)).cuda())
+    out = torch.full((band_h, band_w, 4), 7, dtype=torch.uint8, device="cuda")
+    rows_t = None if rows is None else torch.from_numpy(np.asarray(rows, np.int32)).cuda()
+    opt = rtvk.make_options(max_depth=max_depth, seed_mode=seed_mode, rng_mode=rng_mode, accel=accel,
+                            accumulate=accumulate, sample_base=sample_base, count_tests=count)
+    renderer.render_device(rci, acc, out, rows=rows_t, options=opt)
+    torch.cuda.synchronize()
+    st = renderer.stats()
+    return acc.cpu().numpy(), out.cpu().numpy(), st
+
+
+def assert_same(a_gpu, o_gpu, a_ref, o_ref):
+    diff = np.argwhere(a_gpu != a_ref)
+    assert diff.size == 0, f"{len(diff)} accumulator floats differ, first at {diff[:4].tolist()}"
+    np.testing.assert_array_equal(o_gpu, o_ref)
+
+
+# ---- primitives -------------------------------------------------------------------------------
+@pytest.mark.parametrize("op", [0, 1, 2, 3, 4, 5])
+def test_math_primitives_bit_exact(rtvk, torch, oracle, op):
+    rng = np.random.default_rng(op)
+    n = 20000
+    if op == 0:
+        x = np.abs(rng.standard_normal(n)).astype(np.float32) * np.float32(10) ** rng.integers(-20, 20, n).astype(np.float32)
+        y = np.zeros(n, np.float32)
+        ref = np.sqrt(x)
+    elif op == 1:
+        x = rng.standard_normal(n).astype(np.float32) * 1e3
+        y = rng.standard_normal(n).astype(np.float32)
+        ref = x / y
+    elif op == 2:
+        x = np.concatenate([rng.uniform(-100, 100, n // 2), rng.uniform(-6e4, 6e4, n // 2)]).astype(np.float32)
+        y = np.zeros(n, np.float32)
+        ref = np.array([oracle.sinf(float(v)) for v in x], np.float32)
+    elif op == 3:
+        x = rng.standard_normal(n).astype(np.float32)
+        y = rng.standard_normal(n).astype(np.float32)
+        ref = (x.astype(np.float64) * y.astype(np.float64) + 1.0).astype(np.float32)  # exact fma for f32
+    elif op == 4:  # normalize(v) = v * (1 / sqrt(fma(z,z, fma(y,y, x*x)))), v = (x, y, 0.5)
+        x = rng.standard_normal(n).astype(np.float32)
+        y = rng.standard_normal(n).astype(np.float32)
+        xx = x * x
+        d = (y.astype(np.float64) * y + xx).astype(np.float32)   # fma: exact product, one rounding
+        d = (np.float64(0.25) + d).astype(np.float32)             # fma(0.5, 0.5, d)
+        inv = np.float32(1) / np.sqrt(d)
+        ref = x * inv
+    else:
+        x = rng.uniform(-0.5, 1.5, n).astype(np.float32)
+        y = np.zeros(n, np.float32)
+        x2 = x * x
+        ref = np.where(x < 0, np.float32(np.nan), x2 * x2 * x).astype(np.float32)
+    pairs = np.ascontiguousarray(np.stack([x, y], 1), np.float32)
+    out = np.zeros(n, np.float32)
+    from rtvk import abi
+    abi.check(rtvk.load_library().rt_debug_math(0, op, pairs.ctypes.data, out.ctypes.data, n))
+    same = (out.view(np.uint32) == ref.astype(np.float32).view(np.uint32)) | (np.isnan(out) & np.isnan(ref))
+    assert same.all(), f"op {op}: {np.count_nonzero(~same)} differ, e.g. x={x[~same][:3]} gpu={out[~same][:3]} ref={ref[~same][:3]}"
+
+
+# ---- golden fixtures --------------------------------------------------------------------------
+@pytest.mark.parametrize("accel", [BRUTE, LBVH])
+@pytest.mark.parametrize("case", ["g64x36_spp4", "g48x32_spp3_depth3_local", "g40x24_spp2_counter"])
+def test_golden(rtvk, renderer, torch, oracle, case, accel):
+    m = json.loads((GOLDEN / f"{case}.json").read_text())
+    g = np.load(GOLDEN / f"{case}.npz", allow_pickle=False)
+    sc = oracle.generate_scene(m["t"], m["K"])
+    rci = oracle.render_call_info(m["spp"], m["W"], m["H"], tuple(m["offset"]))
+    a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, m["band_w"], m["band_h"], accel=accel,
+                          max_depth=m["max_depth"], seed_mode=m["seed_mode"], rng_mode=m["rng_mode"])
+    assert_same(a, o, g["accum"], g["rgba8"])
+    assert st.segments == int(g["stats"][0]) and st.samples == int(g["stats"][1])
+
+
+# ---- oracle at the same seed ------------------------------------------------------------------
+CASES = [
+    # (W, H, offset_y, band_h, spp, t, K, kwargs)
+    (96, 54, 0, 54, 6, 0.0, 11, {}),
+    (13, 7, 0, 7, 5, 0.0, 11, {}),            # ragged tiles
+    (1, 1, 0, 1, 9, 0.0, 11, {}),             # single pixel
+    (70, 40, 17, 9, 3, 0.9, 11, {}),          # band with offset, moving spheres
+    (64, 36, 0, 36, 4, 0.0, 3, {}),           # small grid
+    (50, 30, 0, 30, 3, 0.0, 11, {"max_depth": 2}),
+    (50, 30, 5, 20, 3, 0.0, 11, {"seed_mode": 1}),
+]
+
+
+@pytest.mark.parametrize("accel", [BRUTE, LBVH])
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_vs_oracle(rtvk, renderer, torch, oracle, case, accel):
+    W, H, oy, bh, spp, t, K, kw = CASES[case]
+    sc = oracle.generate_scene(t, K)
+    rci = oracle.render_call_info(spp, W, H, (0, oy))
+    ra, ro, rst = oracle.render(sc, rci, W, bh, opts=oracle.options(**kw))
+    a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, bh, accel=accel, **kw)
+    assert_same(a, o, ra, ro)
+    assert (st.segments, st.samples) == rst[:2]
+
+
+def test_empty_and_single_sphere(rtvk, renderer, torch, oracle):
+    rci = oracle.render_call_info(2, 20, 10)
+    for sc in (np.zeros((0, 80), np.uint8), oracle.generate_scene()[:1], oracle.generate_scene()[3:4]):
+        ra, ro, _ = oracle.render(sc, rci, 20, 10)
+        for accel in (BRUTE, LBVH):
+            a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, 20, 10, accel=accel)
+            assert_same(a, o, ra, ro)
+
+
+def test_rows_strip_map(rtvk, renderer, torch, oracle):
+    W, H = 40, 30
+    sc = oracle.generate_scene()
+    rci = oracle.render_call_info(3, W, H)
+    fa, fo, _ = oracle.render(sc, rci, W, H)
+    rows = np.array([29, 0, 8, 9, 10, 15], np.int32)
+    a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, len(rows), rows=rows)
+    assert_same(a, o, fa[rows], fo[rows])
+
+
+def test_accumulate_and_counter_rng(rtvk, renderer, torch, oracle):
+    W, H = 24, 16
+    sc = oracle.generate_scene()
+    rci = oracle.render_call_info(2, W, H)
+    base, _, _ = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=1))
+    ra, ro, _ = oracle.render(sc, rci, W, H, accum=base, opts=oracle.options(rng_mode=1, accumulate=1, sample_base=2))
+    a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accum=base, rng_mode=1, accumulate=True, sample_base=2)
+    assert_same(a, o, ra, ro)
+
+
+def test_host_rt_render_bands(rtvk, oracle):
+    """rt_render with 3 bands (one per GPU in the reference; here all on the visible devices)."""
+    W, H = 32, 20
+    sc = oracle.generate_scene()
+    rcis = [rtvk.canonical_render_call_info(2, W, H) for _ in range(3)]
+    for r, y in zip(rcis, (0, 7, 13)):
+        r.offset.y = y
+    res = rtvk.render(rtvk.generateRandomScene(), rcis)
+    ra, ro, _ = oracle.render(sc, oracle.render_call_info(2, W, H), W, H)
+    assert_same(res.accum, res.rgba8, ra, ro)
+
+
+# ---- full size --------------------------------------------------------------------------------
+def test_full_frame_1spp_vs_oracle(rtvk, renderer, torch, oracle):
+    """Config 1 frame (1920x1080, 1 spp) against the oracle: bit-exact => PSNR = inf >= 50 dB."""
+    sc = oracle.generate_scene()
+    rci = oracle.render_call_info(1, 1920, 1080)
+    ra, ro, rst = oracle.render(sc, rci, 1920, 1080, threads=16)
+    a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, 1920, 1080, accel=LBVH)
+    n_diff = int(np.count_nonzero(np.any(a != ra, axis=-1)))
+    mse = np.mean((o[..., :3].astype(np.float64) - ro[..., :3]) ** 2)
+    psnr = float("inf") if mse == 0 else 10 * np.log10(255 ** 2 / mse)
+    assert psnr >= 50.0
+    assert n_diff == 0, f"{n_diff} pixels differ (PSNR {psnr:.1f} dB)"
+    assert (st.segments, st.samples) == rst[:2]
+
+
+@pytest.mark.parametrize("W,H,spp,K", [(1920, 1080, 2, 11), (3840, 2160, 1, 11), (256, 144, 1, 158)])
+def test_lbvh_equals_brute_full_size(rtvk, renderer, torch, oracle, W, H, spp, K):
+    sc = oracle.generate_scene(0.0, K)
+    rci = oracle.render_call_info(spp, W, H)
+    ab, ob, sb = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=BRUTE)
+    al, ol, sl = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH)
+    assert_same(al, ol, ab, ob)
+    assert sb.segments == sl.segments
+
+
+def test_band_split_invariance_full_size(rtvk, renderer, torch, oracle):
+    sc = oracle.generate_scene()
+    W, H = 1920, 1080
+    rci = oracle.render_call_info(1, W, H)
+    fa, fo, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H)
+    rows = np.arange(H, dtype=np.int32).reshape(-1, 8)[1::3].reshape(-1)   # every third 8-row strip
+    a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, len(rows), rows=rows)
+    assert_same(a, o, fa[rows], fo[rows])
+
+
+def test_count_variant_same_image(rtvk, renderer, torch, oracle):
+    sc = oracle.generate_scene()
+    rci = oracle.render_call_info(2, 128, 72)
+    a0, o0, s0 = gpu_render(rtvk, renderer, torch, sc, rci, 128, 72, accel=LBVH)
+    a1, o1, s1 = gpu_render(rtvk, renderer, torch, sc, rci, 128, 72, accel=LBVH, count=True)
+    assert_same(a1, o1, a0, o0)
+    assert s1.box_tests > 0 and s1.sphere_tests > 0 and s0.box_tests == 0

@@ -1,0 +1,163 @@
+"""The CPU oracle against every pin the reference offers and against the
+committed golden fixtures (tests/golden/, made by tests/golden/make_golden.py)."""
+import math
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+GOLDEN = Path(__file__).resolve().parent / "golden"
+
+# SURVEY.md §4 pin 1: random.glsl restated in C and Python during the survey.
+RNG_KNOWN = [((0, 0), 0xC9A6502E, 0.317775071), ((1, 0), 0x469EAABE, 0.0754855275),
+             ((0, 1), 0x641949FF, 0.102772832), ((959, 539), 0x84C2F065, 0.978126526),
+             ((1919, 1079), 0xBB27E01B, 0.387065768)]
+
+
+@pytest.mark.parametrize("xy,seed,first", RNG_KNOWN)
+def test_rng_known_answers(oracle, xy, seed, first):
+    s = oracle.pixel_seed(*xy, 0)
+    assert s == seed
+    assert oracle.random_floats(s, 1)[0] == pytest.approx(first, abs=5e-10)
+
+
+def test_lcg_and_float_exact(oracle):
+    # random.glsl:15-22: seed = 1664525 * seed + 1013904223; float(seed & 0xFFFFFF) / 2^24
+    s = 0x12345678
+    fl = oracle.random_floats(s, 4)
+    for f in fl:
+        s = (1664525 * s + 1013904223) & 0xFFFFFFFF
+        assert f == (s & 0xFFFFFF) / 16777216.0
+
+
+def _f(a, lo, hi):
+    return a[lo:hi].copy().view(np.float32)
+
+
+def test_scene_reference_pins(oracle):
+    """SURVEY.md §4 pin 2 (from the reference's own scene.h compiled by g++ 11.4)."""
+    sc = oracle.generate_scene(0.0)
+    assert sc.shape == (488, 80)
+    mat = sc[:, 16:20].copy().view(np.uint32).ravel()
+    assert np.bincount(mat, minlength=3).tolist() == [360, 70, 58]
+    np.testing.assert_array_equal(_f(sc[4], 0, 16), np.float32([-10.878071, 0.2, -10.266748, 0.2]))
+    assert mat[4] == 2
+    assert mat[6] == 0
+    np.testing.assert_allclose(_f(sc[6], 32, 44), [0.168750, 0.450000, 0.112500], atol=1e-6)
+    np.testing.assert_array_equal(_f(sc[487], 0, 16),
+                                  np.float32([10.1279688, 0.200000003, 10.8928413, 0.200000003]))
+    assert mat[487] == 0
+    np.testing.assert_array_equal(_f(sc[487], 32, 48),
+                                  np.float32([0.449999988, 0.163125008, 0.112500012, 1.0]))
+    # fixed spheres, scene.h:85-116 at t = 0 (cos 0 = 1)
+    np.testing.assert_array_equal(_f(sc[0], 0, 16), np.float32([0, -1000, 1, 1000]))
+    for i, x in ((1, -4.0), (2, 4.0), (3, 0.0)):
+        np.testing.assert_array_equal(_f(sc[i], 0, 16), np.float32([x, 1, 1, 1]))
+
+
+def test_scene_time_dependence(oracle):
+    t = 0.7
+    sc = oracle.generate_scene(t)
+    z = [float(_f(sc[i], 8, 12)[0]) for i in (1, 2, 3)]
+    assert z == [np.float32(math.cos(2 * np.float32(t))), np.float32(math.cos(3 * np.float32(t))),
+                 np.float32(math.cos(np.float32(t)))]
+    np.testing.assert_array_equal(sc[4:], oracle.generate_scene(0.0)[4:])
+
+
+def test_scene_regression_hash(oracle):
+    """FNV-1a-64 over spheres[4..487]. SURVEY.md §4 quotes b1fa62b66a87952d from a survey-time
+    build whose hashing procedure is not recorded; no draw-order / padding variant of scene.h
+    reproduces it, so the reference-derived pins above carry parity and this
+    value pins the oracle against regressions."""
+    sc = oracle.generate_scene(0.0)
+    h = 0xCBF29CE484222325
+    for c in sc[4:].tobytes():
+        h = ((h ^ c) * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+    assert h == 0x9E1C4982E10FE953
+
+
+def test_big_grid_generator(oracle):
+    sc = oracle.generate_scene(0.0, 158)
+    assert sc.shape[0] == 4 + 316 * 316
+    np.testing.assert_array_equal(sc[:4], oracle.generate_scene(0.0)[:4])
+
+
+def test_sin_accuracy(oracle):
+    rng = np.random.default_rng(1)
+    xs = np.concatenate([rng.uniform(-100, 100, 2000), rng.uniform(-6e4, 6e4, 2000),
+                         np.arange(-50, 50) * np.pi]).astype(np.float32)
+    for x in xs:
+        got = oracle.sinf(float(x))
+        ref = math.sin(float(x))
+        assert abs(got - ref) <= 2e-7 + 2e-7 * abs(ref), (x, got, ref)
+
+
+@pytest.mark.parametrize("case", ["g64x36_spp4", "g48x32_spp3_depth3_local", "g40x24_spp2_counter"])
+def test_golden_fixtures(oracle, case):
+    import json
+    meta = json.loads((GOLDEN / f"{case}.json").read_text())
+    sc = oracle.generate_scene(meta["t"], meta["K"])
+    rci = oracle.render_call_info(meta["spp"], meta["W"], meta["H"], tuple(meta["offset"]))
+    op = oracle.options(max_depth=meta["max_depth"], seed_mode=meta["seed_mode"], rng_mode=meta["rng_mode"])
+    acc, out, st = oracle.render(sc, rci, meta["band_w"], meta["band_h"], opts=op, threads=4)
+    g = np.load(GOLDEN / f"{case}.npz", allow_pickle=False)
+    np.testing.assert_array_equal(acc, g["accum"])
+    np.testing.assert_array_equal(out, g["rgba8"])
+    assert list(st) == g["stats"].tolist()
+
+
+def test_band_split_invariance(oracle):
+    """Global seeds make an image independent of how it is split into bands."""
+    sc = oracle.generate_scene()
+    W, H = 40, 30
+    full_a, full_o, _ = oracle.render(sc, oracle.render_call_info(2, W, H), W, H, threads=4)
+    top_a, top_o, _ = oracle.render(sc, oracle.render_call_info(2, W, H, (0, 0)), W, 11, threads=4)
+    bot_a, bot_o, _ = oracle.render(sc, oracle.render_call_info(2, W, H, (0, 11)), W, 19, threads=4)
+    np.testing.assert_array_equal(np.concatenate([top_a, bot_a]), full_a)
+    np.testing.assert_array_equal(np.concatenate([top_o, bot_o]), full_o)
+    rows = np.array([3, 17, 29, 0], np.uint32)  # strip tiling through the rows map
+    r_a, r_o, _ = oracle.render(sc, oracle.render_call_info(2, W, H), W, 4, rows=rows, threads=2)
+    np.testing.assert_array_equal(r_a, full_a[rows])
+
+
+def test_launch_local_seed_mode(oracle):
+    """shader.rgen:40 verbatim: the seed uses the band-local launch id."""
+    sc = oracle.generate_scene()
+    W, H = 24, 16
+    full_a, _, _ = oracle.render(sc, oracle.render_call_info(1, W, H), W, H, opts=oracle.options(seed_mode=1))
+    glob_a, _, _ = oracle.render(sc, oracle.render_call_info(1, W, H), W, H)
+    np.testing.assert_array_equal(full_a, glob_a)   # offset 0: local == global
+    bot_l, _, _ = oracle.render(sc, oracle.render_call_info(1, W, H, (0, 8)), W, 8, opts=oracle.options(seed_mode=1))
+    assert not np.array_equal(bot_l, glob_a[8:])     # band-local seeds repeat the top band's stream
+
+
+def test_counter_rng_sample_split(oracle):
+    """RT_RNG_SAMPLE_COUNTER: 4 samples in one call == 2 + 2 (accumulate, sample_base)."""
+    sc = oracle.generate_scene()
+    W, H = 16, 12
+    a4, _, _ = oracle.render(sc, oracle.render_call_info(4, W, H), W, H, opts=oracle.options(rng_mode=1))
+    a2, _, _ = oracle.render(sc, oracle.render_call_info(2, W, H), W, H, opts=oracle.options(rng_mode=1))
+    a22, _, _ = oracle.render(sc, oracle.render_call_info(2, W, H), W, H, accum=a2,
+                              opts=oracle.options(rng_mode=1, accumulate=1, sample_base=2))
+    # float accumulator rounding between the two calls: sums agree to float precision
+    np.testing.assert_allclose(a22, a4, rtol=1e-6, atol=1e-6)
+
+
+def test_empty_scene_is_sky(oracle):
+    rci = oracle.render_call_info(3, 8, 4)
+    acc, out, st = oracle.render(np.zeros((0, 80), np.uint8), rci, 8, 4)
+    sky = np.float32([0.7, 0.8, 1.0]).astype(np.float64)
+    expect = (sky + sky + sky).astype(np.float32)          # dvec3 sum, stored as float
+    np.testing.assert_array_equal(acc[..., :3], np.broadcast_to(expect, (4, 8, 3)))
+    px = np.sqrt(expect / np.float32(3)).astype(np.float32)
+    assert out[0, 0].tolist() == [int(v * np.float32(255) + np.float32(0.5)) for v in px] + [255]
+    assert st[0] == 3 * 32 and st[1] == 3 * 32
+
+
+def test_depth_one_is_black_or_direct(oracle):
+    """max_depth 1: a scattering first hit ends with light 0 (Q6); only absorbed hits or misses
+    contribute (here: nothing misses, primaries all hit geometry)."""
+    sc = oracle.generate_scene()
+    acc, out, st = oracle.render(sc, oracle.render_call_info(2, 32, 18), 32, 18, opts=oracle.options(max_depth=1))
+    assert st[0] == st[1]
+    assert (acc[..., :3] == 0).mean() > 0.9
