@@ -153,6 +153,8 @@ int rt_store_ppm(const char* path, const uint8_t* rgba8, uint32_t width, uint32_
 /* Diagnostic (tests only): evaluates one arithmetic-contract primitive on `device` for n
  * (x, y) pairs: op 0 sqrt(x), 1 x/y, 2 sin(x), 3 fma(x,y,1), 4 normalize(x,y,0.5).x, 5 pow(x,5). */
 int rt_debug_math(int device, int op, const float* in_pairs, float* out, uint32_t n);
+/* Diagnostic: per-phase cycle sums of ctx's last launch, filled only by -DRT_STAMPS builds. */
+int rt_debug_stamps(rt_context* ctx, uint64_t* out8);
 
 /* src/ray_trace.h:9-15 — identical symbol and parameter list. Renders the canonical scene once
  * (t = 0), prints the frame time, stores `render.ppm` when storeRenderResult, and returns. */

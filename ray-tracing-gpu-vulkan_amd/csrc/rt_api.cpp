@@ -24,8 +24,9 @@
 #include "rt_internal.h"
 
 namespace rt {
-hipError_t launch_trace(const TraceParams& P, uint32_t accel, bool count, int grid, hipStream_t st);
-hipError_t trace_occupancy(uint32_t accel, bool count, int* blocks_per_cu);
+hipError_t launch_trace(const TraceParams& P, uint32_t accel, bool count, int grid, size_t lds_bytes,
+                        hipStream_t st);
+hipError_t trace_occupancy(uint32_t accel, bool count, size_t lds_bytes, int* blocks_per_cu);
 hipError_t launch_scatter_rows(const float* src_acc, const uint8_t* src_px, const uint32_t* rows,
                                uint32_t n_rows, uint32_t width, float* dst_acc, uint8_t* dst_px,
                                hipStream_t st);
@@ -39,8 +40,12 @@ struct rt_context {
     std::vector<void*> scene_allocs;
     rt::Counters* counters = nullptr;   // device
     hipStream_t last_stream = nullptr;
-    int occ[2][2] = {{0, 0}, {0, 0}};   // [accel-1][count]
+    int occ[3][2] = {{0, 0}, {0, 0}, {0, 0}};   // [accel-1][count], blocks per CU
+    size_t lds_bytes = 0;                        // LBVH_LDS staging size of the current scene
 };
+
+// LBVH staged in LDS when its image is at most this large (keeps >= 6 blocks per CU).
+static constexpr size_t kMaxLdsBvhBytes = 24 * 1024;
 
 namespace {
 
@@ -254,7 +259,7 @@ int rt_context_create(int device, rt_context** out) {
     for (uint32_t acc = 1; acc <= 2; acc++)
         for (int cnt = 0; cnt < 2; cnt++) {
             int b = 0;
-            RT_HIP(rt::trace_occupancy(acc, cnt != 0, &b));
+            RT_HIP(rt::trace_occupancy(acc, cnt != 0, 0, &b));
             ctx->occ[acc - 1][cnt] = std::max(1, b);
         }
     *out = ctx.release();
@@ -309,6 +314,17 @@ int rt_set_scene(rt_context* ctx, const Sphere* spheres, uint32_t count, void* s
         d.n_big = uint32_t(bvh.big_ids.size());
         if (int rc = upload(ctx, bvh.big_ids, &d.big_ids, st)) return rc;
         d.n_nodes = uint32_t(bvh.nodes.size());
+        d.n_leaf = uint32_t(bvh.leaf_ids.size());
+        // leaf ids are read as uint4: pad to a multiple of 4
+        while (bvh.leaf_ids.size() % 4) bvh.leaf_ids.push_back(0u);
+        const size_t lds = size_t(2 * d.n_nodes + d.n_leaf + (d.n_leaf + 3) / 4) * 16;
+        ctx->lds_bytes = (d.n_nodes && lds <= kMaxLdsBvhBytes) ? lds : 0;
+        if (ctx->lds_bytes)
+            for (int cnt = 0; cnt < 2; cnt++) {
+                int b = 0;
+                RT_HIP(rt::trace_occupancy(rt::ACCEL_LBVH_LDS, cnt != 0, ctx->lds_bytes, &b));
+                ctx->occ[rt::ACCEL_LBVH_LDS - 1][cnt] = std::max(1, b);
+            }
         if (int rc = upload(ctx, bvh.nodes, &d.nodes, st)) return rc;
         if (int rc = upload(ctx, bvh.leaf_geom, &d.leaf_geom, st)) return rc;
         if (int rc = upload(ctx, bvh.leaf_ids, &d.leaf_ids, st)) return rc;
@@ -333,7 +349,8 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     rt_options o;
     std::memset(&o, 0, sizeof(o));
     if (opt) o = *opt;
-    uint32_t accel = o.accel == RT_ACCEL_BRUTE ? rt::ACCEL_BRUTE : rt::ACCEL_LBVH;
+    uint32_t accel = o.accel == RT_ACCEL_BRUTE ? rt::ACCEL_BRUTE
+                     : (ctx->lds_bytes ? rt::ACCEL_LBVH_LDS : rt::ACCEL_LBVH);
     if (o.accel > RT_ACCEL_LBVH) return fail(RT_ERR_INVALID_ARGUMENT, "unknown accel");
     if (o.seed_mode > RT_SEED_LAUNCH_LOCAL) return fail(RT_ERR_INVALID_ARGUMENT, "unknown seed_mode");
     if (o.rng_mode > RT_RNG_SAMPLE_COUNTER) return fail(RT_ERR_INVALID_ARGUMENT, "unknown rng_mode");
@@ -364,12 +381,16 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     P.n_big = d.n_big;
     P.big_ids = d.big_ids;
     P.nodes = d.n_nodes ? d.nodes : nullptr;
+    P.n_nodes = d.n_nodes;
+    P.n_leaf = d.n_leaf;
     P.leaf_geom = d.leaf_geom;
     P.leaf_ids = d.leaf_ids;
     // Node-cull slack: a candidate's AABB entry lies at most
     // 2.75 r + 1.15e-3 t beyond its reported t.
     P.cull_abs = 3.0f * d.small_rmax + 1e-3f;
     P.cull_rel = 2e-3f;
+    // reserved[1]: LBVH loop form, 0 = classic (default), 1..64 = compaction threshold
+    P.compact = (o.reserved[1] <= 64u) ? o.reserved[1] : 0u;
     P.accum = accum;
     P.out = reinterpret_cast<uint32_t*>(out);
     P.counters = ctx->counters;
@@ -381,7 +402,8 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     const uint64_t full = uint64_t(ctx->cu_count) * ctx->occ[accel - 1][count ? 1 : 0];
     const uint64_t by_work = (lanes_needed + 255u) / 256u;
     const int grid = int(std::max<uint64_t>(1, std::min(full, by_work)));
-    RT_HIP(rt::launch_trace(P, accel, count, grid, st));
+    const size_t lds = accel == rt::ACCEL_LBVH_LDS ? ctx->lds_bytes : 0;
+    RT_HIP(rt::launch_trace(P, accel, count, grid, lds, st));
     ctx->last_stream = st;
     return RT_OK;
 }
@@ -408,6 +430,17 @@ int rt_scatter_rows(rt_context* ctx, const float* src_accum, const uint8_t* src_
     DeviceGuard g(ctx->device);
     RT_HIP(rt::launch_scatter_rows(src_accum, src_rgba8, rows, n_rows, width, dst_accum, dst_rgba8,
                                    static_cast<hipStream_t>(stream)));
+    return RT_OK;
+}
+
+// Diagnostic export: phase cycle sums of the last launch (RT_STAMPS builds; zeros otherwise).
+int rt_debug_stamps(rt_context* ctx, uint64_t* out8) {
+    if (!ctx || !out8) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    DeviceGuard g(ctx->device);
+    RT_HIP(hipStreamSynchronize(ctx->last_stream));
+    rt::Counters c;
+    RT_HIP(hipMemcpy(&c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
+    for (int k = 0; k < 8; k++) out8[k] = c.stamp[k];
     return RT_OK;
 }
 

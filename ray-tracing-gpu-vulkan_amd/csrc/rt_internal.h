@@ -45,10 +45,11 @@ struct DeviceScene {
     BvhNode* nodes = nullptr;      // 2 * n_leaf_spheres - 1 at most
     GeomRec* leaf_geom = nullptr;  // spheres permuted into leaf order (contiguous per leaf)
     uint32_t* leaf_ids = nullptr;  // original index of each leaf slot
+    uint32_t n_leaf = 0;
     float small_rmax = 0.0f;       // largest radius in the tree
 };
 
-enum : uint32_t { ACCEL_BRUTE = 1, ACCEL_LBVH = 2 };
+enum : uint32_t { ACCEL_BRUTE = 1, ACCEL_LBVH = 2, ACCEL_LBVH_LDS = 3 };
 
 // Counters block (device memory, zeroed before each launch by the host).
 struct Counters {
@@ -58,6 +59,7 @@ struct Counters {
     unsigned long long samples;
     unsigned long long box_tests;
     unsigned long long sphere_tests;
+    unsigned long long stamp[8];   // diagnostic builds only (-DRT_STAMPS): cycles per phase
 };
 
 // Kernel launch parameters (passed by value as the kernel argument).
@@ -84,10 +86,13 @@ struct TraceParams {
     uint32_t n_big;
     const uint32_t* big_ids;
     const BvhNode* nodes;
+    uint32_t n_nodes;
+    uint32_t n_leaf;               // spheres in the tree (leaf slots)
     const GeomRec* leaf_geom;
     const uint32_t* leaf_ids;
     float cull_abs;                // LBVH node-cull slack: best + cull_abs + cull_rel * best
     float cull_rel;
+    uint32_t compact;              // LBVH: service lanes once fewer than this many still traverse
     // outputs
     float* accum;                  // band_w * band_h * 4 floats
     uint32_t* out;                 // band_w * band_h packed rgba8

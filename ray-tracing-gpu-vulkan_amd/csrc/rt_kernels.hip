@@ -28,9 +28,39 @@ constexpr float T_MIN = 0.001f;               // shader.rgen:75
 constexpr float T_MAX_SUCC = 0x1.388002p+13f; // successor of 10000.0f (shader.rgen:26): a report
                                               // at exactly tMax is accepted, so compare with '<'.
 
-enum : uint32_t { ST_NEED_PIXEL = 0, ST_NEED_SAMPLE = 1, ST_TRACING = 2, ST_RETIRED = 3 };
+enum : uint32_t { ST_NEED_PIXEL = 0, ST_NEED_SAMPLE = 1, ST_TRACING = 2, ST_RETIRED = 3, ST_READY = 4 };
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// Diagnostic build only (-DRT_STAMPS): wave-level s_memtime phase stamps, summed per wave and
+// added to Counters::stamp[] at exit (cdna_hip_programming.md §7, In-kernel stamps). The shipped
+// build compiles every STAMP() to nothing.
+#ifdef RT_STAMPS
+#define STAMP(k)                                                                               \
+    do {                                                                                       \
+        __builtin_amdgcn_sched_barrier(0);                                                     \
+        unsigned long long t_;                                                                 \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");           \
+        __builtin_amdgcn_sched_barrier(0);                                                     \
+        stamp_acc[stamp_cur] += t_ - stamp_t;                                                  \
+        stamp_t = t_;                                                                          \
+        stamp_cur = (k);                                                                       \
+    } while (0)
+#define STAMP_DECL                                                                             \
+    unsigned long long stamp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, stamp_t = 0;                   \
+    uint32_t stamp_cur = 7;                                                                    \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_t)::"memory")
+#define STAMP_FLUSH                                                                            \
+    do {                                                                                       \
+        STAMP(7);                                                                              \
+        if (lane_id() == 0)                                                                    \
+            for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&P.counters->stamp[k_], stamp_acc[k_]);   \
+    } while (0)
+#else
+#define STAMP(k) do {} while (0)
+#define STAMP_DECL do {} while (0)
+#define STAMP_FLUSH do {} while (0)
+#endif
 
 // Driver traversal test for one sphere's AABB (src/ray_trace.cpp:586-596: center -/+ radius)
 // over [T_MIN, T_MAX]; identical arithmetic to the oracle's aabb_hit.
@@ -68,6 +98,34 @@ __device__ __forceinline__ void test_sphere(float cx, float cy, float cz, float 
     }
 }
 
+// As test_sphere, with the sphere index read from ids[slot] only when the quadratic reports
+// (LBVH leaves: the id is needed for the tie-break and the radius, both in the rare branch).
+template <bool TB>
+__device__ __forceinline__ void test_sphere_ids(float cx, float cy, float cz, float rr,
+                                                const float* __restrict__ radius,
+                                                const uint32_t* __restrict__ ids, uint32_t slot,
+                                                V3 o, V3 d, V3 inv, float a, float& best,
+                                                uint32_t& bi) {
+    const float ocx = o.x - cx, ocy = o.y - cy, ocz = o.z - cz;
+    const float b = __builtin_fmaf(ocz, d.z, __builtin_fmaf(ocy, d.y, ocx * d.x));
+    const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - rr;
+    const float D = __builtin_fmaf(b, b, -(a * c));
+    if (D >= 0.0f) {
+        const float sq = __builtin_sqrtf(D);
+        const float t1 = (-b - sq) / a;
+        const float t2 = (-b + sq) / a;
+        const float t = (t1 >= T_MIN) ? t1 : t2;
+        if (t >= T_MIN && t <= best) {
+            const uint32_t id = ids[slot];
+            const bool better = TB ? (t < best || id < bi) : (t < best);
+            if (better && aabb_hit(cx, cy, cz, radius[id], o, inv)) {
+                best = t;
+                bi = id;
+            }
+        }
+    }
+}
+
 // Brute force: every lane tests every sphere. The sphere index is wave-uniform, so the geometry
 // comes through the scalar cache: 8 spheres (128 B) per iteration as two s_load_dwordx16 issued
 // before any of the 8 tests, feeding the VALU as SGPR operands (13 VALU per sphere, no VGPR
@@ -90,230 +148,406 @@ __device__ __forceinline__ void closest_brute(const rt::TraceParams& P, V3 o, V3
     }
 }
 
-// LBVH: big spheres exhaustively, then the stackless escape-link walk over the small spheres.
-// Node test: slab test over [T_MIN, min(T_MAX, best + cull)], evaluated with one fma per plane
-// and widened by `tol` (the fma form's rounding relative to the exact slab form).
-// cull = cull_abs + cull_rel * best bounds how far a candidate's AABB entry can lie beyond its
-// reported t (quadratic rounding + box-vs-sphere geometry), so no node holding a candidate that
-// could still win is ever skipped: the result is identical to brute force.
-template <bool COUNT>
-__device__ __forceinline__ void closest_lbvh(const rt::TraceParams& P, V3 o, V3 d, V3 inv, float a,
-                                             float& best, uint32_t& bi, uint32_t& n_box,
-                                             uint32_t& n_sph) {
-    for (uint32_t k = 0; k < P.n_big; ++k) {
-        const uint32_t id = P.big_ids[k];
-        const rt::GeomRec s = P.geom[id];
-        test_sphere<true>(s.cx, s.cy, s.cz, s.rr, P.radius, o, d, inv, a, id, best, bi);
-    }
-    if (COUNT) n_sph += P.n_big;
-    const rt::BvhNode* __restrict__ nodes = P.nodes;
-    if (nodes == nullptr) return;
-    const float ox = o.x * inv.x, oy = o.y * inv.y, oz = o.z * inv.z;
-    const float tol = 4.8e-7f * fmaxf(fmaxf(fabsf(ox), fabsf(oy)), fabsf(oz));
-    uint32_t ni = 0;
-    while (ni != 0xffffffffu) {
-        const float4 n0 = *reinterpret_cast<const float4*>(&nodes[ni]);
-        const float4 n1 = *(reinterpret_cast<const float4*>(&nodes[ni]) + 1);
-        if (COUNT) n_box++;
-        const float tx0 = __builtin_fmaf(n0.x, inv.x, -ox), tx1 = __builtin_fmaf(n1.x, inv.x, -ox);
-        const float ty0 = __builtin_fmaf(n0.y, inv.y, -oy), ty1 = __builtin_fmaf(n1.y, inv.y, -oy);
-        const float tz0 = __builtin_fmaf(n0.z, inv.z, -oz), tz1 = __builtin_fmaf(n1.z, inv.z, -oz);
-        const float tnear = fmaxf(fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1)), T_MIN);
-        const float limit = fminf(__builtin_fmaf(best, P.cull_rel, best + P.cull_abs), 10000.0f);
-        const float tfar = fminf(fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1)), limit);
-        const bool hit = tnear <= __builtin_fmaf(fabsf(tfar), 4.8e-7f, tfar + tol);
-        const uint32_t fc = __float_as_uint(n1.w);
-        if (hit && fc != 0u) {
-            const uint32_t first = fc >> 4, cnt = fc & 15u;
-            for (uint32_t j = 0; j < cnt; ++j) {
-                const rt::GeomRec s = P.leaf_geom[first + j];
-                test_sphere<true>(s.cx, s.cy, s.cz, s.rr, P.radius, o, d, inv, a,
-                                  P.leaf_ids[first + j], best, bi);
-            }
-            if (COUNT) n_sph += cnt;
-            ni = __float_as_uint(n0.w);
-        } else {
-            ni = hit ? ni + 1 : __float_as_uint(n0.w);
-        }
-    }
+// ---------------------------------------------------------------------------------------------
+// Per-lane path state and the pieces of shader.rgen / rchit / rmiss shared by both loops.
+// ---------------------------------------------------------------------------------------------
+struct Camera { V3 lf, hor, ver, ulc, cup, crt; };
+
+__device__ __forceinline__ Camera load_camera(const rt::TraceParams& P) {
+    return Camera{v3(P.lf[0], P.lf[1], P.lf[2]), v3(P.hor[0], P.hor[1], P.hor[2]),
+                  v3(P.ver[0], P.ver[1], P.ver[2]), v3(P.ulc[0], P.ulc[1], P.ulc[2]),
+                  v3(P.cup[0], P.cup[1], P.cup[2]), v3(P.crt[0], P.crt[1], P.crt[2])};
 }
 
-template <uint32_t ACCEL, bool COUNT>
-__global__ __launch_bounds__(256) void rt_trace_kernel(const rt::TraceParams P) {
+struct Path {
+    uint32_t px;           // lx | ly << 16 (band-local launch id)
+    uint32_t pixel_seed;   // TEA(TEA(x, y), number)
+    uint32_t seed;         // LCG state (random.glsl)
+    uint32_t s;            // samples done for this pixel
+    uint32_t depth;        // segments traced in this sample
+    V3 thr;                // reflectedColor (shader.rgen:71)
+    double sx, sy, sz;     // dvec3 sum (shader.rgen:55)
+};
+
+// Pixel refill: lanes in `st == ST_NEED_PIXEL` take the next units of the device work counter
+// (one atomic per wave, ranks from the ballot). Units are pixels in 8x8-tile order.
+__device__ __forceinline__ void refill(const rt::TraceParams& P, uint32_t lane, uint32_t& st,
+                                       Path& ps) {
+    const unsigned long long need = __ballot(st == ST_NEED_PIXEL);
+    if (!need) return;
+    const uint32_t cnt = __popcll(need);
+    const int leader = __ffsll(need) - 1;
+    uint32_t base = 0;
+    if (int(lane) == leader) base = atomicAdd(&P.counters->work_head, cnt);
+    base = __shfl(base, leader);
+    if (st != ST_NEED_PIXEL) return;
+    const uint32_t u = base + __popcll(need & ((1ull << lane) - 1ull));
+    if (u >= P.n_units) { st = ST_RETIRED; return; }
+    const uint32_t t = u >> 6, w = u & 63u;
+    const uint32_t lx = (t % P.tiles_x) * 8u + (w & 7u);
+    const uint32_t ly = (t / P.tiles_x) * 8u + (w >> 3);
+    if (lx >= P.band_w || ly >= P.band_h) return;   // ragged edge: stays NEED_PIXEL, refetches
+    // shader.rgen:40
+    const uint32_t gx = P.off_x + lx;
+    const uint32_t gy = P.rows ? P.rows[ly] : P.off_y + ly;
+    ps.px = lx | (ly << 16);
+    ps.pixel_seed = tea(tea(P.seed_local ? lx : gx, P.seed_local ? ly : gy), P.number);
+    ps.seed = ps.pixel_seed;
+    ps.s = 0;
+    if (P.accumulate) {  // shader.rgen:53-55
+        const float4 acc = reinterpret_cast<const float4*>(P.accum)[size_t(ly) * P.band_w + lx];
+        ps.sx = acc.x; ps.sy = acc.y; ps.sz = acc.z;
+    } else {
+        ps.sx = ps.sy = ps.sz = 0.0;
+    }
+    st = ST_NEED_SAMPLE;
+}
+
+// shader.rgen:56-58 + 107-115: next camera ray of the lane's pixel. Returns false (and stores
+// the pixel, shader.rgen:61-66) when the pixel's samples are done.
+__device__ __forceinline__ bool start_sample(const rt::TraceParams& P, const Camera& cam, Path& ps,
+                                             V3& o, V3& d) {
+    const uint32_t lx = ps.px & 0xffffu, ly = ps.px >> 16;
+    if (ps.s >= P.spp) {
+        const float s0 = float(ps.sx), s1 = float(ps.sy), s2 = float(ps.sz);
+        const size_t texel = size_t(ly) * P.band_w + lx;
+        reinterpret_cast<float4*>(P.accum)[texel] = make_float4(s0, s1, s2, 1.0f);
+        const float spp = float(P.spp);
+        const uint32_t r8 = unorm8(__builtin_sqrtf(s0 / spp));
+        const uint32_t g8 = unorm8(__builtin_sqrtf(s1 / spp));
+        const uint32_t b8 = unorm8(__builtin_sqrtf(s2 / spp));
+        P.out[texel] = r8 | (g8 << 8) | (b8 << 16) | (255u << 24);
+        return false;
+    }
+    const uint32_t gx = P.off_x + lx;
+    const uint32_t gy = P.rows ? P.rows[ly] : P.off_y + ly;
+    if (P.rng_counter) ps.seed = tea(ps.pixel_seed, P.sample_base + ps.s);
+    float ux = float(gx) + rnd(ps.seed);
+    float uy = float(gy) + rnd(ps.seed);
+    ux = ux / P.size_x;
+    uy = uy / P.size_y;
+    const float lxr = rnd_pm1(ps.seed);
+    const float lyr = rnd_pm1(ps.seed);
+    const float l2 = __builtin_sqrtf(__builtin_fmaf(lyr, lyr, lxr * lxr));
+    const float il = 1.0f / l2;
+    const float rx = P.half_aperture * (lxr * il);
+    const float ry = P.half_aperture * (lyr * il);
+    const V3 from = add(cam.lf, add(scale(rx, cam.crt), scale(ry, cam.cup)));
+    const V3 to = sub(add(cam.ulc, scale(ux, cam.hor)), scale(uy, cam.ver));
+    o = from;
+    d = normalize(sub(to, from));
+    ps.thr = v3(1.0f, 1.0f, 1.0f);
+    ps.depth = 0;
+    return true;
+}
+
+// shader.rchit:38-133 / shader.rmiss:13-18 + shader.rgen:77-88 for one finished trace.
+// Returns true when the path continues (o, d hold the next ray), false when the sample ended
+// (its colour has been added to the pixel sum).
+__device__ __forceinline__ bool shade(const rt::TraceParams& P, Path& ps, uint32_t bi, float best,
+                                      V3& o, V3& d) {
+    V3 att;
+    bool scatter = false;
+    V3 sd = v3(0.0f, 0.0f, 0.0f);
+    V3 p = o;
+    if (bi == 0xffffffffu) {
+        att = v3(0.7f, 0.8f, 1.0f);  // shader.rmiss:15
+    } else {
+        // shader.rint:33/37 hit attribute; shader.rchit:38-49
+        p = v3(__builtin_fmaf(best, d.x, o.x), __builtin_fmaf(best, d.y, o.y),
+               __builtin_fmaf(best, d.z, o.z));
+        const rt::GeomRec gc = P.geom[bi];
+        const float4 m0 = reinterpret_cast<const float4*>(P.mat)[2 * bi];
+        const float4 m1 = reinterpret_cast<const float4*>(P.mat)[2 * bi + 1];
+        const uint32_t tt = __float_as_uint(m1.w);
+        const uint32_t mtype = tt & 0xffu, ttype = tt >> 8;
+        const V3 outward = normalize(sub(p, v3(gc.cx, gc.cy, gc.cz)));
+        const bool front = dot(d, outward) < 0.0f;
+        const V3 n = front ? outward : neg(outward);
+        // shader.rchit:53-64
+        att = v3(m0.x, m0.y, m0.z);
+        if (ttype == 1u) {
+            const float sines = sinf_det(6.0f * p.x) * sinf_det(6.0f * p.y) * sinf_det(6.0f * p.z);
+            if (!(sines > 0.0f)) att = v3(m1.x, m1.y, m1.z);
+        }
+        if (mtype == 0u) {                       // diffuse, shader.rchit:68-76
+            sd = add(n, random_unit_vector(ps.seed));
+            if (fabsf(sd.x) < 1e-8f && fabsf(sd.y) < 1e-8f && fabsf(sd.z) < 1e-8f) sd = n;
+        } else if (mtype == 1u) {                // metal, shader.rchit:78-89
+            const V3 refl = reflect(d, n);
+            const V3 fuzz = scale(m0.w, random_unit_vector(ps.seed));
+            const V3 sc = normalize(add(refl, fuzz));
+            if (dot(sc, n) > 0.0f) sd = sc;
+        } else if (mtype == 2u) {                // dielectric, shader.rchit:91-100,125-133
+            const float eta = front ? (1.0f / m0.w) : m0.w;
+            const float cos_t = dot(neg(d), n);
+            bool refracts = false;
+            if (eta * __builtin_sqrtf(1.0f - cos_t * cos_t) <= 1.0f) {
+                const float q = (1.0f - eta) / (1.0f + eta);
+                const float r = q * q;
+                const float refl = r + (1.0f - r) * pow5(1.0f - cos_t);
+                refracts = refl < rnd(ps.seed);
+            }
+            sd = refracts ? refract(d, n, eta) : reflect(d, n);
+        }
+        scatter = !(sd.x == 0.0f && sd.y == 0.0f && sd.z == 0.0f);  // shader.rchit:48
+    }
+    // shader.rgen:77-88
+    V3 col;
+    if (scatter) {
+        ps.thr = mul(ps.thr, att);
+        o = p;
+        d = normalize(sd);
+        ps.depth++;
+        if (ps.depth < P.max_depth) return true;
+        col = mul(ps.thr, v3(0.0f, 0.0f, 0.0f));   // depth exhausted: light stays 0 (Q6)
+    } else {
+        col = mul(ps.thr, att);
+    }
+    ps.sx += double(col.x);
+    ps.sy += double(col.y);
+    ps.sz += double(col.z);
+    ps.s++;
+    return false;
+}
+
+// ---------------------------------------------------------------------------------------------
+// LBVH traversal state and the one-node step.
+// ---------------------------------------------------------------------------------------------
+struct Ray {
+    V3 o, d, inv, oi;      // origin, direction, 1/d, o * (1/d)
+    float a, tol;          // dot(d, d); fma-slab rounding allowance
+    float best;
+    uint32_t bi, ni;       // closest so far, next node (END = done)
+};
+constexpr uint32_t END = 0xffffffffu;
+
+// New segment: hoisted per-ray terms, the exhaustive big spheres, walk from the root.
+__device__ __forceinline__ void setup_ray(const rt::TraceParams& P, Ray& r, uint32_t& n_sph) {
+    r.a = dot(r.d, r.d);
+    r.inv = v3(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+    r.oi = v3(r.o.x * r.inv.x, r.o.y * r.inv.y, r.o.z * r.inv.z);
+    r.tol = 4.8e-7f * fmaxf(fmaxf(fabsf(r.oi.x), fabsf(r.oi.y)), fabsf(r.oi.z));
+    r.best = T_MAX_SUCC;
+    r.bi = 0xffffffffu;
+    typedef const __attribute__((address_space(4))) uint32_t* ConstU;
+    typedef const __attribute__((address_space(4))) float* ConstF;
+    const ConstU ids = (ConstU)(P.big_ids);
+    const ConstF g = (ConstF)(P.geom);
+    for (uint32_t k = 0; k < P.n_big; ++k) {   // wave-uniform: scalar loads
+        const uint32_t id = ids[k];
+        test_sphere<true>(g[4 * id], g[4 * id + 1], g[4 * id + 2], g[4 * id + 3], P.radius, r.o, r.d,
+                          r.inv, r.a, id, r.best, r.bi);
+    }
+    n_sph += P.n_big;
+    r.ni = P.nodes ? 0u : END;
+}
+
+// One node of the stackless escape-link walk. Node test: slab test over
+// [T_MIN, min(T_MAX, best + cull)] with one fma per plane, widened by the fma form's rounding
+// allowance; cull = cull_abs + cull_rel * best bounds how far a candidate's AABB entry can lie
+// beyond its reported t, so no node holding a possible winner is skipped and
+// the result equals brute force bit for bit.
+template <bool COUNT>
+__device__ __forceinline__ void visit_node(const rt::TraceParams& P, const float4* __restrict__ nodes4,
+                                           const float4* __restrict__ leaf4,
+                                           const uint32_t* __restrict__ leaf_ids, Ray& r,
+                                           uint32_t& n_box, uint32_t& n_sph) {
+    const float4 n0 = nodes4[2 * r.ni];
+    const float4 n1 = nodes4[2 * r.ni + 1];
+    if (COUNT) n_box++;
+    const float tx0 = __builtin_fmaf(n0.x, r.inv.x, -r.oi.x), tx1 = __builtin_fmaf(n1.x, r.inv.x, -r.oi.x);
+    const float ty0 = __builtin_fmaf(n0.y, r.inv.y, -r.oi.y), ty1 = __builtin_fmaf(n1.y, r.inv.y, -r.oi.y);
+    const float tz0 = __builtin_fmaf(n0.z, r.inv.z, -r.oi.z), tz1 = __builtin_fmaf(n1.z, r.inv.z, -r.oi.z);
+    const float tnear = fmaxf(fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1)), T_MIN);
+    const float limit = fminf(__builtin_fmaf(r.best, P.cull_rel, r.best + P.cull_abs), 10000.0f);
+    const float tfar = fminf(fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1)), limit);
+    const bool hit = tnear <= __builtin_fmaf(fabsf(tfar), 4.8e-7f, tfar + r.tol);
+    const uint32_t fc = __float_as_uint(n1.w);
+    if (hit && fc != 0u) {
+        const uint32_t first = fc >> 4, cnt = fc & 15u;
+        for (uint32_t j = 0; j < cnt; ++j) {
+            const float4 sp = leaf4[first + j];
+            test_sphere_ids<true>(sp.x, sp.y, sp.z, sp.w, P.radius, leaf_ids, first + j, r.o, r.d,
+                                  r.inv, r.a, r.best, r.bi);
+        }
+        if (COUNT) n_sph += cnt;
+    }
+    r.ni = (hit && fc == 0u) ? r.ni + 1u : __float_as_uint(n0.w);
+}
+
+#ifndef RT_TRACE_WAVES_PER_SIMD
+#define RT_TRACE_WAVES_PER_SIMD 6
+#endif
+
+// ---------------------------------------------------------------------------------------------
+// Brute-force kernel: one segment per loop iteration for every lane (the sphere loop is
+// wave-uniform, so there is no traversal divergence to manage).
+// ---------------------------------------------------------------------------------------------
+template <bool COUNT>
+__global__ __launch_bounds__(256, RT_TRACE_WAVES_PER_SIMD) void rt_trace_brute_kernel(const rt::TraceParams P) {
     const uint32_t lane = lane_id();
-    uint32_t state = ST_NEED_PIXEL;
-    uint32_t lx = 0, ly = 0, gx = 0, gy = 0, pixel_seed = 0, seed = 0, s = 0, depth = 0;
-    V3 o = v3(0, 0, 0), d = v3(0, 0, 1), thr = v3(1, 1, 1);
-    float a = 1.0f;
-    double sum_x = 0.0, sum_y = 0.0, sum_z = 0.0;
-    uint32_t n_seg = 0, n_smp = 0, n_box = 0, n_sph = 0;
-
-    const V3 lf = v3(P.lf[0], P.lf[1], P.lf[2]);
-    const V3 hor = v3(P.hor[0], P.hor[1], P.hor[2]);
-    const V3 ver = v3(P.ver[0], P.ver[1], P.ver[2]);
-    const V3 ulc = v3(P.ulc[0], P.ulc[1], P.ulc[2]);
-    const V3 cup = v3(P.cup[0], P.cup[1], P.cup[2]);
-    const V3 crt = v3(P.crt[0], P.crt[1], P.crt[2]);
-
+    const Camera cam = load_camera(P);
+    uint32_t st = ST_NEED_PIXEL;
+    Path ps{};
+    V3 o = v3(0, 0, 0), d = v3(0, 0, 1);
+    uint32_t n_seg = 0, n_smp = 0, n_sph = 0;
     for (;;) {
-        // ---- refill: lanes without a pixel take the next units of the work counter ----------
-        const unsigned long long need = __ballot(state == ST_NEED_PIXEL);
-        if (need) {
-            const uint32_t cnt = __popcll(need);
-            const int leader = __ffsll(need) - 1;
-            uint32_t base = 0;
-            if (int(lane) == leader) base = atomicAdd(&P.counters->work_head, cnt);
-            base = __shfl(base, leader);
-            if (state == ST_NEED_PIXEL) {
-                const uint32_t rank = __popcll(need & ((1ull << lane) - 1ull));
-                const uint32_t u = base + rank;
-                if (u >= P.n_units) {
-                    state = ST_RETIRED;
-                } else {
-                    const uint32_t t = u >> 6, w = u & 63u;
-                    lx = (t % P.tiles_x) * 8u + (w & 7u);
-                    ly = (t / P.tiles_x) * 8u + (w >> 3);
-                    if (lx < P.band_w && ly < P.band_h) {
-                        // shader.rgen:40-45
-                        gx = P.off_x + lx;
-                        gy = P.rows ? P.rows[ly] : P.off_y + ly;
-                        const uint32_t sx = P.seed_local ? lx : gx;
-                        const uint32_t sy = P.seed_local ? ly : gy;
-                        pixel_seed = tea(tea(sx, sy), P.number);
-                        seed = pixel_seed;
-                        s = 0;
-                        if (P.accumulate) {  // shader.rgen:53-55
-                            const float4 acc = reinterpret_cast<const float4*>(P.accum)[size_t(ly) * P.band_w + lx];
-                            sum_x = acc.x; sum_y = acc.y; sum_z = acc.z;
-                        } else {
-                            sum_x = sum_y = sum_z = 0.0;
-                        }
-                        state = ST_NEED_SAMPLE;
-                    }
-                }
-            }
+        refill(P, lane, st, ps);
+        if (st == ST_NEED_SAMPLE) {
+            if (start_sample(P, cam, ps, o, d)) { st = ST_TRACING; n_smp++; }
+            else st = ST_NEED_PIXEL;
         }
-        // ---- sample start (shader.rgen:56-58, 107-115) or pixel end (:61-66) --------------
-        if (state == ST_NEED_SAMPLE) {
-            if (s < P.spp) {
-                if (P.rng_counter) seed = tea(pixel_seed, P.sample_base + s);
-                float ux = float(gx) + rnd(seed);
-                float uy = float(gy) + rnd(seed);
-                ux = ux / P.size_x;
-                uy = uy / P.size_y;
-                const float lxr = rnd_pm1(seed);
-                const float lyr = rnd_pm1(seed);
-                const float l2 = __builtin_sqrtf(__builtin_fmaf(lyr, lyr, lxr * lxr));
-                const float il = 1.0f / l2;
-                const float rx = P.half_aperture * (lxr * il);
-                const float ry = P.half_aperture * (lyr * il);
-                const V3 from = add(lf, add(scale(rx, crt), scale(ry, cup)));
-                const V3 to = sub(add(ulc, scale(ux, hor)), scale(uy, ver));
-                o = from;
-                d = normalize(sub(to, from));
-                a = dot(d, d);
-                thr = v3(1.0f, 1.0f, 1.0f);
-                depth = 0;
-                n_smp++;
-                state = ST_TRACING;
-            } else {
-                const float s0 = float(sum_x), s1 = float(sum_y), s2 = float(sum_z);
-                const size_t texel = size_t(ly) * P.band_w + lx;
-                reinterpret_cast<float4*>(P.accum)[texel] = make_float4(s0, s1, s2, 1.0f);
-                const float spp = float(P.spp);
-                const uint32_t r8 = unorm8(__builtin_sqrtf(s0 / spp));
-                const uint32_t g8 = unorm8(__builtin_sqrtf(s1 / spp));
-                const uint32_t b8 = unorm8(__builtin_sqrtf(s2 / spp));
-                P.out[texel] = r8 | (g8 << 8) | (b8 << 16) | (255u << 24);
-                state = ST_NEED_PIXEL;
-            }
-        }
-        if (__ballot(state == ST_NEED_PIXEL)) continue;   // refill before the next trace
-        if (!__ballot(state == ST_TRACING)) break;         // every lane retired
-
-        if (state == ST_TRACING) {
-            // ---- one traceRayEXT (shader.rgen:75) ------------------------------------------
+        if (__ballot(st == ST_NEED_PIXEL)) continue;   // refill before the next trace
+        if (!__ballot(st == ST_TRACING)) break;         // every lane retired
+        if (st == ST_TRACING) {
             float best = T_MAX_SUCC;
             uint32_t bi = 0xffffffffu;
             const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-            if (ACCEL == rt::ACCEL_BRUTE) {
-                closest_brute(P, o, d, inv, a, best, bi);
-                if (COUNT) n_sph += P.n_spheres;
-            } else {
-                closest_lbvh<COUNT>(P, o, d, inv, a, best, bi, n_box, n_sph);
-            }
+            closest_brute(P, o, d, inv, dot(d, d), best, bi);
+            if (COUNT) n_sph += P.n_spheres;
             n_seg++;
-            V3 att;
-            bool scatter = false;
-            V3 sd = v3(0.0f, 0.0f, 0.0f);
-            V3 p = o;
-            if (bi == 0xffffffffu) {
-                att = v3(0.7f, 0.8f, 1.0f);  // shader.rmiss:15
-            } else {
-                // shader.rint:33/37 hit attribute; shader.rchit:38-49
-                p = v3(__builtin_fmaf(best, d.x, o.x), __builtin_fmaf(best, d.y, o.y),
-                       __builtin_fmaf(best, d.z, o.z));
-                const rt::GeomRec gc = P.geom[bi];
-                const float4 m0 = reinterpret_cast<const float4*>(P.mat)[2 * bi];
-                const float4 m1 = reinterpret_cast<const float4*>(P.mat)[2 * bi + 1];
-                const uint32_t tt = __float_as_uint(m1.w);
-                const uint32_t mtype = tt & 0xffu, ttype = tt >> 8;
-                const V3 outward = normalize(sub(p, v3(gc.cx, gc.cy, gc.cz)));
-                const bool front = dot(d, outward) < 0.0f;
-                const V3 n = front ? outward : neg(outward);
-                // shader.rchit:53-64
-                att = v3(m0.x, m0.y, m0.z);
-                if (ttype == 1u) {
-                    const float sines = sinf_det(6.0f * p.x) * sinf_det(6.0f * p.y) * sinf_det(6.0f * p.z);
-                    if (!(sines > 0.0f)) att = v3(m1.x, m1.y, m1.z);
-                }
-                if (mtype == 0u) {                       // diffuse, shader.rchit:68-76
-                    sd = add(n, random_unit_vector(seed));
-                    if (fabsf(sd.x) < 1e-8f && fabsf(sd.y) < 1e-8f && fabsf(sd.z) < 1e-8f) sd = n;
-                } else if (mtype == 1u) {                // metal, shader.rchit:78-89
-                    const V3 refl = reflect(d, n);
-                    const V3 fuzz = scale(m0.w, random_unit_vector(seed));
-                    const V3 sc = normalize(add(refl, fuzz));
-                    if (dot(sc, n) > 0.0f) sd = sc;
-                } else if (mtype == 2u) {                // dielectric, shader.rchit:91-100,125-133
-                    const float eta = front ? (1.0f / m0.w) : m0.w;
-                    const float cos_t = dot(neg(d), n);
-                    bool refracts = false;
-                    if (eta * __builtin_sqrtf(1.0f - cos_t * cos_t) <= 1.0f) {
-                        const float q = (1.0f - eta) / (1.0f + eta);
-                        const float r = q * q;
-                        const float refl = r + (1.0f - r) * pow5(1.0f - cos_t);
-                        refracts = refl < rnd(seed);
-                    }
-                    sd = refracts ? refract(d, n, eta) : reflect(d, n);
-                }
-                scatter = !(sd.x == 0.0f && sd.y == 0.0f && sd.z == 0.0f);  // shader.rchit:48
-            }
-            // ---- shader.rgen:77-88 ---------------------------------------------------------
-            bool done;
-            V3 col;
-            if (scatter) {
-                thr = mul(thr, att);
-                o = p;
-                d = normalize(sd);
-                a = dot(d, d);
-                depth++;
-                done = depth >= P.max_depth;
-                col = mul(thr, v3(0.0f, 0.0f, 0.0f));   // depth exhausted: light stays 0 (Q6)
-            } else {
-                done = true;
-                col = mul(thr, att);
-            }
-            if (done) {
-                sum_x += double(col.x);
-                sum_y += double(col.y);
-                sum_z += double(col.z);
-                s++;
-                state = ST_NEED_SAMPLE;
-            }
+            if (!shade(P, ps, bi, best, o, d)) st = ST_NEED_SAMPLE;
         }
     }
-    // ---- statistics: the atomic optimizer folds these into one add per wave ----------------
+    atomicAdd(&P.counters->segments, (unsigned long long)n_seg);
+    atomicAdd(&P.counters->samples, (unsigned long long)n_smp);
+    if (COUNT) atomicAdd(&P.counters->sphere_tests, (unsigned long long)n_sph);
+}
+
+// ---------------------------------------------------------------------------------------------
+// LBVH kernel, classic form: one segment per lane per loop iteration; the wave's walk loop runs
+// until its longest walk ends. Stamp slots: 0 refill+sample start, 1 ray setup (big spheres),
+// 2 LBVH walk, 3 shading, 7 other.
+// ---------------------------------------------------------------------------------------------
+template <bool COUNT>
+__device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const float4* __restrict__ nodes4,
+                                             const float4* __restrict__ leaf4,
+                                             const uint32_t* __restrict__ leaf_ids) {
+    const uint32_t lane = lane_id();
+    const Camera cam = load_camera(P);
+    uint32_t st = ST_NEED_PIXEL;
+    Path ps{};
+    Ray r{};
+    uint32_t n_seg = 0, n_smp = 0, n_box = 0, n_sph = 0;
+    STAMP_DECL;
+    for (;;) {
+        STAMP(0);
+        refill(P, lane, st, ps);
+        if (st == ST_NEED_SAMPLE) {
+            if (start_sample(P, cam, ps, r.o, r.d)) { st = ST_TRACING; n_smp++; }
+            else st = ST_NEED_PIXEL;
+        }
+        if (__ballot(st == ST_NEED_PIXEL)) continue;   // refill before the next trace
+        if (!__ballot(st == ST_TRACING)) break;         // every lane retired
+        STAMP(1);
+        if (st == ST_TRACING) setup_ray(P, r, n_sph);
+        STAMP(2);
+        if (st == ST_TRACING)
+            while (r.ni != END) visit_node<COUNT>(P, nodes4, leaf4, leaf_ids, r, n_box, n_sph);
+        STAMP(3);
+        if (st == ST_TRACING) {
+            n_seg++;
+            if (!shade(P, ps, r.bi, r.best, r.o, r.d)) st = ST_NEED_SAMPLE;
+        }
+    }
+    STAMP_FLUSH;
+    atomicAdd(&P.counters->segments, (unsigned long long)n_seg);
+    atomicAdd(&P.counters->samples, (unsigned long long)n_smp);
+    if (COUNT) {
+        atomicAdd(&P.counters->box_tests, (unsigned long long)n_box);
+        atomicAdd(&P.counters->sphere_tests, (unsigned long long)n_sph);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// LBVH kernel: unified per-lane state machine with threshold compaction.
+//   traverse phase: every TRAVERSING lane visits one node per iteration; a lane whose walk ends
+//                   becomes READY and idles;
+//   service phase:  entered once fewer than P.compact lanes are still traversing (or none):
+//                   READY lanes shade together and set up their next segment, lanes whose
+//                   sample ended start the next sample, lanes whose pixel ended take new pixels.
+// So the wave no longer waits for its longest walk every segment: the expensive shading code runs
+// for many lanes at once and the short walks of one group overlap the long walks of another.
+// ---------------------------------------------------------------------------------------------
+template <bool COUNT>
+__device__ __forceinline__ void lbvh_compact(const rt::TraceParams& P, const float4* __restrict__ nodes4,
+                                             const float4* __restrict__ leaf4,
+                                             const uint32_t* __restrict__ leaf_ids);
+
+template <bool LDS, bool COUNT>
+__global__ __launch_bounds__(256, RT_TRACE_WAVES_PER_SIMD) void rt_trace_lbvh_kernel(const rt::TraceParams P) {
+    extern __shared__ float4 lds[];
+    const float4* nodes4 = reinterpret_cast<const float4*>(P.nodes);
+    const float4* leaf4 = reinterpret_cast<const float4*>(P.leaf_geom);
+    const uint32_t* leaf_ids = P.leaf_ids;
+    if (LDS) {  // stage nodes, leaf spheres and leaf ids once per (persistent) block
+        const uint32_t n_node4 = 2u * P.n_nodes, n_leaf4 = P.n_leaf, n_id4 = (P.n_leaf + 3u) / 4u;
+        for (uint32_t i = threadIdx.x; i < n_node4; i += blockDim.x) lds[i] = nodes4[i];
+        for (uint32_t i = threadIdx.x; i < n_leaf4; i += blockDim.x) lds[n_node4 + i] = leaf4[i];
+        const uint4* ids4 = reinterpret_cast<const uint4*>(P.leaf_ids);
+        for (uint32_t i = threadIdx.x; i < n_id4; i += blockDim.x) {
+            const uint4 v = ids4[i];
+            lds[n_node4 + n_leaf4 + i] = make_float4(__uint_as_float(v.x), __uint_as_float(v.y),
+                                                     __uint_as_float(v.z), __uint_as_float(v.w));
+        }
+        __syncthreads();
+        nodes4 = lds;
+        leaf4 = lds + n_node4;
+        leaf_ids = reinterpret_cast<const uint32_t*>(lds + n_node4 + n_leaf4);
+    }
+    if (P.compact == 0u) lbvh_classic<COUNT>(P, nodes4, leaf4, leaf_ids);
+    else lbvh_compact<COUNT>(P, nodes4, leaf4, leaf_ids);
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void lbvh_compact(const rt::TraceParams& P, const float4* __restrict__ nodes4,
+                                             const float4* __restrict__ leaf4,
+                                             const uint32_t* __restrict__ leaf_ids) {
+    const uint32_t lane = lane_id();
+    const Camera cam = load_camera(P);
+    uint32_t st = ST_NEED_PIXEL;
+    Path ps{};
+    Ray r{};
+    r.ni = END;
+    uint32_t n_seg = 0, n_smp = 0, n_box = 0, n_sph = 0;
+    const uint32_t thresh = P.compact;
+
+    for (;;) {
+        // ---- service phase: bring every live lane back to TRAVERSING -------------------------
+        for (;;) {
+            if (st == ST_READY) {
+                n_seg++;
+                if (shade(P, ps, r.bi, r.best, r.o, r.d)) {
+                    setup_ray(P, r, n_sph);
+                    st = ST_TRACING;
+                } else {
+                    st = ST_NEED_SAMPLE;
+                }
+            }
+            if (st == ST_NEED_SAMPLE) {
+                if (start_sample(P, cam, ps, r.o, r.d)) {
+                    n_smp++;
+                    setup_ray(P, r, n_sph);
+                    st = ST_TRACING;
+                } else {
+                    st = ST_NEED_PIXEL;
+                }
+            }
+            if (!__ballot(st == ST_NEED_PIXEL)) break;
+            refill(P, lane, st, ps);
+        }
+        if (!__ballot(st == ST_TRACING)) break;   // every lane retired
+        // ---- traverse phase ---------------------------------------------------------------------
+        for (;;) {
+            if (st == ST_TRACING) {
+                if (r.ni != END) visit_node<COUNT>(P, nodes4, leaf4, leaf_ids, r, n_box, n_sph);
+                if (r.ni == END) st = ST_READY;
+            }
+            const unsigned long long trav = __ballot(st == ST_TRACING);
+            if (__popcll(trav) < thresh && (trav == 0 || __ballot(st == ST_READY))) break;
+        }
+    }
     atomicAdd(&P.counters->segments, (unsigned long long)n_seg);
     atomicAdd(&P.counters->samples, (unsigned long long)n_smp);
     if (COUNT) {
@@ -362,23 +596,28 @@ __global__ void rt_debug_math_kernel(int op, const float* __restrict__ in, float
 // ---- host-callable launchers (rt_api.cpp) ---------------------------------------------------
 namespace rt {
 
-hipError_t launch_trace(const TraceParams& P, uint32_t accel, bool count, int grid, hipStream_t st) {
-    dim3 g(grid), b(256);
-    if (accel == ACCEL_BRUTE) {
-        if (count) hipLaunchKernelGGL((rt_trace_kernel<ACCEL_BRUTE, true>), g, b, 0, st, P);
-        else hipLaunchKernelGGL((rt_trace_kernel<ACCEL_BRUTE, false>), g, b, 0, st, P);
-    } else {
-        if (count) hipLaunchKernelGGL((rt_trace_kernel<ACCEL_LBVH, true>), g, b, 0, st, P);
-        else hipLaunchKernelGGL((rt_trace_kernel<ACCEL_LBVH, false>), g, b, 0, st, P);
+static const void* pick(uint32_t accel, bool count) {
+    switch (accel) {
+        case ACCEL_BRUTE:
+            return count ? reinterpret_cast<const void*>(rt_trace_brute_kernel<true>)
+                         : reinterpret_cast<const void*>(rt_trace_brute_kernel<false>);
+        case ACCEL_LBVH_LDS:
+            return count ? reinterpret_cast<const void*>(rt_trace_lbvh_kernel<true, true>)
+                         : reinterpret_cast<const void*>(rt_trace_lbvh_kernel<true, false>);
+        default:
+            return count ? reinterpret_cast<const void*>(rt_trace_lbvh_kernel<false, true>)
+                         : reinterpret_cast<const void*>(rt_trace_lbvh_kernel<false, false>);
     }
-    return hipGetLastError();
 }
 
-hipError_t trace_occupancy(uint32_t accel, bool count, int* blocks_per_cu) {
-    const void* f;
-    if (accel == ACCEL_BRUTE) f = count ? (const void*)rt_trace_kernel<ACCEL_BRUTE, true> : (const void*)rt_trace_kernel<ACCEL_BRUTE, false>;
-    else f = count ? (const void*)rt_trace_kernel<ACCEL_LBVH, true> : (const void*)rt_trace_kernel<ACCEL_LBVH, false>;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, f, 256, 0);
+hipError_t launch_trace(const TraceParams& P, uint32_t accel, bool count, int grid, size_t lds_bytes,
+                        hipStream_t st) {
+    void* args[] = {const_cast<TraceParams*>(&P)};
+    return hipLaunchKernel(pick(accel, count), dim3(grid), dim3(256), args, lds_bytes, st);
+}
+
+hipError_t trace_occupancy(uint32_t accel, bool count, size_t lds_bytes, int* blocks_per_cu) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, pick(accel, count), 256, lds_bytes);
 }
 
 hipError_t launch_scatter_rows(const float* src_acc, const uint8_t* src_px, const uint32_t* rows,

@@ -109,6 +109,7 @@ EXPORTS = {
     "rt_render": (_I, [_P, _U32, _P, _U32, _P, _P, ctypes.POINTER(Options), ctypes.POINTER(Stats)]),
     "rt_store_ppm": (_I, [ctypes.c_char_p, _P, _U32, _U32]),
     "rt_debug_math": (_I, [_I, _I, _P, _P, _U32]),
+    "rt_debug_stamps": (_I, [_P, _P]),
     "ray_trace": (None, [_U32, ctypes.c_bool, _U32, _U32, _U32]),
 }
 
