@@ -27,6 +27,7 @@ namespace rt {
 hipError_t launch_trace(const TraceParams& P, uint32_t accel, bool count, int grid, size_t lds_bytes,
                         hipStream_t st);
 hipError_t trace_occupancy(uint32_t accel, bool count, size_t lds_bytes, int* blocks_per_cu);
+uint32_t block_size(uint32_t accel);
 hipError_t launch_scatter_rows(const float* src_acc, const uint8_t* src_px, const uint32_t* rows,
                                uint32_t n_rows, uint32_t width, float* dst_acc, uint8_t* dst_px,
                                hipStream_t st);
@@ -40,12 +41,17 @@ struct rt_context {
     std::vector<void*> scene_allocs;
     rt::Counters* counters = nullptr;   // device
     hipStream_t last_stream = nullptr;
-    int occ[3][2] = {{0, 0}, {0, 0}, {0, 0}};   // [accel-1][count], blocks per CU
+    // occupancy cache per kernel (accel id 1..5) and count flag, valid for occ_lds bytes of LDS
+    int occ[6][2] = {};
+    size_t occ_lds[6][2] = {};
     size_t lds_bytes = 0;                        // LBVH_LDS staging size of the current scene
+    size_t lds2_bytes = 0;                       // LBVH2_LDS staging size (0: does not fit)
 };
 
 // LBVH staged in LDS when its image is at most this large (keeps >= 6 blocks per CU).
 static constexpr size_t kMaxLdsBvhBytes = 24 * 1024;
+// Ordered-walk LBVH staged in LDS up to this size (plus the per-lane stacks).
+static constexpr size_t kMaxLdsBvh2Bytes = 40 * 1024;
 
 namespace {
 
@@ -256,12 +262,8 @@ int rt_context_create(int device, rt_context** out) {
     RT_HIP(hipMalloc(&c, sizeof(rt::Counters)));
     RT_HIP(hipMemset(c, 0, sizeof(rt::Counters)));
     ctx->counters = static_cast<rt::Counters*>(c);
-    for (uint32_t acc = 1; acc <= 2; acc++)
-        for (int cnt = 0; cnt < 2; cnt++) {
-            int b = 0;
-            RT_HIP(rt::trace_occupancy(acc, cnt != 0, 0, &b));
-            ctx->occ[acc - 1][cnt] = std::max(1, b);
-        }
+    for (int a = 0; a < 6; a++)
+        for (int cnt = 0; cnt < 2; cnt++) ctx->occ_lds[a][cnt] = ~size_t(0);
     *out = ctx.release();
     return RT_OK;
 }
@@ -319,12 +321,12 @@ int rt_set_scene(rt_context* ctx, const Sphere* spheres, uint32_t count, void* s
         while (bvh.leaf_ids.size() % 4) bvh.leaf_ids.push_back(0u);
         const size_t lds = size_t(2 * d.n_nodes + d.n_leaf + (d.n_leaf + 3) / 4) * 16;
         ctx->lds_bytes = (d.n_nodes && lds <= kMaxLdsBvhBytes) ? lds : 0;
-        if (ctx->lds_bytes)
-            for (int cnt = 0; cnt < 2; cnt++) {
-                int b = 0;
-                RT_HIP(rt::trace_occupancy(rt::ACCEL_LBVH_LDS, cnt != 0, ctx->lds_bytes, &b));
-                ctx->occ[rt::ACCEL_LBVH_LDS - 1][cnt] = std::max(1, b);
-            }
+        d.n_nodes2 = uint32_t(bvh.nodes2.size());
+        d.root2 = bvh.root2;
+        d.depth2 = bvh.depth2;
+        if (int rc = upload(ctx, bvh.nodes2, &d.nodes2, st)) return rc;
+        const size_t lds2 = size_t(4 * d.n_nodes2 + d.n_leaf + (d.n_leaf + 3) / 4) * 16;
+        ctx->lds2_bytes = (d.n_leaf && lds2 <= kMaxLdsBvh2Bytes) ? lds2 : 0;
         if (int rc = upload(ctx, bvh.nodes, &d.nodes, st)) return rc;
         if (int rc = upload(ctx, bvh.leaf_geom, &d.leaf_geom, st)) return rc;
         if (int rc = upload(ctx, bvh.leaf_ids, &d.leaf_ids, st)) return rc;
@@ -349,8 +351,24 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     rt_options o;
     std::memset(&o, 0, sizeof(o));
     if (opt) o = *opt;
-    uint32_t accel = o.accel == RT_ACCEL_BRUTE ? rt::ACCEL_BRUTE
-                     : (ctx->lds_bytes ? rt::ACCEL_LBVH_LDS : rt::ACCEL_LBVH);
+    // reserved[1] (internal, A/B only): LBVH walk form, 0 = default (stackless escape-link),
+    // 2 = ordered two-wide walk with an LDS stack (slower on the canonical scene)
+    const bool escape_walk = o.reserved[1] != 2u;
+    uint32_t accel;
+    size_t lds = 0;
+    const rt::DeviceScene& ds = ctx->scene;
+    if (o.accel == RT_ACCEL_BRUTE) {
+        accel = rt::ACCEL_BRUTE;
+    } else if (escape_walk) {
+        accel = ctx->lds_bytes ? rt::ACCEL_LBVH_LDS : rt::ACCEL_LBVH;
+        lds = ctx->lds_bytes;
+    } else {
+        const uint32_t blk = rt::block_size(rt::ACCEL_LBVH2);
+        const size_t stack = size_t(blk) * std::max(1u, ds.depth2) * 4u;
+        accel = ctx->lds2_bytes ? rt::ACCEL_LBVH2_LDS : rt::ACCEL_LBVH2;
+        lds = (ctx->lds2_bytes ? ctx->lds2_bytes : 0) + stack;
+        if (lds > 160u * 1024u) return fail(RT_ERR_INVALID_ARGUMENT, "LBVH too deep for the LDS stack");
+    }
     if (o.accel > RT_ACCEL_LBVH) return fail(RT_ERR_INVALID_ARGUMENT, "unknown accel");
     if (o.seed_mode > RT_SEED_LAUNCH_LOCAL) return fail(RT_ERR_INVALID_ARGUMENT, "unknown seed_mode");
     if (o.rng_mode > RT_RNG_SAMPLE_COUNTER) return fail(RT_ERR_INVALID_ARGUMENT, "unknown rng_mode");
@@ -382,6 +400,10 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     P.big_ids = d.big_ids;
     P.nodes = d.n_nodes ? d.nodes : nullptr;
     P.n_nodes = d.n_nodes;
+    P.nodes2 = d.nodes2;   // null when the tree is a single leaf (root2 is then a leaf reference)
+    P.n_nodes2 = d.n_nodes2;
+    P.root2 = d.root2;
+    P.stack_depth = d.depth2;
     P.n_leaf = d.n_leaf;
     P.leaf_geom = d.leaf_geom;
     P.leaf_ids = d.leaf_ids;
@@ -389,8 +411,7 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     // 2.75 r + 1.15e-3 t beyond its reported t.
     P.cull_abs = 3.0f * d.small_rmax + 1e-3f;
     P.cull_rel = 2e-3f;
-    // reserved[1]: LBVH loop form, 0 = classic (default), 1..64 = compaction threshold
-    P.compact = (o.reserved[1] <= 64u) ? o.reserved[1] : 0u;
+
     P.accum = accum;
     P.out = reinterpret_cast<uint32_t*>(out);
     P.counters = ctx->counters;
@@ -398,11 +419,17 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     DeviceGuard g(ctx->device);
     hipStream_t st = static_cast<hipStream_t>(stream);
     RT_HIP(hipMemsetAsync(ctx->counters, 0, sizeof(rt::Counters), st));
-    const uint64_t lanes_needed = P.n_units;
-    const uint64_t full = uint64_t(ctx->cu_count) * ctx->occ[accel - 1][count ? 1 : 0];
-    const uint64_t by_work = (lanes_needed + 255u) / 256u;
+    const int ci = count ? 1 : 0;
+    if (ctx->occ_lds[accel][ci] != lds) {
+        int b = 0;
+        RT_HIP(rt::trace_occupancy(accel, count, lds, &b));
+        ctx->occ[accel][ci] = std::max(1, b);
+        ctx->occ_lds[accel][ci] = lds;
+    }
+    const uint64_t blk = rt::block_size(accel);
+    const uint64_t full = uint64_t(ctx->cu_count) * ctx->occ[accel][ci];
+    const uint64_t by_work = (uint64_t(P.n_units) + blk - 1) / blk;
     const int grid = int(std::max<uint64_t>(1, std::min(full, by_work)));
-    const size_t lds = accel == rt::ACCEL_LBVH_LDS ? ctx->lds_bytes : 0;
     RT_HIP(rt::launch_trace(P, accel, count, grid, lds, st));
     ctx->last_stream = st;
     return RT_OK;
@@ -441,6 +468,7 @@ int rt_debug_stamps(rt_context* ctx, uint64_t* out8) {
     rt::Counters c;
     RT_HIP(hipMemcpy(&c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
     for (int k = 0; k < 8; k++) out8[k] = c.stamp[k];
+    if (!c.stamp[0] && !c.stamp[1]) out8[6] = c.wave_iters;   // non-stamp builds: walk iterations
     return RT_OK;
 }
 

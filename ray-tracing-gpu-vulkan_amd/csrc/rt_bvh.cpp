@@ -11,7 +11,8 @@
 //   2. small-sphere centers quantised to 10 bits per axis inside their bounds, 30-bit Morton
 //      codes, stable sort by (code, index).
 //   3. recursive split at the highest differing Morton bit (the radix-tree split; equal codes
-//      split in the middle), leaves of at most kLeafMax spheres.
+//      split in the middle), leaves of at most kLeafMax spheres, each stored in kLeafMax slots
+//      (dummy-padded) so the device issues a leaf's four loads together.
 //   4. node bounds = exact float min/max of the member spheres' AABBs (center -/+ radius), so
 //      every node box contains its spheres' AABBs bit-exactly (the traversal's exactness
 //      argument, DESIGN.md §4.3, needs this).
@@ -42,6 +43,8 @@ struct Prim {
     uint32_t id;
 };
 
+// Leaves hold 1..kLeafMax spheres chosen by the radix split (spatially tight), stored in
+// kLeafMax slots padded with never-hit dummies so the device loads a leaf as 4 records at once.
 struct Builder {
     const Sphere* sph;
     const std::vector<Prim>& prims;
@@ -54,8 +57,8 @@ struct Builder {
             const rt_vec4& g = sph[prims[i].id].geometry;
             const float c[3] = {g.x, g.y, g.z};
             for (int k = 0; k < 3; k++) {
-                bmin[k] = std::min(bmin[k], c[k] - g.w);
-                bmax[k] = std::max(bmax[k], c[k] + g.w);
+                bmin[k] = std::min(bmin[k], c[k] - g.w);   // the sphere's AABB, exactly as the
+                bmax[k] = std::max(bmax[k], c[k] + g.w);   // traversal test computes it
             }
         }
     }
@@ -73,7 +76,9 @@ struct Builder {
         return s + 1;
     }
 
-    void build(uint32_t lo, uint32_t hi) {
+    // Returns the reference of the subtree [lo, hi) in the two-wide layout (inner nodes emitted
+    // depth first) and its height in inner nodes; also emits the escape-link node list.
+    uint32_t build(uint32_t lo, uint32_t hi, float* bmin_out, float* bmax_out, uint32_t* height) {
         const uint32_t me = uint32_t(out.nodes.size());
         out.nodes.push_back(BvhNode{});
         float bmin[3], bmax[3];
@@ -81,22 +86,44 @@ struct Builder {
         BvhNode n;
         n.lox = bmin[0]; n.loy = bmin[1]; n.loz = bmin[2];
         n.hix = bmax[0]; n.hiy = bmax[1]; n.hiz = bmax[2];
+        for (int k = 0; k < 3; k++) { bmin_out[k] = bmin[k]; bmax_out[k] = bmax[k]; }
+        uint32_t ref;
         if (hi - lo <= kLeafMax) {
             const uint32_t first = uint32_t(out.leaf_geom.size());
-            for (uint32_t i = lo; i < hi; i++) {
-                const rt_vec4& g = sph[prims[i].id].geometry;
-                out.leaf_geom.push_back(GeomRec{g.x, g.y, g.z, g.w * g.w});
-                out.leaf_ids.push_back(prims[i].id);
+            for (uint32_t i = lo; i < lo + kLeafMax; i++) {
+                if (i < hi) {
+                    const rt_vec4& g = sph[prims[i].id].geometry;
+                    out.leaf_geom.push_back(GeomRec{g.x, g.y, g.z, g.w});   // radius, not r^2
+                    out.leaf_ids.push_back(prims[i].id);
+                } else {   // dummy: 1e19 below the scene, radius 0 -> never reports
+                    out.leaf_geom.push_back(GeomRec{0.0f, -1e19f, 0.0f, 0.0f});
+                    out.leaf_ids.push_back(0xffffffffu);
+                }
             }
             n.first_count = (first << 4) | (hi - lo);
+            ref = kLeafFlag | (first << 3) | (hi - lo);
+            *height = 0;
         } else {
             const uint32_t s = split(lo, hi);
-            build(lo, s);
-            build(s, hi);
+            const uint32_t me2 = uint32_t(out.nodes2.size());
+            out.nodes2.push_back(Bvh2Node{});
+            float l0[3], h0[3], l1[3], h1[3];
+            uint32_t ht0 = 0, ht1 = 0;
+            const uint32_t c0 = build(lo, s, l0, h0, &ht0);
+            const uint32_t c1 = build(s, hi, l1, h1, &ht1);
             n.first_count = 0;
+            Bvh2Node m;
+            m.l0x = l0[0]; m.l0y = l0[1]; m.l0z = l0[2]; m.c0 = c0;
+            m.h0x = h0[0]; m.h0y = h0[1]; m.h0z = h0[2]; m.pad0 = 0;
+            m.l1x = l1[0]; m.l1y = l1[1]; m.l1z = l1[2]; m.c1 = c1;
+            m.h1x = h1[0]; m.h1y = h1[1]; m.h1z = h1[2]; m.pad1 = 0;
+            out.nodes2[me2] = m;
+            ref = me2;
+            *height = 1 + std::max(ht0, ht1);
         }
         n.escape = uint32_t(out.nodes.size());  // first node after this subtree
         out.nodes[me] = n;
+        return ref;
     }
 };
 
@@ -105,6 +132,7 @@ struct Builder {
 void build_lbvh_host(const Sphere* sph, uint32_t n, HostBvh& out) {
     out = HostBvh{};
     if (n == 0) return;
+    if (n >= (1u << 27)) return;   // leaf references hold 28-bit slot indices
     // 1. big spheres
     std::vector<float> radii(n);
     for (uint32_t i = 0; i < n; i++) radii[i] = sph[i].geometry.w;
@@ -149,7 +177,8 @@ void build_lbvh_host(const Sphere* sph, uint32_t n, HostBvh& out) {
     // 3-4. hierarchy in depth-first order
     out.nodes.reserve(2 * prims.size());
     Builder b{sph, prims, out};
-    b.build(0, uint32_t(prims.size()));
+    float bmin[3], bmax[3];
+    out.root2 = b.build(0, uint32_t(prims.size()), bmin, bmax, &out.depth2);
     for (BvhNode& nd : out.nodes)
         if (nd.escape >= out.nodes.size()) nd.escape = 0xffffffffu;
 }

@@ -12,9 +12,12 @@ namespace rt {
 struct HostBvh {
     std::vector<uint32_t> big_ids;    // spheres tested exhaustively, ascending index
     std::vector<BvhNode> nodes;       // depth-first, escape links
-    std::vector<GeomRec> leaf_geom;   // small spheres in leaf order
+    std::vector<GeomRec> leaf_geom;   // small spheres in leaf order: center, RADIUS (4 per leaf)
     std::vector<uint32_t> leaf_ids;   // original index per leaf slot
     float small_rmax = 0.0f;          // largest radius inside the tree (traversal slack)
+    std::vector<Bvh2Node> nodes2;     // ordered-walk layout over the same leaves
+    uint32_t root2 = 0;               // root reference for nodes2
+    uint32_t depth2 = 0;              // max inner nodes on a root-to-leaf path
 };
 
 void build_lbvh_host(const Sphere* spheres, uint32_t n, HostBvh& out);

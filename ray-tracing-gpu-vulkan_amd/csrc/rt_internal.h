@@ -31,6 +31,18 @@ struct alignas(16) BvhNode {
     uint32_t first_count;        // leaf: first << 4 | count (count 1..15); inner: 0
 };
 
+// Two-wide LBVH node for the ordered (stack) walk, 64 B: both children's boxes, so one visit
+// tests two boxes and descends into the nearer hit child first (the farther one is pushed).
+// Child reference: bit 31 set = leaf, (first slot << 3) | count in the low bits; else the index
+// of an inner node.
+struct alignas(16) Bvh2Node {
+    float l0x, l0y, l0z; uint32_t c0;   // child 0: box lo, reference
+    float h0x, h0y, h0z; uint32_t pad0; // child 0: box hi
+    float l1x, l1y, l1z; uint32_t c1;   // child 1: box lo, reference
+    float h1x, h1y, h1z; uint32_t pad1; // child 1: box hi
+};
+constexpr uint32_t kLeafFlag = 0x80000000u;
+
 // Scene as resident in HBM (one allocation per context, rebuilt by rt_set_scene).
 struct DeviceScene {
     uint32_t n_spheres = 0;
@@ -46,10 +58,14 @@ struct DeviceScene {
     GeomRec* leaf_geom = nullptr;  // spheres permuted into leaf order (contiguous per leaf)
     uint32_t* leaf_ids = nullptr;  // original index of each leaf slot
     uint32_t n_leaf = 0;
+    Bvh2Node* nodes2 = nullptr;    // ordered-walk layout (same leaves)
+    uint32_t n_nodes2 = 0;
+    uint32_t root2 = 0;            // root reference (inner index or leaf reference)
+    uint32_t depth2 = 0;           // inner nodes on the longest root-to-leaf path (stack bound)
     float small_rmax = 0.0f;       // largest radius in the tree
 };
 
-enum : uint32_t { ACCEL_BRUTE = 1, ACCEL_LBVH = 2, ACCEL_LBVH_LDS = 3 };
+enum : uint32_t { ACCEL_BRUTE = 1, ACCEL_LBVH = 2, ACCEL_LBVH_LDS = 3, ACCEL_LBVH2 = 4, ACCEL_LBVH2_LDS = 5 };
 
 // Counters block (device memory, zeroed before each launch by the host).
 struct Counters {
@@ -59,6 +75,7 @@ struct Counters {
     unsigned long long samples;
     unsigned long long box_tests;
     unsigned long long sphere_tests;
+    unsigned long long wave_iters; // COUNT builds: sum over waves of walk-loop iterations
     unsigned long long stamp[8];   // diagnostic builds only (-DRT_STAMPS): cycles per phase
 };
 
@@ -87,12 +104,13 @@ struct TraceParams {
     const uint32_t* big_ids;
     const BvhNode* nodes;
     uint32_t n_nodes;
+    const Bvh2Node* nodes2;
+    uint32_t n_nodes2, root2, stack_depth;
     uint32_t n_leaf;               // spheres in the tree (leaf slots)
     const GeomRec* leaf_geom;
     const uint32_t* leaf_ids;
     float cull_abs;                // LBVH node-cull slack: best + cull_abs + cull_rel * best
     float cull_rel;
-    uint32_t compact;              // LBVH: service lanes once fewer than this many still traverse
     // outputs
     float* accum;                  // band_w * band_h * 4 floats
     uint32_t* out;                 // band_w * band_h packed rgba8

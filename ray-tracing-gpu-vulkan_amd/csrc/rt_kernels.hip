@@ -98,15 +98,14 @@ __device__ __forceinline__ void test_sphere(float cx, float cy, float cz, float 
     }
 }
 
-// As test_sphere, with the sphere index read from ids[slot] only when the quadratic reports
-// (LBVH leaves: the id is needed for the tie-break and the radius, both in the rare branch).
-template <bool TB>
-__device__ __forceinline__ void test_sphere_ids(float cx, float cy, float cz, float rr,
-                                                const float* __restrict__ radius,
-                                                const uint32_t* __restrict__ ids, uint32_t slot,
-                                                V3 o, V3 d, V3 inv, float a, float& best,
-                                                uint32_t& bi) {
-    const float ocx = o.x - cx, ocy = o.y - cy, ocz = o.z - cz;
+// LBVH leaf sphere: record = (center, radius); r^2 is formed here exactly as the host forms it
+// for brute force (one rounding), so results agree bit for bit. The sphere index is read from
+// ids[slot] only when the quadratic reports (tie-break and result), both in the rare branch.
+__device__ __forceinline__ void test_leaf_sphere(float4 sp, const uint32_t* __restrict__ ids,
+                                                 uint32_t slot, V3 o, V3 d, V3 inv, float a,
+                                                 float& best, uint32_t& bi) {
+    const float rr = sp.w * sp.w;
+    const float ocx = o.x - sp.x, ocy = o.y - sp.y, ocz = o.z - sp.z;
     const float b = __builtin_fmaf(ocz, d.z, __builtin_fmaf(ocy, d.y, ocx * d.x));
     const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - rr;
     const float D = __builtin_fmaf(b, b, -(a * c));
@@ -117,8 +116,7 @@ __device__ __forceinline__ void test_sphere_ids(float cx, float cy, float cz, fl
         const float t = (t1 >= T_MIN) ? t1 : t2;
         if (t >= T_MIN && t <= best) {
             const uint32_t id = ids[slot];
-            const bool better = TB ? (t < best || id < bi) : (t < best);
-            if (better && aabb_hit(cx, cy, cz, radius[id], o, inv)) {
+            if ((t < best || id < bi) && aabb_hit(sp.x, sp.y, sp.z, sp.w, o, inv)) {
                 best = t;
                 bi = id;
             }
@@ -321,6 +319,7 @@ struct Ray {
     uint32_t bi, ni;       // closest so far, next node (END = done)
 };
 constexpr uint32_t END = 0xffffffffu;
+constexpr uint32_t kLeafFlagD = 0x80000000u;
 
 // New segment: hoisted per-ray terms, the exhaustive big spheres, walk from the root.
 __device__ __forceinline__ void setup_ray(const rt::TraceParams& P, Ray& r, uint32_t& n_sph) {
@@ -334,10 +333,18 @@ __device__ __forceinline__ void setup_ray(const rt::TraceParams& P, Ray& r, uint
     typedef const __attribute__((address_space(4))) float* ConstF;
     const ConstU ids = (ConstU)(P.big_ids);
     const ConstF g = (ConstF)(P.geom);
-    for (uint32_t k = 0; k < P.n_big; ++k) {   // wave-uniform: scalar loads
-        const uint32_t id = ids[k];
-        test_sphere<true>(g[4 * id], g[4 * id + 1], g[4 * id + 2], g[4 * id + 3], P.radius, r.o, r.d,
-                          r.inv, r.a, id, r.best, r.bi);
+    for (uint32_t k0 = 0; k0 < P.n_big; k0 += 4) {   // wave-uniform: scalar loads, 4 at a time
+        uint32_t id[4];
+        float sp[16];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) id[j] = ids[min(k0 + j, P.n_big - 1)];
+#pragma unroll
+        for (uint32_t j = 0; j < 16; ++j) sp[j] = g[4 * id[j >> 2] + (j & 3)];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j)
+            if (k0 + j < P.n_big)
+                test_sphere<true>(sp[4 * j], sp[4 * j + 1], sp[4 * j + 2], sp[4 * j + 3], P.radius, r.o,
+                                  r.d, r.inv, r.a, id[j], r.best, r.bi);
     }
     n_sph += P.n_big;
     r.ni = P.nodes ? 0u : END;
@@ -364,16 +371,94 @@ __device__ __forceinline__ void visit_node(const rt::TraceParams& P, const float
     const float tfar = fminf(fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1)), limit);
     const bool hit = tnear <= __builtin_fmaf(fabsf(tfar), 4.8e-7f, tfar + r.tol);
     const uint32_t fc = __float_as_uint(n1.w);
-    if (hit && fc != 0u) {
-        const uint32_t first = fc >> 4, cnt = fc & 15u;
-        for (uint32_t j = 0; j < cnt; ++j) {
-            const float4 sp = leaf4[first + j];
-            test_sphere_ids<true>(sp.x, sp.y, sp.z, sp.w, P.radius, leaf_ids, first + j, r.o, r.d,
-                                  r.inv, r.a, r.best, r.bi);
-        }
-        if (COUNT) n_sph += cnt;
+    if (hit && fc != 0u) {   // leaf: always 4 slots (dummy-padded), loads issued together
+        const uint32_t first = fc >> 4;
+        const float4 s0 = leaf4[first], s1 = leaf4[first + 1], s2 = leaf4[first + 2], s3 = leaf4[first + 3];
+        test_leaf_sphere(s0, leaf_ids, first, r.o, r.d, r.inv, r.a, r.best, r.bi);
+        test_leaf_sphere(s1, leaf_ids, first + 1, r.o, r.d, r.inv, r.a, r.best, r.bi);
+        test_leaf_sphere(s2, leaf_ids, first + 2, r.o, r.d, r.inv, r.a, r.best, r.bi);
+        test_leaf_sphere(s3, leaf_ids, first + 3, r.o, r.d, r.inv, r.a, r.best, r.bi);
+        if (COUNT) n_sph += fc & 15u;
     }
     r.ni = (hit && fc == 0u) ? r.ni + 1u : __float_as_uint(n0.w);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Ordered LBVH walk (two-wide nodes, per-lane stack in LDS): each visit tests both children's
+// boxes with the same conservative slab test as visit_node, processes hit leaf children at once
+// (4-slot block), descends into the nearer hit inner child and pushes the farther one. Nearest-
+// first order finds the closest sphere early, so `best` culls the rest of the walk.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void leaf_block(uint32_t ref, const float4* __restrict__ leaf4,
+                                           const uint32_t* __restrict__ leaf_ids, Ray& r) {
+    const uint32_t first = (ref & ~kLeafFlagD) >> 3;
+    const float4 s0 = leaf4[first], s1 = leaf4[first + 1], s2 = leaf4[first + 2], s3 = leaf4[first + 3];
+    test_leaf_sphere(s0, leaf_ids, first, r.o, r.d, r.inv, r.a, r.best, r.bi);
+    test_leaf_sphere(s1, leaf_ids, first + 1, r.o, r.d, r.inv, r.a, r.best, r.bi);
+    test_leaf_sphere(s2, leaf_ids, first + 2, r.o, r.d, r.inv, r.a, r.best, r.bi);
+    test_leaf_sphere(s3, leaf_ids, first + 3, r.o, r.d, r.inv, r.a, r.best, r.bi);
+}
+
+__device__ __forceinline__ float slab_near(float4 lo, float4 hi, const Ray& r, float& tfar_out) {
+    const float tx0 = __builtin_fmaf(lo.x, r.inv.x, -r.oi.x), tx1 = __builtin_fmaf(hi.x, r.inv.x, -r.oi.x);
+    const float ty0 = __builtin_fmaf(lo.y, r.inv.y, -r.oi.y), ty1 = __builtin_fmaf(hi.y, r.inv.y, -r.oi.y);
+    const float tz0 = __builtin_fmaf(lo.z, r.inv.z, -r.oi.z), tz1 = __builtin_fmaf(hi.z, r.inv.z, -r.oi.z);
+    tfar_out = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+    return fmaxf(fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1)), T_MIN);
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void walk_ordered(const rt::TraceParams& P, const float4* __restrict__ nodes4,
+                                             const float4* __restrict__ leaf4,
+                                             const uint32_t* __restrict__ leaf_ids,
+                                             uint32_t* __restrict__ stk, uint32_t stride, Ray& r,
+                                             uint32_t& n_box, uint32_t& n_sph) {
+    if (P.n_leaf == 0) return;   // no small spheres: nothing to walk
+    uint32_t cur = P.root2;
+    if (cur & kLeafFlagD) {   // the whole tree is one leaf
+        leaf_block(cur, leaf4, leaf_ids, r);
+        if (COUNT) n_sph += cur & 7u;
+        return;
+    }
+    uint32_t sp = 0;
+    for (;;) {
+        const float4 a0 = nodes4[4 * cur], a1 = nodes4[4 * cur + 1];
+        const float4 b0 = nodes4[4 * cur + 2], b1 = nodes4[4 * cur + 3];
+        if (COUNT) n_box += 2;
+        const float limit = fminf(__builtin_fmaf(r.best, P.cull_rel, r.best + P.cull_abs), 10000.0f);
+        float tf0, tf1;
+        const float tn0 = slab_near(a0, a1, r, tf0);
+        const float tn1 = slab_near(b0, b1, r, tf1);
+        tf0 = fminf(tf0, limit);
+        tf1 = fminf(tf1, limit);
+        bool hit0 = tn0 <= __builtin_fmaf(fabsf(tf0), 4.8e-7f, tf0 + r.tol);
+        bool hit1 = tn1 <= __builtin_fmaf(fabsf(tf1), 4.8e-7f, tf1 + r.tol);
+        const uint32_t c0 = __float_as_uint(a0.w), c1 = __float_as_uint(b0.w);
+        // hit leaf children: test their spheres now
+        uint32_t lp0 = (hit0 && (c0 & kLeafFlagD)) ? c0 : 0u;
+        uint32_t lp1 = (hit1 && (c1 & kLeafFlagD)) ? c1 : 0u;
+        hit0 = hit0 && !(c0 & kLeafFlagD);
+        hit1 = hit1 && !(c1 & kLeafFlagD);
+        if (lp0 == 0u) { lp0 = lp1; lp1 = 0u; }
+        while (lp0) {
+            leaf_block(lp0, leaf4, leaf_ids, r);
+            if (COUNT) n_sph += lp0 & 7u;
+            lp0 = lp1;
+            lp1 = 0u;
+        }
+        if (hit0 && hit1) {
+            const bool first0 = tn0 <= tn1;
+            stk[sp * stride] = first0 ? c1 : c0;
+            ++sp;
+            cur = first0 ? c0 : c1;
+        } else if (hit0 || hit1) {
+            cur = hit0 ? c0 : c1;
+        } else {
+            if (sp == 0) break;
+            --sp;
+            cur = stk[sp * stride];
+        }
+    }
 }
 
 #ifndef RT_TRACE_WAVES_PER_SIMD
@@ -430,6 +515,7 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
     Path ps{};
     Ray r{};
     uint32_t n_seg = 0, n_smp = 0, n_box = 0, n_sph = 0;
+    unsigned long long wave_iters = 0;
     STAMP_DECL;
     for (;;) {
         STAMP(0);
@@ -443,8 +529,14 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
         STAMP(1);
         if (st == ST_TRACING) setup_ray(P, r, n_sph);
         STAMP(2);
+        const uint32_t box0 = n_box;
         if (st == ST_TRACING)
             while (r.ni != END) visit_node<COUNT>(P, nodes4, leaf4, leaf_ids, r, n_box, n_sph);
+        if (COUNT) {   // wave iterations of this walk = the longest lane walk
+            uint32_t m = n_box - box0;
+            for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor(m, off));
+            if (lane == 0) wave_iters += m;
+        }
         STAMP(3);
         if (st == ST_TRACING) {
             n_seg++;
@@ -457,23 +549,9 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
     if (COUNT) {
         atomicAdd(&P.counters->box_tests, (unsigned long long)n_box);
         atomicAdd(&P.counters->sphere_tests, (unsigned long long)n_sph);
+        if (lane == 0) atomicAdd(&P.counters->wave_iters, wave_iters);
     }
 }
-
-// ---------------------------------------------------------------------------------------------
-// LBVH kernel: unified per-lane state machine with threshold compaction.
-//   traverse phase: every TRAVERSING lane visits one node per iteration; a lane whose walk ends
-//                   becomes READY and idles;
-//   service phase:  entered once fewer than P.compact lanes are still traversing (or none):
-//                   READY lanes shade together and set up their next segment, lanes whose
-//                   sample ended start the next sample, lanes whose pixel ended take new pixels.
-// So the wave no longer waits for its longest walk every segment: the expensive shading code runs
-// for many lanes at once and the short walks of one group overlap the long walks of another.
-// ---------------------------------------------------------------------------------------------
-template <bool COUNT>
-__device__ __forceinline__ void lbvh_compact(const rt::TraceParams& P, const float4* __restrict__ nodes4,
-                                             const float4* __restrict__ leaf4,
-                                             const uint32_t* __restrict__ leaf_ids);
 
 template <bool LDS, bool COUNT>
 __global__ __launch_bounds__(256, RT_TRACE_WAVES_PER_SIMD) void rt_trace_lbvh_kernel(const rt::TraceParams P) {
@@ -496,63 +574,78 @@ __global__ __launch_bounds__(256, RT_TRACE_WAVES_PER_SIMD) void rt_trace_lbvh_ke
         leaf4 = lds + n_node4;
         leaf_ids = reinterpret_cast<const uint32_t*>(lds + n_node4 + n_leaf4);
     }
-    if (P.compact == 0u) lbvh_classic<COUNT>(P, nodes4, leaf4, leaf_ids);
-    else lbvh_compact<COUNT>(P, nodes4, leaf4, leaf_ids);
+    lbvh_classic<COUNT>(P, nodes4, leaf4, leaf_ids);
 }
 
-template <bool COUNT>
-__device__ __forceinline__ void lbvh_compact(const rt::TraceParams& P, const float4* __restrict__ nodes4,
-                                             const float4* __restrict__ leaf4,
-                                             const uint32_t* __restrict__ leaf_ids) {
+// ---------------------------------------------------------------------------------------------
+// LBVH kernel, ordered walk. Dynamic LDS: [staged nodes2 | leaf spheres | leaf ids] (LDS
+// variant only) followed by the per-lane stacks, stack_depth words per lane, lane-interleaved.
+// ---------------------------------------------------------------------------------------------
+template <bool LDS, bool COUNT, uint32_t BLOCK>
+__global__ __launch_bounds__(BLOCK, RT_TRACE_WAVES_PER_SIMD) void rt_trace_lbvh2_kernel(const rt::TraceParams P) {
+    extern __shared__ float4 lds[];
+    const float4* nodes4 = reinterpret_cast<const float4*>(P.nodes2);
+    const float4* leaf4 = reinterpret_cast<const float4*>(P.leaf_geom);
+    const uint32_t* leaf_ids = P.leaf_ids;
+    uint32_t staged4 = 0;
+    if (LDS) {
+        const uint32_t n_node4 = 4u * P.n_nodes2, n_leaf4 = P.n_leaf, n_id4 = (P.n_leaf + 3u) / 4u;
+        for (uint32_t i = threadIdx.x; i < n_node4; i += BLOCK) lds[i] = nodes4[i];
+        for (uint32_t i = threadIdx.x; i < n_leaf4; i += BLOCK) lds[n_node4 + i] = leaf4[i];
+        const uint4* ids4 = reinterpret_cast<const uint4*>(P.leaf_ids);
+        for (uint32_t i = threadIdx.x; i < n_id4; i += BLOCK) {
+            const uint4 v = ids4[i];
+            lds[n_node4 + n_leaf4 + i] = make_float4(__uint_as_float(v.x), __uint_as_float(v.y),
+                                                     __uint_as_float(v.z), __uint_as_float(v.w));
+        }
+        __syncthreads();
+        nodes4 = lds;
+        leaf4 = lds + n_node4;
+        leaf_ids = reinterpret_cast<const uint32_t*>(lds + n_node4 + n_leaf4);
+        staged4 = n_node4 + n_leaf4 + n_id4;
+    }
+    uint32_t* stk = reinterpret_cast<uint32_t*>(lds + staged4) + threadIdx.x;
+
     const uint32_t lane = lane_id();
     const Camera cam = load_camera(P);
     uint32_t st = ST_NEED_PIXEL;
     Path ps{};
     Ray r{};
-    r.ni = END;
     uint32_t n_seg = 0, n_smp = 0, n_box = 0, n_sph = 0;
-    const uint32_t thresh = P.compact;
-
+    unsigned long long wave_iters = 0;
+    STAMP_DECL;
     for (;;) {
-        // ---- service phase: bring every live lane back to TRAVERSING -------------------------
-        for (;;) {
-            if (st == ST_READY) {
-                n_seg++;
-                if (shade(P, ps, r.bi, r.best, r.o, r.d)) {
-                    setup_ray(P, r, n_sph);
-                    st = ST_TRACING;
-                } else {
-                    st = ST_NEED_SAMPLE;
-                }
-            }
-            if (st == ST_NEED_SAMPLE) {
-                if (start_sample(P, cam, ps, r.o, r.d)) {
-                    n_smp++;
-                    setup_ray(P, r, n_sph);
-                    st = ST_TRACING;
-                } else {
-                    st = ST_NEED_PIXEL;
-                }
-            }
-            if (!__ballot(st == ST_NEED_PIXEL)) break;
-            refill(P, lane, st, ps);
+        STAMP(0);
+        refill(P, lane, st, ps);
+        if (st == ST_NEED_SAMPLE) {
+            if (start_sample(P, cam, ps, r.o, r.d)) { st = ST_TRACING; n_smp++; }
+            else st = ST_NEED_PIXEL;
         }
-        if (!__ballot(st == ST_TRACING)) break;   // every lane retired
-        // ---- traverse phase ---------------------------------------------------------------------
-        for (;;) {
-            if (st == ST_TRACING) {
-                if (r.ni != END) visit_node<COUNT>(P, nodes4, leaf4, leaf_ids, r, n_box, n_sph);
-                if (r.ni == END) st = ST_READY;
-            }
-            const unsigned long long trav = __ballot(st == ST_TRACING);
-            if (__popcll(trav) < thresh && (trav == 0 || __ballot(st == ST_READY))) break;
+        if (__ballot(st == ST_NEED_PIXEL)) continue;   // refill before the next trace
+        if (!__ballot(st == ST_TRACING)) break;         // every lane retired
+        STAMP(1);
+        if (st == ST_TRACING) setup_ray(P, r, n_sph);
+        STAMP(2);
+        const uint32_t box0 = n_box;
+        if (st == ST_TRACING) walk_ordered<COUNT>(P, nodes4, leaf4, leaf_ids, stk, BLOCK, r, n_box, n_sph);
+        if (COUNT) {
+            uint32_t m = (n_box - box0) / 2u;
+            for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor(m, off));
+            if (lane == 0) wave_iters += m;
+        }
+        STAMP(3);
+        if (st == ST_TRACING) {
+            n_seg++;
+            if (!shade(P, ps, r.bi, r.best, r.o, r.d)) st = ST_NEED_SAMPLE;
         }
     }
+    STAMP_FLUSH;
     atomicAdd(&P.counters->segments, (unsigned long long)n_seg);
     atomicAdd(&P.counters->samples, (unsigned long long)n_smp);
     if (COUNT) {
         atomicAdd(&P.counters->box_tests, (unsigned long long)n_box);
         atomicAdd(&P.counters->sphere_tests, (unsigned long long)n_sph);
+        if (lane == 0) atomicAdd(&P.counters->wave_iters, wave_iters);
     }
 }
 
@@ -596,6 +689,11 @@ __global__ void rt_debug_math_kernel(int op, const float* __restrict__ in, float
 // ---- host-callable launchers (rt_api.cpp) ---------------------------------------------------
 namespace rt {
 
+#ifndef RT_LBVH2_BLOCK
+#define RT_LBVH2_BLOCK 256
+#endif
+constexpr uint32_t kLbvh2Block = RT_LBVH2_BLOCK;
+
 static const void* pick(uint32_t accel, bool count) {
     switch (accel) {
         case ACCEL_BRUTE:
@@ -604,20 +702,31 @@ static const void* pick(uint32_t accel, bool count) {
         case ACCEL_LBVH_LDS:
             return count ? reinterpret_cast<const void*>(rt_trace_lbvh_kernel<true, true>)
                          : reinterpret_cast<const void*>(rt_trace_lbvh_kernel<true, false>);
+        case ACCEL_LBVH2:
+            return count ? reinterpret_cast<const void*>(rt_trace_lbvh2_kernel<false, true, kLbvh2Block>)
+                         : reinterpret_cast<const void*>(rt_trace_lbvh2_kernel<false, false, kLbvh2Block>);
+        case ACCEL_LBVH2_LDS:
+            return count ? reinterpret_cast<const void*>(rt_trace_lbvh2_kernel<true, true, kLbvh2Block>)
+                         : reinterpret_cast<const void*>(rt_trace_lbvh2_kernel<true, false, kLbvh2Block>);
         default:
             return count ? reinterpret_cast<const void*>(rt_trace_lbvh_kernel<false, true>)
                          : reinterpret_cast<const void*>(rt_trace_lbvh_kernel<false, false>);
     }
 }
 
+uint32_t block_size(uint32_t accel) {
+    return (accel == ACCEL_LBVH2 || accel == ACCEL_LBVH2_LDS) ? kLbvh2Block : 256u;
+}
+
 hipError_t launch_trace(const TraceParams& P, uint32_t accel, bool count, int grid, size_t lds_bytes,
                         hipStream_t st) {
     void* args[] = {const_cast<TraceParams*>(&P)};
-    return hipLaunchKernel(pick(accel, count), dim3(grid), dim3(256), args, lds_bytes, st);
+    return hipLaunchKernel(pick(accel, count), dim3(grid), dim3(block_size(accel)), args, lds_bytes, st);
 }
 
 hipError_t trace_occupancy(uint32_t accel, bool count, size_t lds_bytes, int* blocks_per_cu) {
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, pick(accel, count), 256, lds_bytes);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, pick(accel, count),
+                                                        block_size(accel), lds_bytes);
 }
 
 hipError_t launch_scatter_rows(const float* src_acc, const uint8_t* src_px, const uint32_t* rows,

@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--grid", type=int, default=11)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--accels", default="2,1")
-    ap.add_argument("--compact", default="0", help="LBVH loop forms to sweep (0 classic, N compaction)")
+    ap.add_argument("--walk", default="0", help="LBVH walk forms to sweep (0 default/ordered, 1 escape-link)")
     args = ap.parse_args()
     libs = [str(abi.LIB_PATH)] + args.libs
     W, H = args.width, args.height
@@ -48,7 +48,7 @@ def main():
     ref = {}
     configs = []
     for accel in [int(a) for a in args.accels.split(",")]:
-        for c in ([int(x) for x in args.compact.split(",")] if accel == 2 else [0]):
+        for c in ([int(x) for x in args.walk.split(",")] if accel == 2 else [0]):
             opt = rtvk.make_options(accel=accel)
             opt.reserved[1] = c
             configs.append((accel, c, opt))
@@ -76,7 +76,7 @@ def main():
     rows = []
     for (accel, cth, name), ts in sorted(times.items()):
         ms = float(np.median(ts))
-        rows.append({"accel": accel, "compact": cth, "lib": name, "ms_median": round(ms, 3), "ms_min": round(min(ts), 3),
+        rows.append({"accel": accel, "walk": cth, "lib": name, "ms_median": round(ms, 3), "ms_min": round(min(ts), 3),
                      "msamples_s": round(W * H * args.spp / ms / 1e3, 1)})
     for r in rows:
         print(json.dumps(r))

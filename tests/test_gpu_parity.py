@@ -16,6 +16,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 GOLDEN = Path(__file__).resolve().parent / "golden"
 BRUTE, LBVH = 1, 2
+LBVH_ORDERED = 3   # test-only alias: accel LBVH with the ordered two-wide walk (options.reserved[1] = 2)
 
 
 @pytest.fixture(scope="module")
@@ -48,8 +49,11 @@ def gpu_render(rtvk, renderer, torch, spheres, rci_u32, band_w, band_h, rows=Non
            else torch.from_numpy(np.ascontiguousarray(accum, np.float32)).cuda())
     out = torch.full((band_h, band_w, 4), 7, dtype=torch.uint8, device="cuda")
     rows_t = None if rows is None else torch.from_numpy(np.asarray(rows, np.int32)).cuda()
-    opt = rtvk.make_options(max_depth=max_depth, seed_mode=seed_mode, rng_mode=rng_mode, accel=accel,
+    opt = rtvk.make_options(max_depth=max_depth, seed_mode=seed_mode, rng_mode=rng_mode,
+                            accel=LBVH if accel == LBVH_ORDERED else accel,
                             accumulate=accumulate, sample_base=sample_base, count_tests=count)
+    if accel == LBVH_ORDERED:
+        opt.reserved[1] = 2
     renderer.render_device(rci, acc, out, rows=rows_t, options=opt)
     torch.cuda.synchronize()
     st = renderer.stats()
@@ -105,7 +109,7 @@ def test_math_primitives_bit_exact(rtvk, torch, oracle, op):
 
 
 # ---- golden fixtures --------------------------------------------------------------------------
-@pytest.mark.parametrize("accel", [BRUTE, LBVH])
+@pytest.mark.parametrize("accel", [BRUTE, LBVH, LBVH_ORDERED])
 @pytest.mark.parametrize("case", ["g64x36_spp4", "g48x32_spp3_depth3_local", "g40x24_spp2_counter"])
 def test_golden(rtvk, renderer, torch, oracle, case, accel):
     m = json.loads((GOLDEN / f"{case}.json").read_text())
@@ -131,7 +135,7 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("accel", [BRUTE, LBVH])
+@pytest.mark.parametrize("accel", [BRUTE, LBVH, LBVH_ORDERED])
 @pytest.mark.parametrize("case", range(len(CASES)))
 def test_vs_oracle(rtvk, renderer, torch, oracle, case, accel):
     W, H, oy, bh, spp, t, K, kw = CASES[case]
@@ -147,7 +151,7 @@ def test_empty_and_single_sphere(rtvk, renderer, torch, oracle):
     rci = oracle.render_call_info(2, 20, 10)
     for sc in (np.zeros((0, 80), np.uint8), oracle.generate_scene()[:1], oracle.generate_scene()[3:4]):
         ra, ro, _ = oracle.render(sc, rci, 20, 10)
-        for accel in (BRUTE, LBVH):
+        for accel in (BRUTE, LBVH, LBVH_ORDERED):
             a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, 20, 10, accel=accel)
             assert_same(a, o, ra, ro)
 
@@ -207,6 +211,8 @@ def test_lbvh_equals_brute_full_size(rtvk, renderer, torch, oracle, W, H, spp, K
     al, ol, sl = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH)
     assert_same(al, ol, ab, ob)
     assert sb.segments == sl.segments
+    ao, oo, so = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH_ORDERED)
+    assert_same(ao, oo, ab, ob)
 
 
 def test_band_split_invariance_full_size(rtvk, renderer, torch, oracle):
