@@ -9,7 +9,7 @@ import sys
 def summarise(d, match="rt_trace"):
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     dur = collections.defaultdict(list)
-    for f in sorted(glob.glob(f"{d}/p*/run_counter_collection.csv")):
+    for f in sorted(glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"]
             if match not in k:
