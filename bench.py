@@ -78,7 +78,8 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-brute-line", action="store_true", help="skip the brute-force side measurement")
     ap.add_argument("--profile", action="store_true", help="short run for rocprofv3 (no side legs)")
-    ap.add_argument("--compact", type=int, default=0, help="LBVH loop form: 0 classic, N = compaction threshold")
+    ap.add_argument("--walk", type=int, default=0,
+                    help="LBVH walk form (A/B only): 0 default escape-link, 2 ordered, 4 compact nodes")
     args = ap.parse_args()
 
     import numpy as np
@@ -106,7 +107,7 @@ def main() -> int:
     renderer.set_scene(scene)
     rci = rtvk.canonical_render_call_info(spp, W, H)
     opts = rtvk.make_options(accel=accel)
-    opts.reserved[1] = args.compact
+    opts.reserved[1] = args.walk
     stream = torch.cuda.current_stream()
     ev = []
 
@@ -150,7 +151,7 @@ def main() -> int:
     # kernel (identical image, same traversal; outside the timed region).
     local_rows = len(dr.rows_np)
     cnt_opts = rtvk.make_options(accel=accel, count_tests=True)
-    cnt_opts.reserved[1] = args.compact
+    cnt_opts.reserved[1] = args.walk
     if local_rows:
         acc = torch.zeros((local_rows, W, 4), dtype=torch.float32, device=dev)
         out = torch.zeros((local_rows, W, 4), dtype=torch.uint8, device=dev)

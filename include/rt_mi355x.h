@@ -155,6 +155,9 @@ int rt_store_ppm(const char* path, const uint8_t* rgba8, uint32_t width, uint32_
 int rt_debug_math(int device, int op, const float* in_pairs, float* out, uint32_t n);
 /* Diagnostic: per-phase cycle sums of ctx's last launch, filled only by -DRT_STAMPS builds. */
 int rt_debug_stamps(rt_context* ctx, uint64_t* out8);
+/* Diagnostic: histogram of LBVH box tests per segment of the last instrumented launch
+ * (options.reserved[0] & 1), 2 x 64 bins: [0] segments that miss, [1] segments that hit. */
+int rt_debug_walk_hist(rt_context* ctx, uint64_t* out128);
 
 /* src/ray_trace.h:9-15 — identical symbol and parameter list. Renders the canonical scene once
  * (t = 0), prints the frame time, stores `render.ppm` when storeRenderResult, and returns. */

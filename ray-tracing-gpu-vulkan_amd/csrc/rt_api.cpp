@@ -42,14 +42,81 @@ struct rt_context {
     rt::Counters* counters = nullptr;   // device
     hipStream_t last_stream = nullptr;
     // occupancy cache per kernel (accel id 1..5) and count flag, valid for occ_lds bytes of LDS
-    int occ[6][2] = {};
-    size_t occ_lds[6][2] = {};
+    int occ[8][2] = {};
+    size_t occ_lds[8][2] = {};
     size_t lds_bytes = 0;                        // LBVH_LDS staging size of the current scene
     size_t lds2_bytes = 0;                       // LBVH2_LDS staging size (0: does not fit)
+    size_t lds16_bytes = 0;                      // compact-node LBVH staging size (0: not used)
+    size_t lds_scene_bytes = 0;                  // LBVH + geometry + materials staging (0: no fit)
+    // unpadded LBVH node boxes (host) and the radius the device copy is padded for
+    std::vector<rt::BvhNode> nodes_host;
+    std::vector<rt::Bvh2Node> nodes2_host;
+    float scene_radius = 0.0f;
+    float pad_radius = 0.0f;
 };
 
-// LBVH staged in LDS when its image is at most this large (keeps >= 6 blocks per CU).
+namespace {
+// Node boxes grow by 12u * R (u = 2^-24): the one-fma slab form of the walk differs from the
+// exact form of the AABB gate by at most u|o| + 5u(|bound| + |o|) in distance along each axis
+// for |o|, |bound| <= R; 1.5x margin.
+float pad_for(float R) { return 18.0f * 5.9604645e-8f * R; }
+
+// float -> binary16 rounded toward -inf (down) or +inf (up), so a box only ever grows.
+uint16_t half_bits(float x, bool up) {
+    const _Float16 h0 = (_Float16)x;   // round to nearest
+    uint16_t b = __builtin_bit_cast(uint16_t, h0);
+    const float back = (float)h0;
+    if ((up && back < x) || (!up && back > x)) {
+        // one binary16 step outward
+        if (up) b = (b == 0x8000u) ? 0x0001u : ((b & 0x8000u) ? uint16_t(b - 1) : uint16_t(b + 1));
+        else b = (b == 0x0000u) ? 0x8001u : ((b & 0x8000u) ? uint16_t(b + 1) : uint16_t(b - 1));
+    }
+    return b;
+}
+
+// Compact nodes from (padded) escape-link nodes; false when the tree does not fit the format.
+bool make_nodes16(const std::vector<rt::BvhNode>& in, std::vector<rt::BvhNode16>& out) {
+    out.clear();
+    if (in.empty() || in.size() >= 0xffffu) return false;
+    out.reserve(in.size());
+    for (const rt::BvhNode& n : in) {
+        uint32_t leaf = 0;
+        if (n.first_count) {
+            const uint32_t first = n.first_count >> 4, cnt = n.first_count & 15u;
+            if ((first & 3u) || (first >> 2) >= 8192u || cnt < 1u || cnt > 4u) return false;
+            leaf = 0x8000u | ((first >> 2) << 2) | (cnt - 1u);
+        }
+        const uint32_t esc = (n.escape == 0xffffffffu) ? 0xffffu : n.escape;
+        rt::BvhNode16 m;
+        m.x = half_bits(n.lox, false) | (uint32_t(half_bits(n.loy, false)) << 16);
+        m.y = half_bits(n.loz, false) | (uint32_t(half_bits(n.hix, true)) << 16);
+        m.z = half_bits(n.hiy, true) | (uint32_t(half_bits(n.hiz, true)) << 16);
+        m.w = esc | (leaf << 16);
+        out.push_back(m);
+    }
+    return true;
+}
+
+void pad_nodes(const std::vector<rt::BvhNode>& in, std::vector<rt::BvhNode>& out,
+               const std::vector<rt::Bvh2Node>& in2, std::vector<rt::Bvh2Node>& out2, float pad) {
+    out = in;
+    for (auto& n : out) {
+        n.lox -= pad; n.loy -= pad; n.loz -= pad;
+        n.hix += pad; n.hiy += pad; n.hiz += pad;
+    }
+    out2 = in2;
+    for (auto& n : out2) {
+        n.l0x -= pad; n.l0y -= pad; n.l0z -= pad; n.h0x += pad; n.h0y += pad; n.h0z += pad;
+        n.l1x -= pad; n.l1y -= pad; n.l1z -= pad; n.h1x += pad; n.h1y += pad; n.h1z += pad;
+    }
+}
+}  // namespace
+
+// LBVH staged in LDS when its image is at most this large.
 static constexpr size_t kMaxLdsBvhBytes = 24 * 1024;
+// LBVH + per-sphere geometry/material records staged together up to this size (512-thread
+// blocks: 3 blocks = 24 waves per CU fit in the 160 KiB LDS).
+static constexpr size_t kMaxLdsSceneBytes = 52 * 1024;
 // Ordered-walk LBVH staged in LDS up to this size (plus the per-lane stacks).
 static constexpr size_t kMaxLdsBvh2Bytes = 40 * 1024;
 
@@ -262,7 +329,7 @@ int rt_context_create(int device, rt_context** out) {
     RT_HIP(hipMalloc(&c, sizeof(rt::Counters)));
     RT_HIP(hipMemset(c, 0, sizeof(rt::Counters)));
     ctx->counters = static_cast<rt::Counters*>(c);
-    for (int a = 0; a < 6; a++)
+    for (int a = 0; a < 8; a++)
         for (int cnt = 0; cnt < 2; cnt++) ctx->occ_lds[a][cnt] = ~size_t(0);
     *out = ctx.release();
     return RT_OK;
@@ -319,8 +386,28 @@ int rt_set_scene(rt_context* ctx, const Sphere* spheres, uint32_t count, void* s
         d.n_leaf = uint32_t(bvh.leaf_ids.size());
         // leaf ids are read as uint4: pad to a multiple of 4
         while (bvh.leaf_ids.size() % 4) bvh.leaf_ids.push_back(0u);
+        // pad node boxes for origins within the scene radius (hit points) and a nearby camera
+        float R = 0.0f;
+        for (uint32_t i = 0; i < count; i++) {
+            const rt_vec4& gg = spheres[i].geometry;
+            R = std::max(R, std::sqrt(gg.x * gg.x + gg.y * gg.y + gg.z * gg.z) + std::fabs(gg.w));
+        }
+        ctx->scene_radius = R;
+        ctx->pad_radius = R * 1.01f + 100.0f;
+        ctx->nodes_host = bvh.nodes;
+        ctx->nodes2_host = bvh.nodes2;
+        pad_nodes(ctx->nodes_host, bvh.nodes, ctx->nodes2_host, bvh.nodes2, pad_for(ctx->pad_radius));
         const size_t lds = size_t(2 * d.n_nodes + d.n_leaf + (d.n_leaf + 3) / 4) * 16;
         ctx->lds_bytes = (d.n_nodes && lds <= kMaxLdsBvhBytes) ? lds : 0;
+        const size_t lds_scene = lds + size_t(count) * 48u;
+        ctx->lds_scene_bytes = (d.n_nodes && lds_scene <= kMaxLdsSceneBytes) ? lds_scene : 0;
+        std::vector<rt::BvhNode16> n16;
+        const size_t lds16 = size_t(d.n_nodes + d.n_leaf + (d.n_leaf + 3) / 4) * 16;
+        ctx->lds16_bytes = 0;
+        if (make_nodes16(bvh.nodes, n16) && lds16 <= kMaxLdsBvhBytes) {
+            if (int rc = upload(ctx, n16, &d.nodes16, st)) return rc;
+            ctx->lds16_bytes = lds16;
+        }
         d.n_nodes2 = uint32_t(bvh.nodes2.size());
         d.root2 = bvh.root2;
         d.depth2 = bvh.depth2;
@@ -351,14 +438,22 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     rt_options o;
     std::memset(&o, 0, sizeof(o));
     if (opt) o = *opt;
-    // reserved[1] (internal, A/B only): LBVH walk form, 0 = default (stackless escape-link),
-    // 2 = ordered two-wide walk with an LDS stack (slower on the canonical scene)
+    // reserved[1] (internal, A/B only): LBVH walk form, 0 = default (stackless escape-link walk
+    // over 32-B nodes), 2 = ordered two-wide walk with an LDS stack, 4 = escape-link walk over
+    // compact 16-B binary16 nodes (both slower on the canonical scene)
     const bool escape_walk = o.reserved[1] != 2u;
+    const bool allow16 = o.reserved[1] == 4u;
     uint32_t accel;
     size_t lds = 0;
     const rt::DeviceScene& ds = ctx->scene;
     if (o.accel == RT_ACCEL_BRUTE) {
         accel = rt::ACCEL_BRUTE;
+    } else if (escape_walk && allow16 && ctx->lds16_bytes) {
+        accel = rt::ACCEL_LBVH16_LDS;
+        lds = ctx->lds16_bytes;
+    } else if (escape_walk && ctx->lds_scene_bytes && o.reserved[1] != 5u) {
+        accel = rt::ACCEL_LBVH_LDS_SCENE;
+        lds = ctx->lds_scene_bytes;
     } else if (escape_walk) {
         accel = ctx->lds_bytes ? rt::ACCEL_LBVH_LDS : rt::ACCEL_LBVH;
         lds = ctx->lds_bytes;
@@ -400,6 +495,7 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     P.big_ids = d.big_ids;
     P.nodes = d.n_nodes ? d.nodes : nullptr;
     P.n_nodes = d.n_nodes;
+    P.nodes16 = d.nodes16;
     P.nodes2 = d.nodes2;   // null when the tree is a single leaf (root2 is then a leaf reference)
     P.n_nodes2 = d.n_nodes2;
     P.root2 = d.root2;
@@ -418,6 +514,25 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
 
     DeviceGuard g(ctx->device);
     hipStream_t st = static_cast<hipStream_t>(stream);
+    {   // a camera outside the padded radius: re-pad the node boxes for it (rare, synchronous)
+        const float cx = rci->camera_pos.x, cy = rci->camera_pos.y, cz = rci->camera_pos.z;
+        const float cam_r = std::sqrt(cx * cx + cy * cy + cz * cz);
+        if (!(cam_r <= ctx->pad_radius) && (d.n_nodes || d.n_nodes2)) {
+            if (!std::isfinite(cam_r)) return fail(RT_ERR_INVALID_ARGUMENT, "camera position is not finite");
+            ctx->pad_radius = std::max(ctx->scene_radius, cam_r) * 1.01f + 100.0f;
+            std::vector<rt::BvhNode> n1;
+            std::vector<rt::Bvh2Node> n2;
+            pad_nodes(ctx->nodes_host, n1, ctx->nodes2_host, n2, pad_for(ctx->pad_radius));
+            RT_HIP(hipStreamSynchronize(st));
+            if (!n1.empty()) RT_HIP(hipMemcpy(d.nodes, n1.data(), n1.size() * sizeof(n1[0]), hipMemcpyHostToDevice));
+            if (!n2.empty()) RT_HIP(hipMemcpy(d.nodes2, n2.data(), n2.size() * sizeof(n2[0]), hipMemcpyHostToDevice));
+            std::vector<rt::BvhNode16> n16;
+            if (d.nodes16) {
+                if (!make_nodes16(n1, n16)) return fail(RT_ERR_DEVICE, "compact LBVH re-pad failed");
+                RT_HIP(hipMemcpy(d.nodes16, n16.data(), n16.size() * sizeof(n16[0]), hipMemcpyHostToDevice));
+            }
+        }
+    }
     RT_HIP(hipMemsetAsync(ctx->counters, 0, sizeof(rt::Counters), st));
     const int ci = count ? 1 : 0;
     if (ctx->occ_lds[accel][ci] != lds) {
@@ -469,6 +584,17 @@ int rt_debug_stamps(rt_context* ctx, uint64_t* out8) {
     RT_HIP(hipMemcpy(&c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
     for (int k = 0; k < 8; k++) out8[k] = c.stamp[k];
     if (!c.stamp[0] && !c.stamp[1]) out8[6] = c.wave_iters;   // non-stamp builds: walk iterations
+    return RT_OK;
+}
+
+// Diagnostic export: walk-length histogram of the last COUNT launch (2 x 64 bins: miss, hit).
+int rt_debug_walk_hist(rt_context* ctx, uint64_t* out128) {
+    if (!ctx || !out128) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    DeviceGuard g(ctx->device);
+    RT_HIP(hipStreamSynchronize(ctx->last_stream));
+    rt::Counters c;
+    RT_HIP(hipMemcpy(&c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
+    std::memcpy(out128, c.walk_hist, sizeof(c.walk_hist));
     return RT_OK;
 }
 

@@ -43,6 +43,16 @@ struct alignas(16) Bvh2Node {
 };
 constexpr uint32_t kLeafFlag = 0x80000000u;
 
+// Compact escape-link node, 16 B (one ds_read_b128 per visit): the padded box rounded OUTWARD to
+// binary16 (so it still contains every member sphere's AABB: the walk stays conservative and
+// exact), the escape index and the leaf field in 16 bits each. Used when the tree has fewer than
+// 65535 nodes and 8192 leaves (the LDS-staged case).
+//   x = lo.x | lo.y << 16, y = lo.z | hi.x << 16, z = hi.y | hi.z << 16  (binary16 bit patterns)
+//   w = escape | leaf << 16, escape 0xffff = end, leaf 0 = inner else 0x8000 | index << 2 | (count - 1)
+struct alignas(16) BvhNode16 {
+    uint32_t x, y, z, w;
+};
+
 // Scene as resident in HBM (one allocation per context, rebuilt by rt_set_scene).
 struct DeviceScene {
     uint32_t n_spheres = 0;
@@ -58,6 +68,7 @@ struct DeviceScene {
     GeomRec* leaf_geom = nullptr;  // spheres permuted into leaf order (contiguous per leaf)
     uint32_t* leaf_ids = nullptr;  // original index of each leaf slot
     uint32_t n_leaf = 0;
+    BvhNode16* nodes16 = nullptr;  // compact escape-link nodes (null when the tree is too big)
     Bvh2Node* nodes2 = nullptr;    // ordered-walk layout (same leaves)
     uint32_t n_nodes2 = 0;
     uint32_t root2 = 0;            // root reference (inner index or leaf reference)
@@ -65,7 +76,7 @@ struct DeviceScene {
     float small_rmax = 0.0f;       // largest radius in the tree
 };
 
-enum : uint32_t { ACCEL_BRUTE = 1, ACCEL_LBVH = 2, ACCEL_LBVH_LDS = 3, ACCEL_LBVH2 = 4, ACCEL_LBVH2_LDS = 5 };
+enum : uint32_t { ACCEL_BRUTE = 1, ACCEL_LBVH = 2, ACCEL_LBVH_LDS = 3, ACCEL_LBVH2 = 4, ACCEL_LBVH2_LDS = 5, ACCEL_LBVH16_LDS = 6, ACCEL_LBVH_LDS_SCENE = 7 };
 
 // Counters block (device memory, zeroed before each launch by the host).
 struct Counters {
@@ -76,6 +87,7 @@ struct Counters {
     unsigned long long box_tests;
     unsigned long long sphere_tests;
     unsigned long long wave_iters; // COUNT builds: sum over waves of walk-loop iterations
+    unsigned long long walk_hist[2][64];  // COUNT builds: box tests per segment, [miss, hit]
     unsigned long long stamp[8];   // diagnostic builds only (-DRT_STAMPS): cycles per phase
 };
 
@@ -104,6 +116,7 @@ struct TraceParams {
     const uint32_t* big_ids;
     const BvhNode* nodes;
     uint32_t n_nodes;
+    const BvhNode16* nodes16;
     const Bvh2Node* nodes2;
     uint32_t n_nodes2, root2, stack_depth;
     uint32_t n_leaf;               // spheres in the tree (leaf slots)

@@ -103,7 +103,8 @@ __device__ __forceinline__ void test_sphere(float cx, float cy, float cz, float 
 // ids[slot] only when the quadratic reports (tie-break and result), both in the rare branch.
 __device__ __forceinline__ void test_leaf_sphere(float4 sp, const uint32_t* __restrict__ ids,
                                                  uint32_t slot, V3 o, V3 d, V3 inv, float a,
-                                                 float& best, uint32_t& bi) {
+                                                 float& best, uint32_t& bi, float& limit,
+                                                 float cull_abs, float cull_rel) {
     const float rr = sp.w * sp.w;
     const float ocx = o.x - sp.x, ocy = o.y - sp.y, ocz = o.z - sp.z;
     const float b = __builtin_fmaf(ocz, d.z, __builtin_fmaf(ocy, d.y, ocx * d.x));
@@ -119,7 +120,76 @@ __device__ __forceinline__ void test_leaf_sphere(float4 sp, const uint32_t* __re
             if ((t < best || id < bi) && aabb_hit(sp.x, sp.y, sp.z, sp.w, o, inv)) {
                 best = t;
                 bi = id;
+                limit = fminf(__builtin_fmaf(t, cull_rel, t + cull_abs), 10000.0f);
             }
+        }
+    }
+}
+
+// Four spheres at once (a leaf, or a batch of big spheres): the discriminants of all four are
+// computed branch-free, then each lane loops over only ITS candidates (D >= 0). Inside the loop
+// sit the expensive exact parts (correctly rounded sqrt and divide, the AABB gate); t2 is
+// computed only when t1 < tmin. Identical arithmetic to test_sphere per sphere, and candidates
+// are accepted with the same (t, index) rule, so the result is the same; but the wave executes the
+// expensive block max-over-lanes-of-candidates times instead of once per slot in which any lane
+// has a candidate.
+struct Sph4 { float4 s[4]; };
+
+template <typename IdOf>
+__device__ __forceinline__ void test4(const float4 s0, const float4 s1, const float4 s2, const float4 s3,
+                                      IdOf id_of, V3 o, V3 d, V3 inv, float a, float& best,
+                                      uint32_t& bi, float& limit, float cull_abs, float cull_rel) {
+    float bv[4], Dv[4];
+    const float4 sv[4] = {s0, s1, s2, s3};
+    uint32_t cand = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float rr = sv[k].w * sv[k].w;
+        const float ocx = o.x - sv[k].x, ocy = o.y - sv[k].y, ocz = o.z - sv[k].z;
+        bv[k] = __builtin_fmaf(ocz, d.z, __builtin_fmaf(ocy, d.y, ocx * d.x));
+        const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - rr;
+        Dv[k] = __builtin_fmaf(bv[k], bv[k], -(a * c));
+        cand |= (Dv[k] >= 0.0f ? 1u : 0u) << k;
+    }
+    while (cand) {
+        const uint32_t k = __builtin_ctz(cand);
+        cand &= cand - 1u;
+        // per-lane select of slot k (no dynamic register indexing)
+        const float b = k == 0 ? bv[0] : k == 1 ? bv[1] : k == 2 ? bv[2] : bv[3];
+        const float D = k == 0 ? Dv[0] : k == 1 ? Dv[1] : k == 2 ? Dv[2] : Dv[3];
+        const float sq = __builtin_sqrtf(D);
+        float t = (-b - sq) / a;
+        if (!(t >= T_MIN)) t = (-b + sq) / a;     // report t1 if t1 >= tmin, else t2
+        if (t >= T_MIN && t <= best) {
+            const uint32_t id = id_of(k);
+            if (t < best || id < bi) {
+                const float4 sp = k == 0 ? s0 : k == 1 ? s1 : k == 2 ? s2 : s3;
+                if (aabb_hit(sp.x, sp.y, sp.z, sp.w, o, inv)) {
+                    best = t;
+                    bi = id;
+                    limit = fminf(__builtin_fmaf(t, cull_rel, t + cull_abs), 10000.0f);
+                }
+            }
+        }
+    }
+}
+
+// test_sphere with the radius already in hand (big spheres: loaded through the scalar path).
+__device__ __forceinline__ void test_sphere_r(float cx, float cy, float cz, float rr, float rad, V3 o,
+                                              V3 d, V3 inv, float a, uint32_t id, float& best,
+                                              uint32_t& bi) {
+    const float ocx = o.x - cx, ocy = o.y - cy, ocz = o.z - cz;
+    const float b = __builtin_fmaf(ocz, d.z, __builtin_fmaf(ocy, d.y, ocx * d.x));
+    const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - rr;
+    const float D = __builtin_fmaf(b, b, -(a * c));
+    if (D >= 0.0f) {
+        const float sq = __builtin_sqrtf(D);
+        const float t1 = (-b - sq) / a;
+        const float t2 = (-b + sq) / a;
+        const float t = (t1 >= T_MIN) ? t1 : t2;
+        if (t >= T_MIN && (t < best || (t == best && id < bi)) && aabb_hit(cx, cy, cz, rad, o, inv)) {
+            best = t;
+            bi = id;
         }
     }
 }
@@ -242,8 +312,9 @@ __device__ __forceinline__ bool start_sample(const rt::TraceParams& P, const Cam
 // shader.rchit:38-133 / shader.rmiss:13-18 + shader.rgen:77-88 for one finished trace.
 // Returns true when the path continues (o, d hold the next ray), false when the sample ended
 // (its colour has been added to the pixel sum).
-__device__ __forceinline__ bool shade(const rt::TraceParams& P, Path& ps, uint32_t bi, float best,
-                                      V3& o, V3& d) {
+__device__ __forceinline__ bool shade(const rt::TraceParams& P, const float4* __restrict__ geom4,
+                                      const float4* __restrict__ mat4, Path& ps, uint32_t bi,
+                                      float best, V3& o, V3& d) {
     V3 att;
     bool scatter = false;
     V3 sd = v3(0.0f, 0.0f, 0.0f);
@@ -254,9 +325,10 @@ __device__ __forceinline__ bool shade(const rt::TraceParams& P, Path& ps, uint32
         // shader.rint:33/37 hit attribute; shader.rchit:38-49
         p = v3(__builtin_fmaf(best, d.x, o.x), __builtin_fmaf(best, d.y, o.y),
                __builtin_fmaf(best, d.z, o.z));
-        const rt::GeomRec gc = P.geom[bi];
-        const float4 m0 = reinterpret_cast<const float4*>(P.mat)[2 * bi];
-        const float4 m1 = reinterpret_cast<const float4*>(P.mat)[2 * bi + 1];
+        const float4 gc4 = geom4[bi];
+        const rt::GeomRec gc{gc4.x, gc4.y, gc4.z, gc4.w};
+        const float4 m0 = mat4[2 * bi];
+        const float4 m1 = mat4[2 * bi + 1];
         const uint32_t tt = __float_as_uint(m1.w);
         const uint32_t mtype = tt & 0xffu, ttype = tt >> 8;
         const V3 outward = normalize(sub(p, v3(gc.cx, gc.cy, gc.cz)));
@@ -314,7 +386,8 @@ __device__ __forceinline__ bool shade(const rt::TraceParams& P, Path& ps, uint32
 // ---------------------------------------------------------------------------------------------
 struct Ray {
     V3 o, d, inv, oi;      // origin, direction, 1/d, o * (1/d)
-    float a, tol;          // dot(d, d); fma-slab rounding allowance
+    float a;               // dot(d, d)
+    float limit;           // node cull limit: min(best + cull_abs + cull_rel * best, tmax)
     float best;
     uint32_t bi, ni;       // closest so far, next node (END = done)
 };
@@ -326,27 +399,32 @@ __device__ __forceinline__ void setup_ray(const rt::TraceParams& P, Ray& r, uint
     r.a = dot(r.d, r.d);
     r.inv = v3(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
     r.oi = v3(r.o.x * r.inv.x, r.o.y * r.inv.y, r.o.z * r.inv.z);
-    r.tol = 4.8e-7f * fmaxf(fmaxf(fabsf(r.oi.x), fabsf(r.oi.y)), fabsf(r.oi.z));
     r.best = T_MAX_SUCC;
     r.bi = 0xffffffffu;
     typedef const __attribute__((address_space(4))) uint32_t* ConstU;
     typedef const __attribute__((address_space(4))) float* ConstF;
     const ConstU ids = (ConstU)(P.big_ids);
     const ConstF g = (ConstF)(P.geom);
+    const ConstF rad = (ConstF)(P.radius);
     for (uint32_t k0 = 0; k0 < P.n_big; k0 += 4) {   // wave-uniform: scalar loads, 4 at a time
         uint32_t id[4];
-        float sp[16];
+        float sp[16], rs[4];
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) id[j] = ids[min(k0 + j, P.n_big - 1)];
 #pragma unroll
         for (uint32_t j = 0; j < 16; ++j) sp[j] = g[4 * id[j >> 2] + (j & 3)];
 #pragma unroll
-        for (uint32_t j = 0; j < 4; ++j)
-            if (k0 + j < P.n_big)
-                test_sphere<true>(sp[4 * j], sp[4 * j + 1], sp[4 * j + 2], sp[4 * j + 3], P.radius, r.o,
-                                  r.d, r.inv, r.a, id[j], r.best, r.bi);
+        for (uint32_t j = 0; j < 4; ++j) rs[j] = rad[id[j]];
+        // records of absent batch members (k0 + j >= n_big) repeat the last big sphere: a
+        // duplicate of an already tested sphere can never change (best, bi).
+        const float4 b0 = make_float4(sp[0], sp[1], sp[2], rs[0]), b1 = make_float4(sp[4], sp[5], sp[6], rs[1]);
+        const float4 b2 = make_float4(sp[8], sp[9], sp[10], rs[2]), b3 = make_float4(sp[12], sp[13], sp[14], rs[3]);
+        float unused_limit = 0.0f;
+        test4(b0, b1, b2, b3, [&](uint32_t k) { return k == 0 ? id[0] : k == 1 ? id[1] : k == 2 ? id[2] : id[3]; },
+              r.o, r.d, r.inv, r.a, r.best, r.bi, unused_limit, 0.0f, 0.0f);
     }
     n_sph += P.n_big;
+    r.limit = fminf(__builtin_fmaf(r.best, P.cull_rel, r.best + P.cull_abs), 10000.0f);
     r.ni = P.nodes ? 0u : END;
 }
 
@@ -367,17 +445,17 @@ __device__ __forceinline__ void visit_node(const rt::TraceParams& P, const float
     const float ty0 = __builtin_fmaf(n0.y, r.inv.y, -r.oi.y), ty1 = __builtin_fmaf(n1.y, r.inv.y, -r.oi.y);
     const float tz0 = __builtin_fmaf(n0.z, r.inv.z, -r.oi.z), tz1 = __builtin_fmaf(n1.z, r.inv.z, -r.oi.z);
     const float tnear = fmaxf(fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1)), T_MIN);
-    const float limit = fminf(__builtin_fmaf(r.best, P.cull_rel, r.best + P.cull_abs), 10000.0f);
-    const float tfar = fminf(fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1)), limit);
-    const bool hit = tnear <= __builtin_fmaf(fabsf(tfar), 4.8e-7f, tfar + r.tol);
+    // Node boxes are padded at build time by 12u x (scene + camera radius), which covers the
+    // rounding of this one-fma slab form against the exact form of the spheres' AABB gates
+    // (DESIGN.md §4.3), so the comparison needs no tolerance term.
+    const float tfar = fminf(fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1)), r.limit);
+    const bool hit = tnear <= tfar;
     const uint32_t fc = __float_as_uint(n1.w);
     if (hit && fc != 0u) {   // leaf: always 4 slots (dummy-padded), loads issued together
         const uint32_t first = fc >> 4;
         const float4 s0 = leaf4[first], s1 = leaf4[first + 1], s2 = leaf4[first + 2], s3 = leaf4[first + 3];
-        test_leaf_sphere(s0, leaf_ids, first, r.o, r.d, r.inv, r.a, r.best, r.bi);
-        test_leaf_sphere(s1, leaf_ids, first + 1, r.o, r.d, r.inv, r.a, r.best, r.bi);
-        test_leaf_sphere(s2, leaf_ids, first + 2, r.o, r.d, r.inv, r.a, r.best, r.bi);
-        test_leaf_sphere(s3, leaf_ids, first + 3, r.o, r.d, r.inv, r.a, r.best, r.bi);
+        test4(s0, s1, s2, s3, [&](uint32_t k) { return leaf_ids[first + k]; }, r.o, r.d, r.inv, r.a,
+              r.best, r.bi, r.limit, P.cull_abs, P.cull_rel);
         if (COUNT) n_sph += fc & 15u;
     }
     r.ni = (hit && fc == 0u) ? r.ni + 1u : __float_as_uint(n0.w);
@@ -389,14 +467,13 @@ __device__ __forceinline__ void visit_node(const rt::TraceParams& P, const float
 // (4-slot block), descends into the nearer hit inner child and pushes the farther one. Nearest-
 // first order finds the closest sphere early, so `best` culls the rest of the walk.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void leaf_block(uint32_t ref, const float4* __restrict__ leaf4,
+__device__ __forceinline__ void leaf_block(const rt::TraceParams& P, uint32_t ref,
+                                           const float4* __restrict__ leaf4,
                                            const uint32_t* __restrict__ leaf_ids, Ray& r) {
     const uint32_t first = (ref & ~kLeafFlagD) >> 3;
     const float4 s0 = leaf4[first], s1 = leaf4[first + 1], s2 = leaf4[first + 2], s3 = leaf4[first + 3];
-    test_leaf_sphere(s0, leaf_ids, first, r.o, r.d, r.inv, r.a, r.best, r.bi);
-    test_leaf_sphere(s1, leaf_ids, first + 1, r.o, r.d, r.inv, r.a, r.best, r.bi);
-    test_leaf_sphere(s2, leaf_ids, first + 2, r.o, r.d, r.inv, r.a, r.best, r.bi);
-    test_leaf_sphere(s3, leaf_ids, first + 3, r.o, r.d, r.inv, r.a, r.best, r.bi);
+    test4(s0, s1, s2, s3, [&](uint32_t k) { return leaf_ids[first + k]; }, r.o, r.d, r.inv, r.a, r.best,
+          r.bi, r.limit, P.cull_abs, P.cull_rel);
 }
 
 __device__ __forceinline__ float slab_near(float4 lo, float4 hi, const Ray& r, float& tfar_out) {
@@ -416,7 +493,7 @@ __device__ __forceinline__ void walk_ordered(const rt::TraceParams& P, const flo
     if (P.n_leaf == 0) return;   // no small spheres: nothing to walk
     uint32_t cur = P.root2;
     if (cur & kLeafFlagD) {   // the whole tree is one leaf
-        leaf_block(cur, leaf4, leaf_ids, r);
+        leaf_block(P, cur, leaf4, leaf_ids, r);
         if (COUNT) n_sph += cur & 7u;
         return;
     }
@@ -425,14 +502,11 @@ __device__ __forceinline__ void walk_ordered(const rt::TraceParams& P, const flo
         const float4 a0 = nodes4[4 * cur], a1 = nodes4[4 * cur + 1];
         const float4 b0 = nodes4[4 * cur + 2], b1 = nodes4[4 * cur + 3];
         if (COUNT) n_box += 2;
-        const float limit = fminf(__builtin_fmaf(r.best, P.cull_rel, r.best + P.cull_abs), 10000.0f);
         float tf0, tf1;
         const float tn0 = slab_near(a0, a1, r, tf0);
         const float tn1 = slab_near(b0, b1, r, tf1);
-        tf0 = fminf(tf0, limit);
-        tf1 = fminf(tf1, limit);
-        bool hit0 = tn0 <= __builtin_fmaf(fabsf(tf0), 4.8e-7f, tf0 + r.tol);
-        bool hit1 = tn1 <= __builtin_fmaf(fabsf(tf1), 4.8e-7f, tf1 + r.tol);
+        bool hit0 = tn0 <= fminf(tf0, r.limit);   // padded boxes: no tolerance term (visit_node)
+        bool hit1 = tn1 <= fminf(tf1, r.limit);
         const uint32_t c0 = __float_as_uint(a0.w), c1 = __float_as_uint(b0.w);
         // hit leaf children: test their spheres now
         uint32_t lp0 = (hit0 && (c0 & kLeafFlagD)) ? c0 : 0u;
@@ -441,7 +515,7 @@ __device__ __forceinline__ void walk_ordered(const rt::TraceParams& P, const flo
         hit1 = hit1 && !(c1 & kLeafFlagD);
         if (lp0 == 0u) { lp0 = lp1; lp1 = 0u; }
         while (lp0) {
-            leaf_block(lp0, leaf4, leaf_ids, r);
+            leaf_block(P, lp0, leaf4, leaf_ids, r);
             if (COUNT) n_sph += lp0 & 7u;
             lp0 = lp1;
             lp1 = 0u;
@@ -458,6 +532,85 @@ __device__ __forceinline__ void walk_ordered(const rt::TraceParams& P, const flo
             --sp;
             cur = stk[sp * stride];
         }
+    }
+}
+
+// The whole escape-link walk of one segment. With RT_PREFETCH both possible successors of the
+// current node (index + 1 and its escape) are loaded before the current box test, so the next
+// visit's LDS latency overlaps this visit's arithmetic (one dependent round trip per visit
+// instead of two).
+template <bool COUNT>
+__device__ __forceinline__ void walk_escape(const rt::TraceParams& P, const float4* __restrict__ nodes4,
+                                            const float4* __restrict__ leaf4,
+                                            const uint32_t* __restrict__ leaf_ids, Ray& r,
+                                            uint32_t& n_box, uint32_t& n_sph) {
+#ifdef RT_LEAF_INLINE
+    while (r.ni != END) visit_node<COUNT>(P, nodes4, leaf4, leaf_ids, r, n_box, n_sph);
+#else
+    // while-while (Aila & Laine 2009): the cheap inner-node loop runs until every active lane has
+    // found a hit leaf (postponed in `pending`) or finished its walk; then all pending leaves are
+    // tested together, so the 4-sphere leaf block runs once per batch instead of in every visit
+    // in which any lane of the wave happens to be at a leaf.
+    uint32_t pending = 0u;
+    for (;;) {
+        while (r.ni != END && pending == 0u) {
+            const float4 n0 = nodes4[2 * r.ni];
+            const float4 n1 = nodes4[2 * r.ni + 1];
+            if (COUNT) n_box++;
+            const float tx0 = __builtin_fmaf(n0.x, r.inv.x, -r.oi.x), tx1 = __builtin_fmaf(n1.x, r.inv.x, -r.oi.x);
+            const float ty0 = __builtin_fmaf(n0.y, r.inv.y, -r.oi.y), ty1 = __builtin_fmaf(n1.y, r.inv.y, -r.oi.y);
+            const float tz0 = __builtin_fmaf(n0.z, r.inv.z, -r.oi.z), tz1 = __builtin_fmaf(n1.z, r.inv.z, -r.oi.z);
+            const float tnear = fmaxf(fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1)), T_MIN);
+            const float tfar = fminf(fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1)), r.limit);
+            const bool hit = tnear <= tfar;
+            const uint32_t fc = __float_as_uint(n1.w);
+            if (hit && fc != 0u) pending = fc;
+            r.ni = (hit && fc == 0u) ? r.ni + 1u : __float_as_uint(n0.w);
+        }
+        if (pending == 0u) break;   // walk finished with no leaf left to test
+        const uint32_t first = pending >> 4;
+        const float4 s0 = leaf4[first], s1 = leaf4[first + 1], s2 = leaf4[first + 2], s3 = leaf4[first + 3];
+        test4(s0, s1, s2, s3, [&](uint32_t k) { return leaf_ids[first + k]; }, r.o, r.d, r.inv, r.a,
+              r.best, r.bi, r.limit, P.cull_abs, P.cull_rel);
+        if (COUNT) n_sph += pending & 15u;
+        pending = 0u;
+    }
+#endif
+}
+
+// Escape-link walk over compact 16-B nodes (BvhNode16): one ds_read_b128 per visit; the binary16
+// bounds enter the slab fmas directly through v_fma_mix_f32 (exact f16 -> f32 widening).
+__device__ __forceinline__ float h_lo(uint32_t v) {
+    return (float)__builtin_bit_cast(_Float16, (unsigned short)(v & 0xffffu));
+}
+__device__ __forceinline__ float h_hi(uint32_t v) {
+    return (float)__builtin_bit_cast(_Float16, (unsigned short)(v >> 16));
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void walk_escape16(const rt::TraceParams& P, const uint4* __restrict__ nodes,
+                                              const float4* __restrict__ leaf4,
+                                              const uint32_t* __restrict__ leaf_ids, Ray& r,
+                                              uint32_t& n_box, uint32_t& n_sph) {
+    uint32_t ni = (P.n_nodes != 0u) ? 0u : 0xffffu;
+    while (ni != 0xffffu) {
+        const uint4 n = nodes[ni];
+        if (COUNT) n_box++;
+        const float tx0 = __builtin_fmaf(h_lo(n.x), r.inv.x, -r.oi.x), tx1 = __builtin_fmaf(h_hi(n.y), r.inv.x, -r.oi.x);
+        const float ty0 = __builtin_fmaf(h_hi(n.x), r.inv.y, -r.oi.y), ty1 = __builtin_fmaf(h_lo(n.z), r.inv.y, -r.oi.y);
+        const float tz0 = __builtin_fmaf(h_lo(n.y), r.inv.z, -r.oi.z), tz1 = __builtin_fmaf(h_hi(n.z), r.inv.z, -r.oi.z);
+        const float tnear = fmaxf(fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1)), T_MIN);
+        const float tfar = fminf(fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1)), r.limit);
+        const bool hit = tnear <= tfar;
+        const uint32_t leaf = n.w >> 16;
+        if (hit && leaf != 0u) {
+            const uint32_t first = (leaf & 0x7fffu) & ~3u;   // (index << 2) = first slot
+            const float4 s0 = leaf4[first], s1 = leaf4[first + 1], s2 = leaf4[first + 2], s3 = leaf4[first + 3];
+            test4(s0, s1, s2, s3, [&](uint32_t k) { return leaf_ids[first + k]; }, r.o, r.d, r.inv, r.a,
+                  r.best, r.bi, r.limit, P.cull_abs, P.cull_rel);
+            if (COUNT) n_sph += (leaf & 3u) + 1u;
+        }
+        ni = (hit && leaf == 0u) ? ni + 1u : (n.w & 0xffffu);
     }
 }
 
@@ -492,7 +645,9 @@ __global__ __launch_bounds__(256, RT_TRACE_WAVES_PER_SIMD) void rt_trace_brute_k
             closest_brute(P, o, d, inv, dot(d, d), best, bi);
             if (COUNT) n_sph += P.n_spheres;
             n_seg++;
-            if (!shade(P, ps, bi, best, o, d)) st = ST_NEED_SAMPLE;
+            if (!shade(P, reinterpret_cast<const float4*>(P.geom), reinterpret_cast<const float4*>(P.mat),
+                       ps, bi, best, o, d))
+                st = ST_NEED_SAMPLE;
         }
     }
     atomicAdd(&P.counters->segments, (unsigned long long)n_seg);
@@ -505,10 +660,12 @@ __global__ __launch_bounds__(256, RT_TRACE_WAVES_PER_SIMD) void rt_trace_brute_k
 // until its longest walk ends. Stamp slots: 0 refill+sample start, 1 ray setup (big spheres),
 // 2 LBVH walk, 3 shading, 7 other.
 // ---------------------------------------------------------------------------------------------
-template <bool COUNT>
+template <bool COUNT, bool NODE16>
 __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const float4* __restrict__ nodes4,
                                              const float4* __restrict__ leaf4,
-                                             const uint32_t* __restrict__ leaf_ids) {
+                                             const uint32_t* __restrict__ leaf_ids,
+                                             const float4* __restrict__ geom4,
+                                             const float4* __restrict__ mat4) {
     const uint32_t lane = lane_id();
     const Camera cam = load_camera(P);
     uint32_t st = ST_NEED_PIXEL;
@@ -530,8 +687,16 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
         if (st == ST_TRACING) setup_ray(P, r, n_sph);
         STAMP(2);
         const uint32_t box0 = n_box;
-        if (st == ST_TRACING)
-            while (r.ni != END) visit_node<COUNT>(P, nodes4, leaf4, leaf_ids, r, n_box, n_sph);
+        if (st == ST_TRACING) {
+            if (NODE16)
+                walk_escape16<COUNT>(P, reinterpret_cast<const uint4*>(nodes4), leaf4, leaf_ids, r, n_box, n_sph);
+            else
+                walk_escape<COUNT>(P, nodes4, leaf4, leaf_ids, r, n_box, n_sph);
+        }
+        if (COUNT && st == ST_TRACING) {   // walk-length histogram (diagnostic, COUNT builds only)
+            const uint32_t len = min(n_box - box0, 63u);
+            atomicAdd(&P.counters->walk_hist[r.bi != 0xffffffffu ? 1 : 0][len], 1ull);
+        }
         if (COUNT) {   // wave iterations of this walk = the longest lane walk
             uint32_t m = n_box - box0;
             for (int off = 32; off > 0; off >>= 1) m = max(m, (uint32_t)__shfl_xor(m, off));
@@ -540,7 +705,7 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
         STAMP(3);
         if (st == ST_TRACING) {
             n_seg++;
-            if (!shade(P, ps, r.bi, r.best, r.o, r.d)) st = ST_NEED_SAMPLE;
+            if (!shade(P, geom4, mat4, ps, r.bi, r.best, r.o, r.d)) st = ST_NEED_SAMPLE;
         }
     }
     STAMP_FLUSH;
@@ -553,28 +718,46 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
     }
 }
 
-template <bool LDS, bool COUNT>
-__global__ __launch_bounds__(256, RT_TRACE_WAVES_PER_SIMD) void rt_trace_lbvh_kernel(const rt::TraceParams P) {
+#ifndef RT_LBVH_BLOCK
+#define RT_LBVH_BLOCK 512
+#endif
+
+// LBVH kernel. LDS: stage the tree (nodes, leaf spheres, leaf ids) and, when SCENE_LDS, the
+// per-sphere geometry + material records read by shading, once per persistent block. Blocks of
+// RT_LBVH_BLOCK threads share one staged copy.
+template <bool LDS, bool COUNT, bool NODE16, bool SCENE_LDS, uint32_t BLOCK>
+__global__ __launch_bounds__(BLOCK, RT_TRACE_WAVES_PER_SIMD) void rt_trace_lbvh_kernel(const rt::TraceParams P) {
     extern __shared__ float4 lds[];
-    const float4* nodes4 = reinterpret_cast<const float4*>(P.nodes);
+    const float4* nodes4 = NODE16 ? reinterpret_cast<const float4*>(P.nodes16)
+                                  : reinterpret_cast<const float4*>(P.nodes);
     const float4* leaf4 = reinterpret_cast<const float4*>(P.leaf_geom);
     const uint32_t* leaf_ids = P.leaf_ids;
-    if (LDS) {  // stage nodes, leaf spheres and leaf ids once per (persistent) block
-        const uint32_t n_node4 = 2u * P.n_nodes, n_leaf4 = P.n_leaf, n_id4 = (P.n_leaf + 3u) / 4u;
-        for (uint32_t i = threadIdx.x; i < n_node4; i += blockDim.x) lds[i] = nodes4[i];
-        for (uint32_t i = threadIdx.x; i < n_leaf4; i += blockDim.x) lds[n_node4 + i] = leaf4[i];
+    const float4* geom4 = reinterpret_cast<const float4*>(P.geom);
+    const float4* mat4 = reinterpret_cast<const float4*>(P.mat);
+    if (LDS) {
+        const uint32_t n_node4 = (NODE16 ? 1u : 2u) * P.n_nodes, n_leaf4 = P.n_leaf, n_id4 = (P.n_leaf + 3u) / 4u;
+        for (uint32_t i = threadIdx.x; i < n_node4; i += BLOCK) lds[i] = nodes4[i];
+        for (uint32_t i = threadIdx.x; i < n_leaf4; i += BLOCK) lds[n_node4 + i] = leaf4[i];
         const uint4* ids4 = reinterpret_cast<const uint4*>(P.leaf_ids);
-        for (uint32_t i = threadIdx.x; i < n_id4; i += blockDim.x) {
+        for (uint32_t i = threadIdx.x; i < n_id4; i += BLOCK) {
             const uint4 v = ids4[i];
             lds[n_node4 + n_leaf4 + i] = make_float4(__uint_as_float(v.x), __uint_as_float(v.y),
                                                      __uint_as_float(v.z), __uint_as_float(v.w));
+        }
+        const uint32_t base = n_node4 + n_leaf4 + n_id4;
+        if (SCENE_LDS) {
+            const uint32_t ng = P.n_spheres, nm = 2u * P.n_spheres;
+            for (uint32_t i = threadIdx.x; i < ng; i += BLOCK) lds[base + i] = geom4[i];
+            for (uint32_t i = threadIdx.x; i < nm; i += BLOCK) lds[base + ng + i] = mat4[i];
+            geom4 = lds + base;
+            mat4 = lds + base + ng;
         }
         __syncthreads();
         nodes4 = lds;
         leaf4 = lds + n_node4;
         leaf_ids = reinterpret_cast<const uint32_t*>(lds + n_node4 + n_leaf4);
     }
-    lbvh_classic<COUNT>(P, nodes4, leaf4, leaf_ids);
+    lbvh_classic<COUNT, NODE16>(P, nodes4, leaf4, leaf_ids, geom4, mat4);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -636,7 +819,9 @@ __global__ __launch_bounds__(BLOCK, RT_TRACE_WAVES_PER_SIMD) void rt_trace_lbvh2
         STAMP(3);
         if (st == ST_TRACING) {
             n_seg++;
-            if (!shade(P, ps, r.bi, r.best, r.o, r.d)) st = ST_NEED_SAMPLE;
+            if (!shade(P, reinterpret_cast<const float4*>(P.geom), reinterpret_cast<const float4*>(P.mat),
+                       ps, r.bi, r.best, r.o, r.d))
+                st = ST_NEED_SAMPLE;
         }
     }
     STAMP_FLUSH;
@@ -694,14 +879,20 @@ namespace rt {
 #endif
 constexpr uint32_t kLbvh2Block = RT_LBVH2_BLOCK;
 
+constexpr uint32_t kLbvhBlock = RT_LBVH_BLOCK;
+
+#define RT_LBVH_FN(L, C, N16, S) reinterpret_cast<const void*>(rt_trace_lbvh_kernel<L, C, N16, S, kLbvhBlock>)
 static const void* pick(uint32_t accel, bool count) {
     switch (accel) {
         case ACCEL_BRUTE:
             return count ? reinterpret_cast<const void*>(rt_trace_brute_kernel<true>)
                          : reinterpret_cast<const void*>(rt_trace_brute_kernel<false>);
         case ACCEL_LBVH_LDS:
-            return count ? reinterpret_cast<const void*>(rt_trace_lbvh_kernel<true, true>)
-                         : reinterpret_cast<const void*>(rt_trace_lbvh_kernel<true, false>);
+            return count ? RT_LBVH_FN(true, true, false, false) : RT_LBVH_FN(true, false, false, false);
+        case ACCEL_LBVH_LDS_SCENE:
+            return count ? RT_LBVH_FN(true, true, false, true) : RT_LBVH_FN(true, false, false, true);
+        case ACCEL_LBVH16_LDS:
+            return count ? RT_LBVH_FN(true, true, true, false) : RT_LBVH_FN(true, false, true, false);
         case ACCEL_LBVH2:
             return count ? reinterpret_cast<const void*>(rt_trace_lbvh2_kernel<false, true, kLbvh2Block>)
                          : reinterpret_cast<const void*>(rt_trace_lbvh2_kernel<false, false, kLbvh2Block>);
@@ -709,13 +900,17 @@ static const void* pick(uint32_t accel, bool count) {
             return count ? reinterpret_cast<const void*>(rt_trace_lbvh2_kernel<true, true, kLbvh2Block>)
                          : reinterpret_cast<const void*>(rt_trace_lbvh2_kernel<true, false, kLbvh2Block>);
         default:
-            return count ? reinterpret_cast<const void*>(rt_trace_lbvh_kernel<false, true>)
-                         : reinterpret_cast<const void*>(rt_trace_lbvh_kernel<false, false>);
+            return count ? RT_LBVH_FN(false, true, false, false) : RT_LBVH_FN(false, false, false, false);
     }
 }
+#undef RT_LBVH_FN
 
 uint32_t block_size(uint32_t accel) {
-    return (accel == ACCEL_LBVH2 || accel == ACCEL_LBVH2_LDS) ? kLbvh2Block : 256u;
+    switch (accel) {
+        case ACCEL_LBVH2: case ACCEL_LBVH2_LDS: return kLbvh2Block;
+        case ACCEL_BRUTE: return 256u;
+        default: return kLbvhBlock;
+    }
 }
 
 hipError_t launch_trace(const TraceParams& P, uint32_t accel, bool count, int grid, size_t lds_bytes,

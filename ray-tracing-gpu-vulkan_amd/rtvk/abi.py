@@ -110,6 +110,7 @@ EXPORTS = {
     "rt_store_ppm": (_I, [ctypes.c_char_p, _P, _U32, _U32]),
     "rt_debug_math": (_I, [_I, _I, _P, _P, _U32]),
     "rt_debug_stamps": (_I, [_P, _P]),
+    "rt_debug_walk_hist": (_I, [_P, _P]),
     "ray_trace": (None, [_U32, ctypes.c_bool, _U32, _U32, _U32]),
 }
 
@@ -127,7 +128,8 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = Path(path) if path else LIB_PATH
+    # RT_LIB (diagnostics / A-B profiling only) points at an alternative build of the same ABI.
+    p = Path(path) if path else Path(os.environ.get("RT_LIB", LIB_PATH))
     # torch ships its own libamdhip64.so (SONAME libamdhip64.so.7). Importing torch first makes
     # the loader reuse that copy for this library too: one HIP runtime per process, so torch
     # device pointers and streams are valid here. Loading this library first would let torch

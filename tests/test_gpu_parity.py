@@ -17,6 +17,8 @@ pytestmark = pytest.mark.gpu
 GOLDEN = Path(__file__).resolve().parent / "golden"
 BRUTE, LBVH = 1, 2
 LBVH_ORDERED = 3   # test-only alias: accel LBVH with the ordered two-wide walk (options.reserved[1] = 2)
+LBVH_COMPACT = 4   # test-only alias: accel LBVH, escape-link walk over 16-B nodes (options.reserved[1] = 4)
+WALK_FORM = {LBVH_ORDERED: 2, LBVH_COMPACT: 4}
 
 
 @pytest.fixture(scope="module")
@@ -50,10 +52,9 @@ def gpu_render(rtvk, renderer, torch, spheres, rci_u32, band_w, band_h, rows=Non
     out = torch.full((band_h, band_w, 4), 7, dtype=torch.uint8, device="cuda")
     rows_t = None if rows is None else torch.from_numpy(np.asarray(rows, np.int32)).cuda()
     opt = rtvk.make_options(max_depth=max_depth, seed_mode=seed_mode, rng_mode=rng_mode,
-                            accel=LBVH if accel == LBVH_ORDERED else accel,
+                            accel=LBVH if accel in WALK_FORM else accel,
                             accumulate=accumulate, sample_base=sample_base, count_tests=count)
-    if accel == LBVH_ORDERED:
-        opt.reserved[1] = 2
+    opt.reserved[1] = WALK_FORM.get(accel, 0)
     renderer.render_device(rci, acc, out, rows=rows_t, options=opt)
     torch.cuda.synchronize()
     st = renderer.stats()
@@ -109,7 +110,7 @@ def test_math_primitives_bit_exact(rtvk, torch, oracle, op):
 
 
 # ---- golden fixtures --------------------------------------------------------------------------
-@pytest.mark.parametrize("accel", [BRUTE, LBVH, LBVH_ORDERED])
+@pytest.mark.parametrize("accel", [BRUTE, LBVH, LBVH_ORDERED, LBVH_COMPACT])
 @pytest.mark.parametrize("case", ["g64x36_spp4", "g48x32_spp3_depth3_local", "g40x24_spp2_counter"])
 def test_golden(rtvk, renderer, torch, oracle, case, accel):
     m = json.loads((GOLDEN / f"{case}.json").read_text())
@@ -135,7 +136,7 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("accel", [BRUTE, LBVH, LBVH_ORDERED])
+@pytest.mark.parametrize("accel", [BRUTE, LBVH, LBVH_ORDERED, LBVH_COMPACT])
 @pytest.mark.parametrize("case", range(len(CASES)))
 def test_vs_oracle(rtvk, renderer, torch, oracle, case, accel):
     W, H, oy, bh, spp, t, K, kw = CASES[case]
@@ -151,7 +152,7 @@ def test_empty_and_single_sphere(rtvk, renderer, torch, oracle):
     rci = oracle.render_call_info(2, 20, 10)
     for sc in (np.zeros((0, 80), np.uint8), oracle.generate_scene()[:1], oracle.generate_scene()[3:4]):
         ra, ro, _ = oracle.render(sc, rci, 20, 10)
-        for accel in (BRUTE, LBVH, LBVH_ORDERED):
+        for accel in (BRUTE, LBVH, LBVH_ORDERED, LBVH_COMPACT):
             a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, 20, 10, accel=accel)
             assert_same(a, o, ra, ro)
 
@@ -211,8 +212,9 @@ def test_lbvh_equals_brute_full_size(rtvk, renderer, torch, oracle, W, H, spp, K
     al, ol, sl = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH)
     assert_same(al, ol, ab, ob)
     assert sb.segments == sl.segments
-    ao, oo, so = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH_ORDERED)
-    assert_same(ao, oo, ab, ob)
+    for form in (LBVH_ORDERED, LBVH_COMPACT):
+        ao, oo, so = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=form)
+        assert_same(ao, oo, ab, ob)
 
 
 def test_band_split_invariance_full_size(rtvk, renderer, torch, oracle):
@@ -232,3 +234,19 @@ def test_count_variant_same_image(rtvk, renderer, torch, oracle):
     a1, o1, s1 = gpu_render(rtvk, renderer, torch, sc, rci, 128, 72, accel=LBVH, count=True)
     assert_same(a1, o1, a0, o0)
     assert s1.box_tests > 0 and s1.sphere_tests > 0 and s0.box_tests == 0
+
+
+@pytest.mark.parametrize("cam", [(500.0, 300.0, -200.0), (0.0, 4000.0, 0.5), (13.0, 0.05, -3.0)])
+def test_far_and_grazing_cameras(rtvk, renderer, torch, oracle, cam):
+    """Cameras outside the padded scene radius force a re-pad of the LBVH boxes; a camera just
+    above the ground makes grazing primary rays. LBVH must equal brute force and the oracle."""
+    W, H = 48, 32
+    sc = oracle.generate_scene()
+    rci = oracle.render_call_info(2, W, H)
+    f = rci.view(np.float32)
+    f[8:11] = cam
+    f[12:15] = [-cam[0], -cam[1], -cam[2]]
+    ra, ro, _ = oracle.render(sc, rci, W, H)
+    for accel in (BRUTE, LBVH, LBVH_ORDERED, LBVH_COMPACT):
+        a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=accel)
+        assert_same(a, o, ra, ro)
