@@ -75,6 +75,9 @@ def main() -> int:
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--accel", choices=["lbvh", "brute"], default="lbvh")
     ap.add_argument("--grid", type=int, default=11, help="scene grid half extent (11: 488 spheres)")
+    ap.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=None,
+                    help="BASELINE.json config preset: 2/3/4 = 1920x1080 at 100/10000/10000 spp, "
+                         "5 = 3840x2160, 99 860 spheres, 1000 spp (overrides --width/--height/--spp/--grid)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-brute-line", action="store_true", help="skip the brute-force side measurement")
     ap.add_argument("--profile", action="store_true", help="short run for rocprofv3 (no side legs)")
@@ -95,16 +98,32 @@ def main() -> int:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    # RT_SHARE_DEVICE=1 (rehearsal only): map ranks onto the visible devices round robin, so the
+    # multi-rank code path can be exercised on a one-GPU box.
+    ndev = torch.cuda.device_count()
+    # RCCL refuses two ranks on one device, so the rehearsal runs over gloo with host staging.
+    shared = os.environ.get("RT_SHARE_DEVICE") == "1" and ndev > 0
+    if shared:
+        local = local % ndev
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
+    if args.config is not None:
+        args.width, args.height = (3840, 2160) if args.config == 5 else (1920, 1080)
+        args.spp = {2: 100, 3: 10000, 4: 10000, 5: 1000}[args.config]
+        args.grid = 158 if args.config == 5 else 11
     W, H, spp = args.width, args.height, args.spp
     accel = abi.RT_ACCEL_BRUTE if args.accel == "brute" else abi.RT_ACCEL_LBVH
     renderer = rtvk.Renderer(local)
     scene = rtvk.generateRandomScene(0.0, args.grid)
+    t_scene = time.perf_counter()
     renderer.set_scene(scene)
+    t_scene = time.perf_counter() - t_scene
     rci = rtvk.canonical_render_call_info(spp, W, H)
     opts = rtvk.make_options(accel=accel)
     opts.reserved[1] = args.walk
@@ -138,7 +157,7 @@ def main() -> int:
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if shared else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / max(1, len(ev))
@@ -197,10 +216,13 @@ def main() -> int:
             "dtype": "f32",
             "data": f"synthetic: canonical scene generateRandomScene(t=0), {len(scene)} spheres, "
                     "camera (13,11,-3) -> origin, global per-pixel seeds TEA(TEA(x,y),0)",
-            "config": {"workload": f"rtiow-{W}x{H}-{spp}spp-depth50 (BASELINE config 2 input)",
+            "config": {"workload": f"rtiow-{W}x{H}-{spp}spp-depth50"
+                                   + (f" (BASELINE config {args.config})" if args.config else
+                                      " (BASELINE config 2 input)" if (W, H, spp, args.grid) == (1920, 1080, 100, 11) else ""),
                        "width": W, "height": H, "spp": spp, "depth": 50, "spheres": len(scene),
                        "accel": args.accel, "parallelism": f"row-strips x{world} + rccl gather"},
             "segments_per_sample": round(st.segments / max(1, st.samples), 4),
+            "scene_setup_ms": round(t_scene * 1e3, 2),
             "msegments_per_s": round(st.segments / max(1, st.samples) * value, 2),
             "roofline": roof,
             "context": {"reference_rx6800xt_vulkan_rt_msamples": 1658.9,

@@ -19,6 +19,8 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "rt_bvh.h"
@@ -29,6 +31,7 @@ namespace {
 
 constexpr uint32_t kLeafMax = 4;
 constexpr uint32_t kBigMax = 64;
+constexpr bool kDefaultSah = false;
 
 inline uint32_t expand_bits(uint32_t v) {  // 10 bits -> every third bit of 30
     v = (v * 0x00010001u) & 0xFF0000FFu;
@@ -47,8 +50,9 @@ struct Prim {
 // kLeafMax slots padded with never-hit dummies so the device loads a leaf as 4 records at once.
 struct Builder {
     const Sphere* sph;
-    const std::vector<Prim>& prims;
+    std::vector<Prim>& prims;
     HostBvh& out;
+    bool sah;
 
     void bounds(uint32_t lo, uint32_t hi, float* bmin, float* bmax) const {
         bmin[0] = bmin[1] = bmin[2] = INFINITY;
@@ -74,6 +78,78 @@ struct Builder {
             if (ns < hi - 1 && __builtin_clz(a ^ prims[ns].code) > common) s = ns;
         } while (step > 1);
         return s + 1;
+    }
+
+    // Binned surface-area split of [lo, hi) (hi - lo > kLeafMax): 32 centroid bins per axis, cost
+    // = sum over both sides of area x leaves needed (a leaf costs the same for 1..4 spheres, the
+    // device always tests four slots). Reorders prims[lo, hi) and returns the split index;
+    // degenerate centroid bounds fall back to a median split on the widest axis.
+    uint32_t split_sah(uint32_t lo, uint32_t hi) {
+        constexpr int kBins = 32;
+        float cmin[3] = {INFINITY, INFINITY, INFINITY}, cmax[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (uint32_t i = lo; i < hi; i++) {
+            const rt_vec4& g = sph[prims[i].id].geometry;
+            const float c[3] = {g.x, g.y, g.z};
+            for (int k = 0; k < 3; k++) { cmin[k] = std::min(cmin[k], c[k]); cmax[k] = std::max(cmax[k], c[k]); }
+        }
+        auto area = [](const float* l, const float* h) {
+            const double ex = double(h[0]) - l[0], ey = double(h[1]) - l[1], ez = double(h[2]) - l[2];
+            return ex * ey + ey * ez + ez * ex;
+        };
+        auto bin_of = [&](int k, float c) {
+            const float ext = cmax[k] - cmin[k];
+            int b = int(double(c - cmin[k]) / ext * kBins);
+            return std::min(std::max(b, 0), kBins - 1);
+        };
+        double best_cost = INFINITY;
+        int best_axis = -1, best_plane = 0;
+        for (int k = 0; k < 3; k++) {
+            if (!(cmax[k] > cmin[k])) continue;
+            float bl[kBins][3], bh[kBins][3];
+            uint32_t cnt[kBins] = {};
+            for (int b = 0; b < kBins; b++)
+                for (int j = 0; j < 3; j++) { bl[b][j] = INFINITY; bh[b][j] = -INFINITY; }
+            for (uint32_t i = lo; i < hi; i++) {
+                const rt_vec4& g = sph[prims[i].id].geometry;
+                const float c[3] = {g.x, g.y, g.z};
+                const int b = bin_of(k, c[k]);
+                cnt[b]++;
+                for (int j = 0; j < 3; j++) {
+                    bl[b][j] = std::min(bl[b][j], c[j] - g.w);
+                    bh[b][j] = std::max(bh[b][j], c[j] + g.w);
+                }
+            }
+            double right_area[kBins];
+            uint32_t right_cnt[kBins];
+            float rl[3] = {INFINITY, INFINITY, INFINITY}, rh[3] = {-INFINITY, -INFINITY, -INFINITY};
+            uint32_t rc = 0;
+            for (int b = kBins - 1; b > 0; b--) {
+                rc += cnt[b];
+                for (int j = 0; j < 3; j++) { rl[j] = std::min(rl[j], bl[b][j]); rh[j] = std::max(rh[j], bh[b][j]); }
+                right_area[b] = rc ? area(rl, rh) : 0.0;
+                right_cnt[b] = rc;
+            }
+            float ll[3] = {INFINITY, INFINITY, INFINITY}, lh[3] = {-INFINITY, -INFINITY, -INFINITY};
+            uint32_t lc = 0;
+            for (int b = 0; b + 1 < kBins; b++) {   // plane between bin b and b + 1
+                lc += cnt[b];
+                for (int j = 0; j < 3; j++) { ll[j] = std::min(ll[j], bl[b][j]); lh[j] = std::max(lh[j], bh[b][j]); }
+                const uint32_t rcnt = right_cnt[b + 1];
+                if (lc == 0 || rcnt == 0) continue;
+                const double cost = area(ll, lh) * ((lc + kLeafMax - 1) / kLeafMax) +
+                                    right_area[b + 1] * ((rcnt + kLeafMax - 1) / kLeafMax);
+                if (cost < best_cost) { best_cost = cost; best_axis = k; best_plane = b; }
+            }
+        }
+        if (best_axis < 0) {   // all centroids coincide on every axis: split by count
+            return (lo + hi) / 2;
+        }
+        const auto mid = std::stable_partition(prims.begin() + lo, prims.begin() + hi, [&](const Prim& p) {
+            const rt_vec4& g = sph[p.id].geometry;
+            const float c = best_axis == 0 ? g.x : best_axis == 1 ? g.y : g.z;
+            return bin_of(best_axis, c) <= best_plane;
+        });
+        return uint32_t(mid - prims.begin());
     }
 
     // Returns the reference of the subtree [lo, hi) in the two-wide layout (inner nodes emitted
@@ -104,7 +180,7 @@ struct Builder {
             ref = kLeafFlag | (first << 3) | (hi - lo);
             *height = 0;
         } else {
-            const uint32_t s = split(lo, hi);
+            const uint32_t s = sah ? split_sah(lo, hi) : split(lo, hi);
             const uint32_t me2 = uint32_t(out.nodes2.size());
             out.nodes2.push_back(Bvh2Node{});
             float l0[3], h0[3], l1[3], h1[3];
@@ -176,7 +252,9 @@ void build_lbvh_host(const Sphere* sph, uint32_t n, HostBvh& out) {
     std::stable_sort(prims.begin(), prims.end(), [](const Prim& a, const Prim& b) { return a.code < b.code; });
     // 3-4. hierarchy in depth-first order
     out.nodes.reserve(2 * prims.size());
-    Builder b{sph, prims, out};
+    const char* env = std::getenv("RT_BVH_BUILDER");   // A/B switch: "morton" or "sah"
+    const bool sah = env ? std::strcmp(env, "morton") != 0 : kDefaultSah;
+    Builder b{sph, prims, out, sah};
     float bmin[3], bmax[3];
     out.root2 = b.build(0, uint32_t(prims.size()), bmin, bmax, &out.depth2);
     for (BvhNode& nd : out.nodes)

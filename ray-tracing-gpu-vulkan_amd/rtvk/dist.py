@@ -62,6 +62,10 @@ class DistributedRenderer:
         self.accum = torch.zeros((self.nmax, width, 4), dtype=torch.float32, device=device)
         self.out = torch.zeros((self.nmax, width, 4), dtype=torch.uint8, device=device)
         self.n = n
+        # gloo moves host tensors only: stage device bands through host memory (rehearsal of the
+        # multi-rank path on a shared GPU; RCCL gathers device memory directly).
+        self.staged = (self.world > 1 and getattr(device, "type", str(device)) != "cpu"
+                       and dist.get_backend() == "gloo")
         if self.rank == 0:
             self.all_rows = [torch.from_numpy(strip_rows(r, self.world, height, strip)).to(device)
                              for r in range(self.world)]
@@ -76,10 +80,9 @@ class DistributedRenderer:
         self.render_band(self.rows, self.accum[: self.n], self.out[: self.n])
         if self.world == 1:
             return self.accum[: self.n], self.out[: self.n]
-        dist = self.dist
         if self.gather_accum:
-            dist.gather(self.accum, self.g_accum if self.rank == 0 else None, dst=0)
-        dist.gather(self.out, self.g_out if self.rank == 0 else None, dst=0)
+            self._gather(self.accum, self.g_accum if self.rank == 0 else None)
+        self._gather(self.out, self.g_out if self.rank == 0 else None)
         if self.rank != 0:
             return None
         for r in range(self.world):
@@ -88,6 +91,18 @@ class DistributedRenderer:
             self.assemble(self.g_accum[r][:k] if self.gather_accum else None, self.g_out[r][:k], rows,
                           self.full_accum if self.gather_accum else None, self.full_out)
         return self.full_accum, self.full_out
+
+    def _gather(self, band, glist):
+        dist = self.dist
+        if not self.staged:
+            dist.gather(band, glist, dst=0)
+            return
+        host = band.cpu()
+        hlist = [self.torch.empty_like(host) for _ in range(self.world)] if self.rank == 0 else None
+        dist.gather(host, hlist, dst=0)
+        if self.rank == 0:
+            for g, h in zip(glist, hlist):
+                g.copy_(h)
 
 
 def hip_band_renderer(renderer, rci, options, stream=None):

@@ -250,3 +250,25 @@ def test_far_and_grazing_cameras(rtvk, renderer, torch, oracle, cam):
     for accel in (BRUTE, LBVH, LBVH_ORDERED, LBVH_COMPACT):
         a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=accel)
         assert_same(a, o, ra, ro)
+
+
+def test_scatter_rows_reassembles_strips(rtvk, renderer, torch, oracle):
+    """The multi-GPU reassembly on device: strips rendered through row maps, scattered back with
+    rt_scatter_rows, equal the full-frame render (rtvk.dist's rank-0 step)."""
+    from rtvk.dist import strip_rows
+    W, H, world = 64, 45, 3
+    sc = oracle.generate_scene()
+    rci = oracle.render_call_info(2, W, H)
+    ra, ro, _ = oracle.render(sc, rci, W, H)
+    renderer.set_scene(sc)
+    rci_c = rtvk.RenderCallInfo.from_buffer_copy(rci.tobytes())
+    full_a = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+    full_o = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+    for rank in range(world):
+        rows = torch.from_numpy(strip_rows(rank, world, H)).cuda()
+        a = torch.zeros((rows.numel(), W, 4), dtype=torch.float32, device="cuda")
+        o = torch.zeros((rows.numel(), W, 4), dtype=torch.uint8, device="cuda")
+        renderer.render_device(rci_c, a, o, rows=rows, options=rtvk.make_options())
+        renderer.scatter_rows(a, o, rows, full_a, full_o)
+    torch.cuda.synchronize()
+    assert_same(full_a.cpu().numpy(), full_o.cpu().numpy(), ra, ro)
