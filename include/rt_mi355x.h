@@ -114,8 +114,21 @@ int rt_canonical_render_call_info(uint32_t spp, uint32_t width, uint32_t height,
 /* ---- device API ------------------------------------------------------------------- */
 int rt_context_create(int device, rt_context** out);
 int rt_context_destroy(rt_context* ctx);
-/* Uploads `count` spheres (host memory) and builds the acceleration structures on the device. */
+/* Uploads `count` spheres (host memory) and builds the acceleration structures on the device
+ * (parallel LBVH build, rt_build.hip; RT_BVH_BUILD=host selects the host builder for A/B).
+ * Returns after the build (one small device-to-host copy of the tree's counts). */
 int rt_set_scene(rt_context* ctx, const Sphere* spheres, uint32_t count, void* stream);
+/* As rt_set_scene, spheres already in DEVICE memory (read during the call only). */
+int rt_set_scene_device(rt_context* ctx, const Sphere* d_spheres, uint32_t count, void* stream);
+/*
+ * Per-frame update of an animated scene (the reference rebuilds BLAS/TLAS every frame,
+ * src/vulkan.h:1020-1059, because spheres move with t, src/scene.h:94-111): same count, new
+ * positions / radii / materials; keeps the tree topology of the last device build and refits its
+ * boxes, records and padding on the device. Without a device-built tree of the same count it
+ * performs a full rt_set_scene. Rendering stays exact (any topology is), only walk cost changes.
+ */
+int rt_refit_scene(rt_context* ctx, const Sphere* spheres, uint32_t count, void* stream);
+int rt_refit_scene_device(rt_context* ctx, const Sphere* d_spheres, uint32_t count, void* stream);
 /*
  * Render one band on ctx's device, asynchronously on `stream` (hipStream_t; NULL = default).
  *   rci          host pointer; rci->offset / rci->image_size / camera / spp / number as in the UBO.
@@ -158,6 +171,13 @@ int rt_debug_stamps(rt_context* ctx, uint64_t* out8);
 /* Diagnostic: histogram of LBVH box tests per segment of the last instrumented launch
  * (options.reserved[0] & 1), 2 x 64 bins: [0] segments that miss, [1] segments that hit. */
 int rt_debug_walk_hist(rt_context* ctx, uint64_t* out128);
+
+/* Diagnostic (tests): copies one scene array of ctx to host memory. what: 0 geometry records,
+ * 1 radii, 2 material records, 3 big-sphere ids, 4 LBVH nodes (padded), 5 LBVH nodes (unpadded),
+ * 6 leaf geometry, 7 leaf ids, 8 info {u32 n_spheres, n_big, n_nodes, n_leaf_slots,
+ * device_built, 0; f32 small_rmax, scene_radius}. *bytes = the array's size; RT_ERR_INVALID_ARGUMENT
+ * when it exceeds capacity. */
+int rt_debug_scene(rt_context* ctx, uint32_t what, void* out, uint64_t capacity, uint64_t* bytes);
 
 /* src/ray_trace.h:9-15 — identical symbol and parameter list. Renders the canonical scene once
  * (t = 0), prints the frame time, stores `render.ppm` when storeRenderResult, and returns. */

@@ -10,6 +10,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <memory>
@@ -20,6 +21,7 @@
 
 #include "../../include/rt_abi.h"
 #include "../../include/rt_mi355x.h"
+#include "rt_build.h"
 #include "rt_bvh.h"
 #include "rt_internal.h"
 
@@ -53,6 +55,13 @@ struct rt_context {
     std::vector<rt::Bvh2Node> nodes2_host;
     float scene_radius = 0.0f;
     float pad_radius = 0.0f;
+    // device-side build (rt_build.hip): scratch kept for refits, and a staging copy of
+    // host-provided spheres
+    float padded_for = 0.0f;   // pad radius the device node copy currently carries
+    bool gpu_tree = false;
+    rt::BuildWorkspace ws;
+    Sphere* d_spheres = nullptr;
+    uint32_t d_spheres_cap = 0;
 };
 
 namespace {
@@ -340,20 +349,23 @@ int rt_context_destroy(rt_context* ctx) {
     DeviceGuard g(ctx->device);
     (void)hipDeviceSynchronize();
     free_scene(ctx);
+    rt::build_release(ctx->ws);
+    if (ctx->d_spheres) (void)hipFree(ctx->d_spheres);
     if (ctx->counters) (void)hipFree(ctx->counters);
     delete ctx;
     return RT_OK;
 }
 
-int rt_set_scene(rt_context* ctx, const Sphere* spheres, uint32_t count, void* stream) {
-    if (!ctx) return fail(RT_ERR_INVALID_ARGUMENT, "ctx is NULL");
-    if (!spheres && count) return fail(RT_ERR_INVALID_ARGUMENT, "spheres is NULL");
-    if (count >= (1u << 27)) return fail(RT_ERR_INVALID_ARGUMENT, "too many spheres");
+}  // extern "C"
+
+namespace {
+
+// Host-built tree (rt_bvh.cpp): the A/B reference for the device builder and the only source of
+// the alternative walk layouts (ordered two-wide, compact binary16 nodes).
+int set_scene_host(rt_context* ctx, const Sphere* spheres, uint32_t count, hipStream_t st) {
     try {
-        DeviceGuard g(ctx->device);
-        hipStream_t st = static_cast<hipStream_t>(stream);
-        RT_HIP(hipStreamSynchronize(st));  // previous launches may still read the old scene
         free_scene(ctx);
+        ctx->gpu_tree = false;
         std::vector<rt::GeomRec> geom(count);
         std::vector<float> radius(count);
         std::vector<rt::MatRec> mat(count);
@@ -394,6 +406,7 @@ int rt_set_scene(rt_context* ctx, const Sphere* spheres, uint32_t count, void* s
         }
         ctx->scene_radius = R;
         ctx->pad_radius = R * 1.01f + 100.0f;
+        ctx->padded_for = ctx->pad_radius;
         ctx->nodes_host = bvh.nodes;
         ctx->nodes2_host = bvh.nodes2;
         pad_nodes(ctx->nodes_host, bvh.nodes, ctx->nodes2_host, bvh.nodes2, pad_for(ctx->pad_radius));
@@ -424,6 +437,131 @@ int rt_set_scene(rt_context* ctx, const Sphere* spheres, uint32_t count, void* s
     }
 }
 
+template <typename T>
+int scene_alloc(rt_context* ctx, T** dst, size_t count) {
+    void* p = nullptr;
+    RT_HIP(hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T) + 16));
+    ctx->scene_allocs.push_back(p);
+    *dst = static_cast<T*>(p);
+    return RT_OK;
+}
+
+// Device-built tree (rt_build.hip) from spheres already in device memory. refit: keep the
+// topology of the previous build over the same count (positions / radii / materials may change).
+int set_scene_gpu(rt_context* ctx, const Sphere* d_sph, uint32_t count, hipStream_t st, bool refit) {
+    rt::DeviceScene& d = ctx->scene;
+    if (!refit) {
+        free_scene(ctx);
+        ctx->gpu_tree = true;
+        if (int rc = scene_alloc(ctx, &d.geom, (size_t(count) + 7u) & ~size_t(7))) return rc;
+        if (int rc = scene_alloc(ctx, &d.radius, count)) return rc;
+        if (int rc = scene_alloc(ctx, &d.mat, count)) return rc;
+        if (int rc = scene_alloc(ctx, &d.big_ids, 64)) return rc;
+        if (int rc = scene_alloc(ctx, &d.nodes, 2 * size_t(count))) return rc;
+        if (int rc = scene_alloc(ctx, &d.nodes_raw, 2 * size_t(count))) return rc;
+        if (int rc = scene_alloc(ctx, &d.leaf_geom, 4 * size_t(count))) return rc;
+        if (int rc = scene_alloc(ctx, &d.leaf_ids, 4 * size_t(count))) return rc;
+    }
+    rt::BuildOutputs o{d.geom, d.radius, d.mat, d.big_ids, d.nodes, d.nodes_raw, d.leaf_geom, d.leaf_ids};
+    rt::BuildSummary sm;
+    const hipError_t e = rt::build_scene_gpu(ctx->ws, d_sph, count, o, refit, st, &sm);
+    if (e != hipSuccess) {
+        if (!refit) free_scene(ctx);
+        return fail(e == hipErrorOutOfMemory ? RT_ERR_OUT_OF_MEMORY : RT_ERR_DEVICE,
+                    std::string("device LBVH build: ") + hipGetErrorString(e));
+    }
+    d.n_spheres = count;
+    d.n_big = sm.n_big;
+    d.n_nodes = sm.n_nodes;
+    d.n_leaf = sm.n_leaf_slots;
+    d.small_rmax = rt::summary_float(sm.rmax_o);
+    d.nodes16 = nullptr;
+    d.nodes2 = nullptr;
+    d.n_nodes2 = d.root2 = d.depth2 = 0;
+    ctx->scene_radius = rt::summary_float(sm.R_o);
+    ctx->pad_radius = ctx->scene_radius * 1.01f + 100.0f;   // the build padded for this radius
+    ctx->padded_for = ctx->pad_radius;
+    ctx->nodes_host.clear();
+    ctx->nodes2_host.clear();
+    const size_t lds = size_t(2 * d.n_nodes + d.n_leaf + (d.n_leaf + 3) / 4) * 16;
+    ctx->lds_bytes = (d.n_nodes && lds <= kMaxLdsBvhBytes) ? lds : 0;
+    const size_t lds_scene = lds + size_t(count) * 48u;
+    ctx->lds_scene_bytes = (d.n_nodes && lds_scene <= kMaxLdsSceneBytes) ? lds_scene : 0;
+    ctx->lds16_bytes = 0;
+    ctx->lds2_bytes = 0;
+    return RT_OK;
+}
+
+bool host_build_requested() {
+    const char* b = std::getenv("RT_BVH_BUILD");   // "host" | "gpu" (default)
+    const char* f = std::getenv("RT_BVH_BUILDER");  // host builder form (A/B): implies host
+    return (b && std::strcmp(b, "host") == 0) || f;
+}
+
+int stage_spheres(rt_context* ctx, const Sphere* spheres, uint32_t count, hipStream_t st) {
+    if (count > ctx->d_spheres_cap) {
+        if (ctx->d_spheres) (void)hipFree(ctx->d_spheres);
+        ctx->d_spheres = nullptr;
+        ctx->d_spheres_cap = 0;
+        void* p = nullptr;
+        RT_HIP(hipMalloc(&p, size_t(count) * sizeof(Sphere)));
+        ctx->d_spheres = static_cast<Sphere*>(p);
+        ctx->d_spheres_cap = count;
+    }
+    if (count) RT_HIP(hipMemcpyAsync(ctx->d_spheres, spheres, size_t(count) * sizeof(Sphere), hipMemcpyHostToDevice, st));
+    return RT_OK;
+}
+
+int check_scene_args(rt_context* ctx, const Sphere* spheres, uint32_t count) {
+    if (!ctx) return fail(RT_ERR_INVALID_ARGUMENT, "ctx is NULL");
+    if (!spheres && count) return fail(RT_ERR_INVALID_ARGUMENT, "spheres is NULL");
+    if (count >= (1u << 27)) return fail(RT_ERR_INVALID_ARGUMENT, "too many spheres");
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_set_scene(rt_context* ctx, const Sphere* spheres, uint32_t count, void* stream) {
+    if (int rc = check_scene_args(ctx, spheres, count)) return rc;
+    DeviceGuard g(ctx->device);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    RT_HIP(hipStreamSynchronize(st));  // previous launches may still read the old scene
+    if (host_build_requested()) return set_scene_host(ctx, spheres, count, st);
+    if (int rc = stage_spheres(ctx, spheres, count, st)) return rc;
+    return set_scene_gpu(ctx, ctx->d_spheres, count, st, false);
+}
+
+int rt_set_scene_device(rt_context* ctx, const Sphere* d_spheres, uint32_t count, void* stream) {
+    if (int rc = check_scene_args(ctx, d_spheres, count)) return rc;
+    DeviceGuard g(ctx->device);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    RT_HIP(hipStreamSynchronize(st));
+    return set_scene_gpu(ctx, d_spheres, count, st, false);
+}
+
+int rt_refit_scene(rt_context* ctx, const Sphere* spheres, uint32_t count, void* stream) {
+    if (int rc = check_scene_args(ctx, spheres, count)) return rc;
+    if (!ctx->gpu_tree || count != ctx->scene.n_spheres || ctx->ws.topo_n != count)
+        return rt_set_scene(ctx, spheres, count, stream);   // no topology to reuse: full build
+    DeviceGuard g(ctx->device);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    RT_HIP(hipStreamSynchronize(st));
+    if (int rc = stage_spheres(ctx, spheres, count, st)) return rc;
+    return set_scene_gpu(ctx, ctx->d_spheres, count, st, true);
+}
+
+int rt_refit_scene_device(rt_context* ctx, const Sphere* d_spheres, uint32_t count, void* stream) {
+    if (int rc = check_scene_args(ctx, d_spheres, count)) return rc;
+    if (!ctx->gpu_tree || count != ctx->scene.n_spheres || ctx->ws.topo_n != count)
+        return rt_set_scene_device(ctx, d_spheres, count, stream);
+    DeviceGuard g(ctx->device);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    RT_HIP(hipStreamSynchronize(st));
+    return set_scene_gpu(ctx, d_spheres, count, st, true);
+}
+
 int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t* rows,
                      uint32_t band_width, uint32_t band_height, float* accum, uint8_t* out,
                      const rt_options* opt, void* stream) {
@@ -442,6 +580,8 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     // over 32-B nodes), 2 = ordered two-wide walk with an LDS stack, 4 = escape-link walk over
     // compact 16-B binary16 nodes (both slower on the canonical scene)
     const bool escape_walk = o.reserved[1] != 2u;
+    if (!escape_walk && ctx->gpu_tree && ctx->scene.n_nodes)
+        return fail(RT_ERR_INVALID_ARGUMENT, "the ordered walk needs the host-built tree (RT_BVH_BUILD=host)");
     const bool allow16 = o.reserved[1] == 4u;
     uint32_t accel;
     size_t lds = 0;
@@ -520,6 +660,11 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
         if (!(cam_r <= ctx->pad_radius) && (d.n_nodes || d.n_nodes2)) {
             if (!std::isfinite(cam_r)) return fail(RT_ERR_INVALID_ARGUMENT, "camera position is not finite");
             ctx->pad_radius = std::max(ctx->scene_radius, cam_r) * 1.01f + 100.0f;
+        }
+        if (ctx->gpu_tree && ctx->pad_radius != ctx->padded_for) {
+            RT_HIP(rt::repad_nodes_gpu(d.nodes_raw, d.nodes, d.n_nodes, pad_for(ctx->pad_radius), st));
+            ctx->padded_for = ctx->pad_radius;
+        } else if (!ctx->gpu_tree && ctx->pad_radius != ctx->padded_for) {
             std::vector<rt::BvhNode> n1;
             std::vector<rt::Bvh2Node> n2;
             pad_nodes(ctx->nodes_host, n1, ctx->nodes2_host, n2, pad_for(ctx->pad_radius));
@@ -531,6 +676,7 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
                 if (!make_nodes16(n1, n16)) return fail(RT_ERR_DEVICE, "compact LBVH re-pad failed");
                 RT_HIP(hipMemcpy(d.nodes16, n16.data(), n16.size() * sizeof(n16[0]), hipMemcpyHostToDevice));
             }
+            ctx->padded_for = ctx->pad_radius;
         }
     }
     RT_HIP(hipMemsetAsync(ctx->counters, 0, sizeof(rt::Counters), st));
@@ -595,6 +741,44 @@ int rt_debug_walk_hist(rt_context* ctx, uint64_t* out128) {
     rt::Counters c;
     RT_HIP(hipMemcpy(&c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
     std::memcpy(out128, c.walk_hist, sizeof(c.walk_hist));
+    return RT_OK;
+}
+
+int rt_debug_scene(rt_context* ctx, uint32_t what, void* out, uint64_t capacity, uint64_t* bytes) {
+    if (!ctx || !bytes) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    const rt::DeviceScene& d = ctx->scene;
+    DeviceGuard g(ctx->device);
+    RT_HIP(hipDeviceSynchronize());
+    if (what == 8) {
+        struct { uint32_t n_spheres, n_big, n_nodes, n_leaf, gpu, z; float rmax, R; } info{
+            d.n_spheres, d.n_big, d.n_nodes, d.n_leaf, ctx->gpu_tree ? 1u : 0u, 0u, d.small_rmax, ctx->scene_radius};
+        *bytes = sizeof(info);
+        if (!out || capacity < sizeof(info)) return fail(RT_ERR_INVALID_ARGUMENT, "capacity too small");
+        std::memcpy(out, &info, sizeof(info));
+        return RT_OK;
+    }
+    const void* src = nullptr;
+    size_t n = 0;
+    std::vector<rt::BvhNode> raw;
+    switch (what) {
+        case 0: src = d.geom; n = size_t(d.n_spheres) * sizeof(rt::GeomRec); break;
+        case 1: src = d.radius; n = size_t(d.n_spheres) * 4; break;
+        case 2: src = d.mat; n = size_t(d.n_spheres) * sizeof(rt::MatRec); break;
+        case 3: src = d.big_ids; n = size_t(d.n_big) * 4; break;
+        case 4: src = d.nodes; n = size_t(d.n_nodes) * sizeof(rt::BvhNode); break;
+        case 5: src = ctx->gpu_tree ? d.nodes_raw : nullptr; n = size_t(d.n_nodes) * sizeof(rt::BvhNode); break;
+        case 6: src = d.leaf_geom; n = size_t(d.n_leaf) * sizeof(rt::GeomRec); break;
+        case 7: src = d.leaf_ids; n = size_t(d.n_leaf) * 4; break;
+        default: return fail(RT_ERR_INVALID_ARGUMENT, "unknown scene array");
+    }
+    *bytes = n;
+    if (n == 0) return RT_OK;
+    if (!out || capacity < n) return fail(RT_ERR_INVALID_ARGUMENT, "capacity too small");
+    if (what == 5 && !ctx->gpu_tree) {   // host-built: the unpadded boxes live on the host
+        std::memcpy(out, ctx->nodes_host.data(), n);
+        return RT_OK;
+    }
+    RT_HIP(hipMemcpy(out, src, n, hipMemcpyDeviceToHost));
     return RT_OK;
 }
 

@@ -1,0 +1,65 @@
+// rt_build.h — device-side scene build and refit (rt_build.hip). Replaces the per-frame
+// BLAS/TLAS rebuild of the reference (src/vulkan.h:395-554, :1020-1059) and its AABB fill
+// (src/ray_trace.cpp:583-599) with a parallel LBVH build over the spheres in HBM.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rt_abi.h"
+#include "rt_internal.h"
+
+namespace rt {
+
+// Build results read back by the host (one small copy per build / refit).
+struct BuildSummary {
+    uint32_t n_big, n_small, n_nodes, n_leaf_slots;
+    uint32_t rmax_o, R_o;            // order-preserving bit patterns of small_rmax and R
+    uint32_t cmin_o[3], cmax_o[3];   // centroid bounds of the small spheres (Morton frame)
+};
+float summary_float(uint32_t ordered);
+
+// Destination arrays (DeviceScene), sized for n spheres:
+//   geom round_up(n, 8), radius n, mat n, big_ids 64, nodes / nodes_raw max(1, 2n),
+//   leaf_geom / leaf_ids 4n.
+struct BuildOutputs {
+    GeomRec* geom;
+    float* radius;
+    MatRec* mat;
+    uint32_t* big_ids;
+    BvhNode* nodes;       // padded for pad(R) (the traversal's copy)
+    BvhNode* nodes_raw;   // exact unions (re-padded for far cameras)
+    GeomRec* leaf_geom;
+    uint32_t* leaf_ids;
+};
+
+// Scratch that persists between a build and later refits (sorted order, radix-tree topology).
+struct BuildWorkspace {
+    uint32_t cap = 0;        // spheres the buffers hold
+    uint32_t topo_n = 0;     // sphere count of the topology a refit may reuse (0: none)
+    float* rkeys = nullptr;  float* rkeys_s = nullptr;
+    uint32_t* ids = nullptr; uint32_t* ids_s = nullptr;
+    uint32_t* keys = nullptr; uint32_t* keys_s = nullptr; uint32_t* sids = nullptr;
+    uint8_t* is_big = nullptr;
+    uint32_t* par_i = nullptr; uint32_t* par_l = nullptr;
+    uint32_t* left = nullptr;  uint32_t* right = nullptr;
+    uint32_t* lo = nullptr;    uint32_t* hi = nullptr;
+    uint32_t* flags = nullptr; uint32_t* cnt = nullptr; uint32_t* lcnt = nullptr;
+    float4* bnd = nullptr;   // 2 per inner node: lo.xyz, hi.xyz
+    void* tmp = nullptr;     size_t tmp_bytes = 0;
+    BuildSummary* S = nullptr;
+};
+
+hipError_t build_reserve(BuildWorkspace& ws, uint32_t n);
+void build_release(BuildWorkspace& ws);
+
+// Full build (refit = false) or refit of the previous topology (refit = true: same n, same big
+// set and leaf assignment; boxes, records, radii bounds and padding recomputed). Asynchronous on
+// `st` except for the final copy of the summary into *out (synchronous).
+hipError_t build_scene_gpu(BuildWorkspace& ws, const Sphere* d_spheres, uint32_t n,
+                           const BuildOutputs& o, bool refit, hipStream_t st, BuildSummary* out);
+
+// nodes[i] = nodes_raw[i] grown by `pad` on every side (far-camera re-pad).
+hipError_t repad_nodes_gpu(const BvhNode* raw, BvhNode* nodes, uint32_t n_nodes, float pad, hipStream_t st);
+
+}  // namespace rt

@@ -10,8 +10,9 @@
 //      inflate every ancestor box up to the root.
 //   2. small-sphere centers quantised to 10 bits per axis inside their bounds, 30-bit Morton
 //      codes, stable sort by (code, index).
-//   3. recursive split at the highest differing Morton bit (the radix-tree split; equal codes
-//      split in the middle), leaves of at most kLeafMax spheres, each stored in kLeafMax slots
+//   3. recursive split at the highest differing bit of (Morton code, sorted position) — the
+//      binary radix tree of Karras 2012, which rt_build.hip constructs in parallel — cut
+//      at subtrees of at most kLeafMax spheres, which become leaves stored in kLeafMax slots
 //      (dummy-padded) so the device issues a leaf's four loads together.
 //   4. node bounds = exact float min/max of the member spheres' AABBs (center -/+ radius), so
 //      every node box contains its spheres' AABBs bit-exactly (the traversal's exactness
@@ -67,15 +68,21 @@ struct Builder {
         }
     }
 
+    // Common-prefix length of the keys at sorted positions i and j, each key augmented by its
+    // position (Karras 2012, duplicate codes): the GPU builder (rt_build.hip) uses the same rule,
+    // so both emit the identical tree.
+    int delta(uint32_t i, uint32_t j) const {
+        const uint32_t a = prims[i].code, b = prims[j].code;
+        return a == b ? 32 + __builtin_clz(i ^ j) : __builtin_clz(a ^ b);
+    }
+
     uint32_t split(uint32_t lo, uint32_t hi) const {  // [lo, hi), hi - lo >= 2
-        const uint32_t a = prims[lo].code, b = prims[hi - 1].code;
-        if (a == b) return (lo + hi) / 2;
-        const int common = __builtin_clz(a ^ b);
+        const int common = delta(lo, hi - 1);
         uint32_t s = lo, step = hi - 1 - lo;
-        do {  // binary search for the last index sharing more than `common` prefix bits with a
+        do {  // binary search for the last index sharing more than `common` prefix bits with lo
             step = (step + 1) >> 1;
             const uint32_t ns = s + step;
-            if (ns < hi - 1 && __builtin_clz(a ^ prims[ns].code) > common) s = ns;
+            if (ns < hi - 1 && delta(lo, ns) > common) s = ns;
         } while (step > 1);
         return s + 1;
     }

@@ -65,6 +65,7 @@ struct DeviceScene {
     uint32_t* big_ids = nullptr;   // n_big sphere indices, ascending
     uint32_t n_nodes = 0;
     BvhNode* nodes = nullptr;      // 2 * n_leaf_spheres - 1 at most
+    BvhNode* nodes_raw = nullptr;  // device-built trees: unpadded boxes (far-camera re-pad)
     GeomRec* leaf_geom = nullptr;  // spheres permuted into leaf order (contiguous per leaf)
     uint32_t* leaf_ids = nullptr;  // original index of each leaf slot
     uint32_t n_leaf = 0;

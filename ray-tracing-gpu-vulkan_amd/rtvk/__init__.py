@@ -122,6 +122,49 @@ class Renderer:
         check(self._lib.rt_set_scene(self._ctx, ptr if n else None, n, st))
         self.sphere_count = n
 
+    def refit_scene(self, spheres, stream=None) -> None:
+        """Per-frame update (same count): refit the device-built tree to moved spheres."""
+        buf = spheres if not isinstance(spheres, np.ndarray) else np.ascontiguousarray(spheres, np.uint8)
+        n = len(spheres)
+        ptr = ctypes.addressof(buf) if not isinstance(buf, np.ndarray) else buf.ctypes.data
+        st = 0 if stream is None else _stream_ptr(stream)
+        check(self._lib.rt_refit_scene(self._ctx, ptr if n else None, n, st))
+        self.sphere_count = n
+
+    def set_scene_device(self, spheres_dev, refit: bool = False, stream=None) -> None:
+        """Spheres already on the device: a contiguous uint8 cuda tensor [n, 80]."""
+        import torch
+        if not spheres_dev.is_cuda or spheres_dev.dtype != torch.uint8 or spheres_dev.dim() != 2 \
+                or spheres_dev.shape[1] != 80 or not spheres_dev.is_contiguous():
+            raise ValueError("spheres_dev must be a contiguous uint8 cuda tensor [n, 80]")
+        n = int(spheres_dev.shape[0])
+        st = _stream_ptr(stream if stream is not None else torch.cuda.current_stream())
+        fn = self._lib.rt_refit_scene_device if refit else self._lib.rt_set_scene_device
+        check(fn(self._ctx, spheres_dev.data_ptr() if n else None, n, st))
+        self.sphere_count = n
+
+    _SCENE_DTYPES = {0: (np.float32, 4), 1: (np.float32, 1), 2: (np.uint8, 32), 3: (np.uint32, 1),
+                     4: (np.uint8, 32), 5: (np.uint8, 32), 6: (np.float32, 4), 7: (np.uint32, 1)}
+
+    def scene_array(self, what: int) -> np.ndarray:
+        """Diagnostic copy of one device scene array (rt_debug_scene); what 8 returns a dict."""
+        nbytes = ctypes.c_uint64(0)
+        if what == 8:
+            raw = (ctypes.c_uint8 * 32)()
+            check(self._lib.rt_debug_scene(self._ctx, 8, raw, 32, ctypes.byref(nbytes)))
+            u = np.frombuffer(bytes(raw), np.uint32)
+            f = np.frombuffer(bytes(raw), np.float32)
+            return {"n_spheres": int(u[0]), "n_big": int(u[1]), "n_nodes": int(u[2]),
+                    "n_leaf": int(u[3]), "device_built": bool(u[4]), "small_rmax": float(f[6]),
+                    "scene_radius": float(f[7])}
+        self._lib.rt_debug_scene(self._ctx, what, None, 0, ctypes.byref(nbytes))   # size query
+        buf = np.zeros(max(1, nbytes.value), np.uint8)
+        if nbytes.value:
+            check(self._lib.rt_debug_scene(self._ctx, what, buf.ctypes.data, nbytes.value, ctypes.byref(nbytes)))
+        dt, w = self._SCENE_DTYPES[what]
+        a = buf[: nbytes.value].view(dt)
+        return a.reshape(-1, w) if w > 1 else a
+
     def render_device(self, rci: RenderCallInfo, accum, out, rows=None,
                       options: Optional[Options] = None, stream=None) -> None:
         """One band on this device, asynchronous on `stream` (torch current stream by default).

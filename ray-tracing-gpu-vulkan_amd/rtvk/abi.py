@@ -102,6 +102,9 @@ EXPORTS = {
     "rt_context_create": (_I, [_I, ctypes.POINTER(_P)]),
     "rt_context_destroy": (_I, [_P]),
     "rt_set_scene": (_I, [_P, _P, _U32, _P]),
+    "rt_set_scene_device": (_I, [_P, _P, _U32, _P]),
+    "rt_refit_scene": (_I, [_P, _P, _U32, _P]),
+    "rt_refit_scene_device": (_I, [_P, _P, _U32, _P]),
     "rt_render_device": (_I, [_P, ctypes.POINTER(RenderCallInfo), _P, _U32, _U32, _P, _P,
                               ctypes.POINTER(Options), _P]),
     "rt_get_stats": (_I, [_P, ctypes.POINTER(Stats)]),
@@ -111,6 +114,7 @@ EXPORTS = {
     "rt_debug_math": (_I, [_I, _I, _P, _P, _U32]),
     "rt_debug_stamps": (_I, [_P, _P]),
     "rt_debug_walk_hist": (_I, [_P, _P]),
+    "rt_debug_scene": (_I, [_P, _U32, _P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     "ray_trace": (None, [_U32, ctypes.c_bool, _U32, _U32, _U32]),
 }
 

@@ -6,8 +6,10 @@ every rgba8 byte must be identical, and the traced-segment counts must agree. Fu
 use size-independent properties (LBVH == brute force, band-split invariance) plus one full-frame
 oracle comparison at 1 spp.
 """
+import contextlib
 import ctypes
 import json
+import os
 from pathlib import Path
 
 import numpy as np
@@ -19,6 +21,21 @@ BRUTE, LBVH = 1, 2
 LBVH_ORDERED = 3   # test-only alias: accel LBVH with the ordered two-wide walk (options.reserved[1] = 2)
 LBVH_COMPACT = 4   # test-only alias: accel LBVH, escape-link walk over 16-B nodes (options.reserved[1] = 4)
 WALK_FORM = {LBVH_ORDERED: 2, LBVH_COMPACT: 4}
+
+
+@contextlib.contextmanager
+def tree_builder(kind):
+    """RT_BVH_BUILD for the scenes set inside (the walk A/B forms need the host-built tree)."""
+    prev = os.environ.get("RT_BVH_BUILD")
+    if kind:
+        os.environ["RT_BVH_BUILD"] = kind
+    try:
+        yield
+    finally:
+        if prev is None:
+            os.environ.pop("RT_BVH_BUILD", None)
+        else:
+            os.environ["RT_BVH_BUILD"] = prev
 
 
 @pytest.fixture(scope="module")
@@ -45,7 +62,8 @@ def renderer(rtvk):
 def gpu_render(rtvk, renderer, torch, spheres, rci_u32, band_w, band_h, rows=None, accel=LBVH,
                max_depth=50, seed_mode=0, rng_mode=0, accumulate=False, sample_base=0, accum=None,
                count=False):
-    renderer.set_scene(np.ascontiguousarray(spheres, np.uint8).reshape(-1, 80))
+    with tree_builder("host" if accel in WALK_FORM else None):
+        renderer.set_scene(np.ascontiguousarray(spheres, np.uint8).reshape(-1, 80))
     rci = rtvk.RenderCallInfo.from_buffer_copy(np.ascontiguousarray(rci_u32).tobytes())
     acc = (torch.zeros((band_h, band_w, 4), dtype=torch.float32, device="cuda") if accum is None
            else torch.from_numpy(np.ascontiguousarray(accum, np.float32)).cuda())
