@@ -147,13 +147,25 @@ def main() -> int:
             dist.barrier()
         torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
+    build_s = []
+
+    def frame():
+        # The reference rebuilds its acceleration structure every frame (src/vulkan.h:1020-1059)
+        # and SURVEY.md 8(d) counts the build in the wall clock: rebuild, then render + gather.
+        torch.cuda.synchronize()   # rt_set_scene waits for the previous frame anyway; time the build alone
+        tb = time.perf_counter()
+        renderer.set_scene(scene)
+        build_s.append(time.perf_counter() - tb)
         dr.step()
+
+    for _ in range(args.warmup):
+        frame()
     barrier()
     ev.clear()
+    build_s.clear()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        dr.step()
+        frame()
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -223,6 +235,8 @@ def main() -> int:
                        "accel": args.accel, "parallelism": f"row-strips x{world} + rccl gather"},
             "segments_per_sample": round(st.segments / max(1, st.samples), 4),
             "scene_setup_ms": round(t_scene * 1e3, 2),
+            "scene_build_ms_per_step": round(sum(build_s) / max(1, len(build_s)) * 1e3, 3),
+            "tree": "device-lbvh" if renderer.scene_array(8)["device_built"] else "host-sah",
             "msegments_per_s": round(st.segments / max(1, st.samples) * value, 2),
             "roofline": roof,
             "context": {"reference_rx6800xt_vulkan_rt_msamples": 1658.9,

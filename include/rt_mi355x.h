@@ -114,9 +114,10 @@ int rt_canonical_render_call_info(uint32_t spp, uint32_t width, uint32_t height,
 /* ---- device API ------------------------------------------------------------------- */
 int rt_context_create(int device, rt_context** out);
 int rt_context_destroy(rt_context* ctx);
-/* Uploads `count` spheres (host memory) and builds the acceleration structures on the device
- * (parallel LBVH build, rt_build.hip; RT_BVH_BUILD=host selects the host builder for A/B).
- * Returns after the build (one small device-to-host copy of the tree's counts). */
+/* Uploads `count` spheres (host memory) and builds the closest-hit structure: a binned-SAH tree
+ * built on the host for scenes of up to 4096 spheres (the cheaper walk), the parallel device
+ * LBVH build (rt_build.hip) above that. RT_BVH_BUILD=gpu|sah|morton forces one builder (A/B).
+ * Returns after the build. */
 int rt_set_scene(rt_context* ctx, const Sphere* spheres, uint32_t count, void* stream);
 /* As rt_set_scene, spheres already in DEVICE memory (read during the call only). */
 int rt_set_scene_device(rt_context* ctx, const Sphere* d_spheres, uint32_t count, void* stream);

@@ -362,7 +362,7 @@ namespace {
 
 // Host-built tree (rt_bvh.cpp): the A/B reference for the device builder and the only source of
 // the alternative walk layouts (ordered two-wide, compact binary16 nodes).
-int set_scene_host(rt_context* ctx, const Sphere* spheres, uint32_t count, hipStream_t st) {
+int set_scene_host(rt_context* ctx, const Sphere* spheres, uint32_t count, hipStream_t st, bool sah) {
     try {
         free_scene(ctx);
         ctx->gpu_tree = false;
@@ -385,7 +385,7 @@ int set_scene_host(rt_context* ctx, const Sphere* spheres, uint32_t count, hipSt
         // radius^2 = -1e38, so D = b^2 - a(|oc|^2 + 1e38) < 0 for every ray.
         while (geom.size() % 8) geom.push_back(rt::GeomRec{0.0f, 1e19f, 0.0f, -1e38f});
         rt::HostBvh bvh;
-        rt::build_lbvh_host(spheres, count, bvh);
+        rt::build_lbvh_host(spheres, count, bvh, sah);
         rt::DeviceScene& d = ctx->scene;
         d.n_spheres = count;
         if (int rc = upload(ctx, geom, &d.geom, st)) return rc;
@@ -492,10 +492,16 @@ int set_scene_gpu(rt_context* ctx, const Sphere* d_sph, uint32_t count, hipStrea
     return RT_OK;
 }
 
-bool host_build_requested() {
-    const char* b = std::getenv("RT_BVH_BUILD");   // "host" | "gpu" (default)
-    const char* f = std::getenv("RT_BVH_BUILDER");  // host builder form (A/B): implies host
-    return (b && std::strcmp(b, "host") == 0) || f;
+// Tree builder (RT_BVH_BUILD): "auto" (default) = host SAH up to kHostSahMaxSpheres (best walk
+// cost, build <= ~2 ms) else the device LBVH; "gpu", "sah", "morton" force one (A/B, tests).
+constexpr uint32_t kHostSahMaxSpheres = 4096;
+enum class Builder { GPU, HOST_SAH, HOST_MORTON };
+Builder pick_builder(uint32_t count) {
+    const char* b = std::getenv("RT_BVH_BUILD");
+    if (b && std::strcmp(b, "gpu") == 0) return Builder::GPU;
+    if (b && std::strcmp(b, "sah") == 0) return Builder::HOST_SAH;
+    if (b && std::strcmp(b, "morton") == 0) return Builder::HOST_MORTON;
+    return count <= kHostSahMaxSpheres ? Builder::HOST_SAH : Builder::GPU;
 }
 
 int stage_spheres(rt_context* ctx, const Sphere* spheres, uint32_t count, hipStream_t st) {
@@ -528,7 +534,8 @@ int rt_set_scene(rt_context* ctx, const Sphere* spheres, uint32_t count, void* s
     DeviceGuard g(ctx->device);
     hipStream_t st = static_cast<hipStream_t>(stream);
     RT_HIP(hipStreamSynchronize(st));  // previous launches may still read the old scene
-    if (host_build_requested()) return set_scene_host(ctx, spheres, count, st);
+    const Builder b = pick_builder(count);
+    if (b != Builder::GPU) return set_scene_host(ctx, spheres, count, st, b == Builder::HOST_SAH);
     if (int rc = stage_spheres(ctx, spheres, count, st)) return rc;
     return set_scene_gpu(ctx, ctx->d_spheres, count, st, false);
 }
@@ -581,7 +588,7 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     // compact 16-B binary16 nodes (both slower on the canonical scene)
     const bool escape_walk = o.reserved[1] != 2u;
     if (!escape_walk && ctx->gpu_tree && ctx->scene.n_nodes)
-        return fail(RT_ERR_INVALID_ARGUMENT, "the ordered walk needs the host-built tree (RT_BVH_BUILD=host)");
+        return fail(RT_ERR_INVALID_ARGUMENT, "the ordered walk needs a host-built tree (RT_BVH_BUILD=sah or morton)");
     const bool allow16 = o.reserved[1] == 4u;
     uint32_t accel;
     size_t lds = 0;

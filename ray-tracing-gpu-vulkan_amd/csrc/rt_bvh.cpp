@@ -32,7 +32,6 @@ namespace {
 
 constexpr uint32_t kLeafMax = 4;
 constexpr uint32_t kBigMax = 64;
-constexpr bool kDefaultSah = false;
 
 inline uint32_t expand_bits(uint32_t v) {  // 10 bits -> every third bit of 30
     v = (v * 0x00010001u) & 0xFF0000FFu;
@@ -47,13 +46,19 @@ struct Prim {
     uint32_t id;
 };
 
-// Leaves hold 1..kLeafMax spheres chosen by the radix split (spatially tight), stored in
-// kLeafMax slots padded with never-hit dummies so the device loads a leaf as 4 records at once.
+// Host SAH builder knobs (A/B experiments; defaults are the measured best).
+struct SahKnobs {
+    bool classic = false;   // cost = area x spheres (else area x leaves needed)
+    bool sweep = false;     // exact sweep over sorted centroids for ranges <= 4096 (else 32 bins)
+    int order = 0;          // child order: 0 split order, 1 larger-area child first, 2 smaller first
+};
+
 struct Builder {
     const Sphere* sph;
     std::vector<Prim>& prims;
     HostBvh& out;
     bool sah;
+    SahKnobs knobs;
 
     void bounds(uint32_t lo, uint32_t hi, float* bmin, float* bmax) const {
         bmin[0] = bmin[1] = bmin[2] = INFINITY;
@@ -87,11 +92,59 @@ struct Builder {
         return s + 1;
     }
 
+    // Exact sweep variant of split_sah (A/B knob "sweep"): every split position along each axis
+    // of the centroid-sorted range.
+    uint32_t split_sweep(uint32_t lo, uint32_t hi) {
+        auto area = [](const float* l, const float* h) {
+            const double ex = double(h[0]) - l[0], ey = double(h[1]) - l[1], ez = double(h[2]) - l[2];
+            return ex * ey + ey * ez + ez * ex;
+        };
+        const uint32_t n = hi - lo;
+        double best_cost = INFINITY;
+        int best_axis = -1;
+        uint32_t best_s = 0;
+        std::vector<Prim> tmp(prims.begin() + lo, prims.begin() + hi);
+        std::vector<double> right(n);
+        for (int k = 0; k < 3; k++) {
+            auto key = [&](const Prim& p) {
+                const rt_vec4& g = sph[p.id].geometry;
+                return k == 0 ? g.x : k == 1 ? g.y : g.z;
+            };
+            std::stable_sort(tmp.begin(), tmp.end(), [&](const Prim& a, const Prim& b) { return key(a) < key(b); });
+            float rl[3] = {INFINITY, INFINITY, INFINITY}, rh[3] = {-INFINITY, -INFINITY, -INFINITY};
+            for (uint32_t i = n; i-- > 1;) {
+                const rt_vec4& g = sph[tmp[i].id].geometry;
+                const float c[3] = {g.x, g.y, g.z};
+                for (int j = 0; j < 3; j++) { rl[j] = std::min(rl[j], c[j] - g.w); rh[j] = std::max(rh[j], c[j] + g.w); }
+                right[i] = area(rl, rh);
+            }
+            float ll[3] = {INFINITY, INFINITY, INFINITY}, lh[3] = {-INFINITY, -INFINITY, -INFINITY};
+            for (uint32_t i = 0; i + 1 < n; i++) {   // left = [0, i], right = [i + 1, n)
+                const rt_vec4& g = sph[tmp[i].id].geometry;
+                const float c[3] = {g.x, g.y, g.z};
+                for (int j = 0; j < 3; j++) { ll[j] = std::min(ll[j], c[j] - g.w); lh[j] = std::max(lh[j], c[j] + g.w); }
+                const uint32_t nl = i + 1, nr = n - nl;
+                const double cost = knobs.classic ? area(ll, lh) * nl + right[i + 1] * nr
+                                                  : area(ll, lh) * ((nl + kLeafMax - 1) / kLeafMax) +
+                                                        right[i + 1] * ((nr + kLeafMax - 1) / kLeafMax);
+                if (cost < best_cost) { best_cost = cost; best_axis = k; best_s = nl; }
+            }
+        }
+        if (best_axis < 0) return (lo + hi) / 2;
+        auto key = [&](const Prim& p) {
+            const rt_vec4& g = sph[p.id].geometry;
+            return best_axis == 0 ? g.x : best_axis == 1 ? g.y : g.z;
+        };
+        std::stable_sort(prims.begin() + lo, prims.begin() + hi, [&](const Prim& a, const Prim& b) { return key(a) < key(b); });
+        return lo + best_s;
+    }
+
     // Binned surface-area split of [lo, hi) (hi - lo > kLeafMax): 32 centroid bins per axis, cost
     // = sum over both sides of area x leaves needed (a leaf costs the same for 1..4 spheres, the
     // device always tests four slots). Reorders prims[lo, hi) and returns the split index;
-    // degenerate centroid bounds fall back to a median split on the widest axis.
+    // coincident centroids fall back to a split by count.
     uint32_t split_sah(uint32_t lo, uint32_t hi) {
+        if (knobs.sweep && hi - lo <= 4096) return split_sweep(lo, hi);
         constexpr int kBins = 32;
         float cmin[3] = {INFINITY, INFINITY, INFINITY}, cmax[3] = {-INFINITY, -INFINITY, -INFINITY};
         for (uint32_t i = lo; i < hi; i++) {
@@ -143,8 +196,10 @@ struct Builder {
                 for (int j = 0; j < 3; j++) { ll[j] = std::min(ll[j], bl[b][j]); lh[j] = std::max(lh[j], bh[b][j]); }
                 const uint32_t rcnt = right_cnt[b + 1];
                 if (lc == 0 || rcnt == 0) continue;
-                const double cost = area(ll, lh) * ((lc + kLeafMax - 1) / kLeafMax) +
-                                    right_area[b + 1] * ((rcnt + kLeafMax - 1) / kLeafMax);
+                const double cost = knobs.classic
+                                         ? area(ll, lh) * lc + right_area[b + 1] * rcnt
+                                         : area(ll, lh) * ((lc + kLeafMax - 1) / kLeafMax) +
+                                               right_area[b + 1] * ((rcnt + kLeafMax - 1) / kLeafMax);
                 if (cost < best_cost) { best_cost = cost; best_axis = k; best_plane = b; }
             }
         }
@@ -187,7 +242,21 @@ struct Builder {
             ref = kLeafFlag | (first << 3) | (hi - lo);
             *height = 0;
         } else {
-            const uint32_t s = sah ? split_sah(lo, hi) : split(lo, hi);
+            uint32_t s = sah ? split_sah(lo, hi) : split(lo, hi);
+            if (knobs.order) {   // put the larger (order 1) / smaller (order 2) child first
+                float la[3], ha[3], lb[3], hb[3];
+                bounds(lo, s, la, ha);
+                bounds(s, hi, lb, hb);
+                auto area = [](const float* l, const float* h) {
+                    const double ex = double(h[0]) - l[0], ey = double(h[1]) - l[1], ez = double(h[2]) - l[2];
+                    return ex * ey + ey * ez + ez * ex;
+                };
+                const double a0 = area(la, ha), a1 = area(lb, hb);
+                if ((knobs.order == 1 && a1 > a0) || (knobs.order == 2 && a1 < a0)) {
+                    std::rotate(prims.begin() + lo, prims.begin() + s, prims.begin() + hi);
+                    s = lo + (hi - s);
+                }
+            }
             const uint32_t me2 = uint32_t(out.nodes2.size());
             out.nodes2.push_back(Bvh2Node{});
             float l0[3], h0[3], l1[3], h1[3];
@@ -212,7 +281,7 @@ struct Builder {
 
 }  // namespace
 
-void build_lbvh_host(const Sphere* sph, uint32_t n, HostBvh& out) {
+void build_lbvh_host(const Sphere* sph, uint32_t n, HostBvh& out, bool sah) {
     out = HostBvh{};
     if (n == 0) return;
     if (n >= (1u << 27)) return;   // leaf references hold 28-bit slot indices
@@ -259,9 +328,13 @@ void build_lbvh_host(const Sphere* sph, uint32_t n, HostBvh& out) {
     std::stable_sort(prims.begin(), prims.end(), [](const Prim& a, const Prim& b) { return a.code < b.code; });
     // 3-4. hierarchy in depth-first order
     out.nodes.reserve(2 * prims.size());
-    const char* env = std::getenv("RT_BVH_BUILDER");   // A/B switch: "morton" or "sah"
-    const bool sah = env ? std::strcmp(env, "morton") != 0 : kDefaultSah;
-    Builder b{sph, prims, out, sah};
+    SahKnobs knobs;
+    if (const char* k = std::getenv("RT_SAH_KNOBS")) {   // e.g. "classic,sweep,order1"
+        knobs.classic = std::strstr(k, "classic") != nullptr;
+        knobs.sweep = std::strstr(k, "sweep") != nullptr;
+        knobs.order = std::strstr(k, "order1") ? 1 : std::strstr(k, "order2") ? 2 : 0;
+    }
+    Builder b{sph, prims, out, sah, knobs};
     float bmin[3], bmax[3];
     out.root2 = b.build(0, uint32_t(prims.size()), bmin, bmax, &out.depth2);
     for (BvhNode& nd : out.nodes)

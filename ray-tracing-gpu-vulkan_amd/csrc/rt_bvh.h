@@ -20,6 +20,8 @@ struct HostBvh {
     uint32_t depth2 = 0;              // max inner nodes on a root-to-leaf path
 };
 
-void build_lbvh_host(const Sphere* spheres, uint32_t n, HostBvh& out);
+// sah: binned surface-area splits (the default tree for small scenes); else the Morton radix
+// split that rt_build.hip reproduces on the device.
+void build_lbvh_host(const Sphere* spheres, uint32_t n, HostBvh& out, bool sah);
 
 }  // namespace rt

@@ -1,4 +1,6 @@
-"""A/B of the host tree builders (RT_BVH_BUILDER=morton|sah) on the canonical 1080p frame.
+"""A/B of the tree builders (RT_BVH_BUILD=gpu|morton|sah, RT_SAH_KNOBS) on a 1080p frame.
+
+Usage: python scripts/bvh_ab.py [grid_half_extent [spp [builder:knobs/builder:knobs...]]]
 
 Prints per builder: box / sphere tests per segment and walk SIMD utilisation (instrumented
 build, 8 spp), then the kernel time of the 100-spp frame (HIP events, median of 5).
@@ -19,8 +21,13 @@ spp = int(sys.argv[2]) if len(sys.argv) > 2 else 100
 r = rtvk.Renderer(0)
 sc = rtvk.generateRandomScene(grid_half_extent=grid) if grid != 11 else rtvk.generateRandomScene()
 images = {}
-for builder in ("morton", "sah"):
-    os.environ["RT_BVH_BUILDER"] = builder
+combos = [("gpu", ""), ("morton", ""), ("sah", ""), ("sah", "classic"), ("sah", "sweep"),
+          ("sah", "order1"), ("sah", "order2")]
+if len(sys.argv) > 3:
+    combos = [tuple((c + ":").split(":")[:2]) for c in sys.argv[3].split("/")]
+for builder, knobs in combos:
+    os.environ["RT_BVH_BUILD"] = builder
+    os.environ["RT_SAH_KNOBS"] = knobs
     r.set_scene(sc)
     torch.cuda.synchronize()
     rci8 = rtvk.canonical_render_call_info(8, W, H)
@@ -44,9 +51,10 @@ for builder in ("morton", "sah"):
         if i:
             ts.append(e0.elapsed_time(e1))
     ts.sort()
-    images[builder] = out.cpu()
-    print(f"{builder:7s} grid {grid}: box/seg {st.box_tests / st.segments:.2f} "
+    images[(builder, knobs)] = out.cpu()
+    print(f"{builder:7s} {knobs:14s} grid {grid}: box/seg {st.box_tests / st.segments:.2f} "
           f"sph/seg {st.sphere_tests / st.segments:.2f} walk util {util:.3f} "
           f"frame {ts[len(ts) // 2]:.2f} ms ({spp} spp)", flush=True)
-assert torch.equal(images["morton"], images["sah"]), "builders disagree"
+first = next(iter(images.values()))
+assert all(torch.equal(first, v) for v in images.values()), "builders disagree"
 print("images identical")

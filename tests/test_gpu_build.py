@@ -43,7 +43,7 @@ def scene_arrays(renderer):
 
 
 def build_both(renderer, spheres):
-    with tree_builder("host"):
+    with tree_builder("morton"):   # the host form the device builder reproduces
         renderer.set_scene(spheres)
         host = scene_arrays(renderer)
         host[5] = renderer.scene_array(5)
@@ -120,6 +120,15 @@ def test_device_tree_edge_cases(renderer, oracle, case):
         r = np.full(129, 0.05, np.float32)
     host, dev = build_both(renderer, records(oracle, c, r))
     assert_trees_equal(host, dev)
+
+
+@pytest.mark.parametrize("K,device_built", [(11, False), (31, False), (32, True), (158, True)])
+def test_auto_builder_policy(renderer, oracle, K, device_built):
+    """Default: host SAH tree up to 4096 spheres (K = 31 -> 3848), device LBVH above."""
+    with tree_builder(None):
+        os.environ.pop("RT_BVH_BUILD", None)
+        renderer.set_scene(oracle.generate_scene(0.0, K))
+    assert renderer.scene_array(8)["device_built"] == device_built
 
 
 def test_empty_scene_device_build(renderer):

@@ -25,7 +25,8 @@ WALK_FORM = {LBVH_ORDERED: 2, LBVH_COMPACT: 4}
 
 @contextlib.contextmanager
 def tree_builder(kind):
-    """RT_BVH_BUILD for the scenes set inside (the walk A/B forms need the host-built tree)."""
+    """RT_BVH_BUILD (gpu | sah | morton) for the scenes set inside; the walk A/B forms need a
+    host-built tree."""
     prev = os.environ.get("RT_BVH_BUILD")
     if kind:
         os.environ["RT_BVH_BUILD"] = kind
@@ -61,8 +62,8 @@ def renderer(rtvk):
 
 def gpu_render(rtvk, renderer, torch, spheres, rci_u32, band_w, band_h, rows=None, accel=LBVH,
                max_depth=50, seed_mode=0, rng_mode=0, accumulate=False, sample_base=0, accum=None,
-               count=False):
-    with tree_builder("host" if accel in WALK_FORM else None):
+               count=False, builder=None):
+    with tree_builder(builder or ("sah" if accel in WALK_FORM else None)):
         renderer.set_scene(np.ascontiguousarray(spheres, np.uint8).reshape(-1, 80))
     rci = rtvk.RenderCallInfo.from_buffer_copy(np.ascontiguousarray(rci_u32).tobytes())
     acc = (torch.zeros((band_h, band_w, 4), dtype=torch.float32, device="cuda") if accum is None
@@ -227,9 +228,10 @@ def test_lbvh_equals_brute_full_size(rtvk, renderer, torch, oracle, W, H, spp, K
     sc = oracle.generate_scene(0.0, K)
     rci = oracle.render_call_info(spp, W, H)
     ab, ob, sb = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=BRUTE)
-    al, ol, sl = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH)
-    assert_same(al, ol, ab, ob)
-    assert sb.segments == sl.segments
+    for builder in ("gpu", "sah", "morton"):
+        al, ol, sl = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH, builder=builder)
+        assert_same(al, ol, ab, ob)
+        assert sb.segments == sl.segments
     for form in (LBVH_ORDERED, LBVH_COMPACT):
         ao, oo, so = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=form)
         assert_same(ao, oo, ab, ob)
@@ -268,6 +270,8 @@ def test_far_and_grazing_cameras(rtvk, renderer, torch, oracle, cam):
     for accel in (BRUTE, LBVH, LBVH_ORDERED, LBVH_COMPACT):
         a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=accel)
         assert_same(a, o, ra, ro)
+    a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH, builder="gpu")
+    assert_same(a, o, ra, ro)
 
 
 def test_scatter_rows_reassembles_strips(rtvk, renderer, torch, oracle):
