@@ -172,6 +172,14 @@ int rt_debug_stamps(rt_context* ctx, uint64_t* out8);
 /* Diagnostic: histogram of LBVH box tests per segment of the last instrumented launch
  * (options.reserved[0] & 1), 2 x 64 bins: [0] segments that miss, [1] segments that hit. */
 int rt_debug_walk_hist(rt_context* ctx, uint64_t* out128);
+/* Diagnostic: segment-loop iterations of the last instrumented launch by the number of lanes
+ * (0..64) of the wave tracing in that iteration (the persistent kernel's lane occupancy), then
+ * three s_memrealtime stamps (100 MHz): first wave start, pixel queue dry, last wave exit. */
+int rt_debug_lane_hist(rt_context* ctx, uint64_t* out68);
+/* Diagnostic: traced segments per 8x8 tile of ctx's last LBVH launch (the costs its next launch
+ * over the same band geometry hands tiles out by); *count = tiles (ceil(W/8) x ceil(H/8),
+ * row-major), 0 before the first launch. */
+int rt_debug_tile_cost(rt_context* ctx, uint32_t* out, uint64_t capacity, uint64_t* count);
 
 /* Diagnostic (tests): copies one scene array of ctx to host memory. what: 0 geometry records,
  * 1 radii, 2 material records, 3 big-sphere ids, 4 LBVH nodes (padded), 5 LBVH nodes (unpadded),

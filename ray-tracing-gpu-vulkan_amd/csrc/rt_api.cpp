@@ -59,6 +59,7 @@ struct rt_context {
     // host-provided spheres
     float padded_for = 0.0f;   // pad radius the device node copy currently carries
     bool gpu_tree = false;
+    rt::TileSchedule sched;           // pixel hand-out order (LPT from the last launch's costs)
     rt::BuildWorkspace ws;
     Sphere* d_spheres = nullptr;
     uint32_t d_spheres_cap = 0;
@@ -350,6 +351,7 @@ int rt_context_destroy(rt_context* ctx) {
     (void)hipDeviceSynchronize();
     free_scene(ctx);
     rt::build_release(ctx->ws);
+    rt::schedule_release(ctx->sched);
     if (ctx->d_spheres) (void)hipFree(ctx->d_spheres);
     if (ctx->counters) (void)hipFree(ctx->counters);
     delete ctx;
@@ -615,7 +617,6 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     if (o.seed_mode > RT_SEED_LAUNCH_LOCAL) return fail(RT_ERR_INVALID_ARGUMENT, "unknown seed_mode");
     if (o.rng_mode > RT_RNG_SAMPLE_COUNTER) return fail(RT_ERR_INVALID_ARGUMENT, "unknown rng_mode");
     const bool count = (o.reserved[0] & 1u) != 0;  // internal: count box / sphere tests
-
     rt::TraceParams P;
     std::memset(&P, 0, sizeof(P));
     fill_camera(*rci, P);
@@ -686,7 +687,24 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
             ctx->padded_for = ctx->pad_radius;
         }
     }
+    // Longest-processing-time-first hand-out from the last launch of this band geometry
+    // (RT_SCHEDULE=rowmajor disables it, A/B only); this launch records the next costs.
+    if (accel == rt::ACCEL_LBVH || accel == rt::ACCEL_LBVH_LDS || accel == rt::ACCEL_LBVH16_LDS ||
+        accel == rt::ACCEL_LBVH_LDS_SCENE) {   // the escape-walk kernels record tile costs
+        rt::TileSchedule& sc = ctx->sched;
+        RT_HIP(rt::schedule_reserve(sc, uint32_t(tiles_x * tiles_y), st));
+        const char* e = std::getenv("RT_SCHEDULE");
+        const bool lpt = !(e && std::strcmp(e, "rowmajor") == 0);
+        if (lpt && sc.valid) {
+            RT_HIP(rt::schedule_order(sc, st));
+            P.tile_order = sc.order;
+        }
+        RT_HIP(hipMemsetAsync(sc.cost[sc.cur], 0, size_t(sc.n) * 4, st));
+        P.tile_cost = sc.cost[sc.cur];
+    }
     RT_HIP(hipMemsetAsync(ctx->counters, 0, sizeof(rt::Counters), st));
+    // first-time stamps start at the maximum (atomicMin); 0xff bytes = ~0ull
+    RT_HIP(hipMemsetAsync(&ctx->counters->t_first, 0xff, 2 * sizeof(unsigned long long), st));
     const int ci = count ? 1 : 0;
     if (ctx->occ_lds[accel][ci] != lds) {
         int b = 0;
@@ -700,6 +718,10 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     const int grid = int(std::max<uint64_t>(1, std::min(full, by_work)));
     RT_HIP(rt::launch_trace(P, accel, count, grid, lds, st));
     ctx->last_stream = st;
+    if (P.tile_cost) {
+        ctx->sched.cur ^= 1;
+        ctx->sched.valid = true;
+    }
     return RT_OK;
 }
 
@@ -737,6 +759,31 @@ int rt_debug_stamps(rt_context* ctx, uint64_t* out8) {
     RT_HIP(hipMemcpy(&c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
     for (int k = 0; k < 8; k++) out8[k] = c.stamp[k];
     if (!c.stamp[0] && !c.stamp[1]) out8[6] = c.wave_iters;   // non-stamp builds: walk iterations
+    return RT_OK;
+}
+
+int rt_debug_tile_cost(rt_context* ctx, uint32_t* out, uint64_t capacity, uint64_t* count) {
+    if (!ctx || !count) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    const rt::TileSchedule& sc = ctx->sched;
+    *count = sc.valid ? sc.n : 0;
+    if (!sc.valid || !out) return RT_OK;   // size query
+    if (capacity < sc.n) return fail(RT_ERR_INVALID_ARGUMENT, "capacity");
+    DeviceGuard g(ctx->device);
+    RT_HIP(hipStreamSynchronize(ctx->last_stream));
+    RT_HIP(hipMemcpy(out, sc.cost[sc.cur ^ 1], size_t(sc.n) * 4, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+int rt_debug_lane_hist(rt_context* ctx, uint64_t* out68) {
+    if (!ctx || !out68) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    DeviceGuard g(ctx->device);
+    RT_HIP(hipStreamSynchronize(ctx->last_stream));
+    rt::Counters c;
+    RT_HIP(hipMemcpy(&c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
+    std::memcpy(out68, c.lane_hist, sizeof(c.lane_hist));
+    out68[65] = c.t_first;
+    out68[66] = c.t_dry;
+    out68[67] = c.t_last;
     return RT_OK;
 }
 

@@ -59,6 +59,28 @@ void build_release(BuildWorkspace& ws);
 hipError_t build_scene_gpu(BuildWorkspace& ws, const Sphere* d_spheres, uint32_t n,
                            const BuildOutputs& o, bool refit, hipStream_t st, BuildSummary* out);
 
+// Pixel hand-out order of the persistent trace kernel (longest-processing-time first). A lane
+// runs one pixel's samples as one sequential chain (the per-pixel LCG stream), so the frame ends
+// with every lane finishing its last pixel alone; handing out expensive tiles first and cheap
+// ones last shortens that tail. Costs are the previous launch's traced segments per 8x8 tile
+// over the same band geometry, recorded by the kernel itself (one atomic per finished pixel).
+struct TileSchedule {
+    uint32_t n = 0;                // tiles of the geometry the tables belong to
+    uint32_t* cost[2] = {nullptr, nullptr};   // ping-pong: the launch being recorded, the last one
+    uint32_t* order = nullptr;     // hand-out rank -> tile
+    uint32_t* keys = nullptr;      // sort scratch
+    uint32_t* iota = nullptr;
+    void* tmp = nullptr;
+    size_t tmp_bytes = 0;
+    int cur = 0;                   // table the next launch records into
+    bool valid = false;            // cost[cur ^ 1] holds a completed launch of this geometry
+};
+// (Re)allocates for n tiles when the geometry changes (tables zeroed, valid = false).
+hipError_t schedule_reserve(TileSchedule& s, uint32_t n, hipStream_t st);
+void schedule_release(TileSchedule& s);
+// order = tiles by descending cost of the last launch (stable: ties in tile order).
+hipError_t schedule_order(TileSchedule& s, hipStream_t st);
+
 // nodes[i] = nodes_raw[i] grown by `pad` on every side (far-camera re-pad).
 hipError_t repad_nodes_gpu(const BvhNode* raw, BvhNode* nodes, uint32_t n_nodes, float pad, hipStream_t st);
 

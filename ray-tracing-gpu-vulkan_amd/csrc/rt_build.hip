@@ -356,6 +356,11 @@ __global__ void __launch_bounds__(kBlock) k_repad(const BvhNode* __restrict__ ra
     nodes[i] = nd;
 }
 
+__global__ void __launch_bounds__(kBlock) k_iota(uint32_t* v, uint32_t n) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) v[i] = i;
+}
+
 inline uint32_t blocks(uint32_t n) { return (n + kBlock - 1) / kBlock; }
 
 template <typename T>
@@ -454,6 +459,46 @@ hipError_t build_scene_gpu(BuildWorkspace& ws, const Sphere* sph, uint32_t n, co
     if (hipError_t e = hipStreamSynchronize(st)) return e;
     if (!refit) ws.topo_n = n;
     return hipSuccess;
+}
+
+void schedule_release(TileSchedule& s) {
+    void* ptrs[] = {s.cost[0], s.cost[1], s.order, s.keys, s.iota, s.tmp};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    s = TileSchedule{};
+}
+
+hipError_t schedule_reserve(TileSchedule& s, uint32_t n, hipStream_t st) {
+    if (s.n == n && s.cost[0]) return hipSuccess;
+    schedule_release(s);
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = alloc(&s.cost[0], n);
+    if (e == hipSuccess) e = alloc(&s.cost[1], n);
+    if (e == hipSuccess) e = alloc(&s.order, n);
+    if (e == hipSuccess) e = alloc(&s.keys, n);
+    if (e == hipSuccess) e = alloc(&s.iota, n);
+    if (e == hipSuccess)
+        e = hipcub::DeviceRadixSort::SortPairsDescending(nullptr, s.tmp_bytes, s.cost[0], s.keys, s.iota, s.order,
+                                                         int(n), 0, 32);
+    if (e == hipSuccess) e = hipMalloc(&s.tmp, s.tmp_bytes + 16);
+    if (e == hipSuccess) e = hipMemsetAsync(s.cost[0], 0, size_t(n) * 4, st);
+    if (e == hipSuccess) e = hipMemsetAsync(s.cost[1], 0, size_t(n) * 4, st);
+    if (e == hipSuccess) {
+        k_iota<<<blocks(n), kBlock, 0, st>>>(s.iota, n);
+        e = hipGetLastError();
+    }
+    if (e != hipSuccess) {
+        schedule_release(s);
+        return e;
+    }
+    s.n = n;
+    return hipSuccess;
+}
+
+hipError_t schedule_order(TileSchedule& s, hipStream_t st) {
+    size_t tb = s.tmp_bytes;
+    return hipcub::DeviceRadixSort::SortPairsDescending(s.tmp, tb, s.cost[s.cur ^ 1], s.keys, s.iota, s.order,
+                                                        int(s.n), 0, 32, st);
 }
 
 hipError_t repad_nodes_gpu(const BvhNode* raw, BvhNode* nodes, uint32_t n_nodes, float pad, hipStream_t st) {

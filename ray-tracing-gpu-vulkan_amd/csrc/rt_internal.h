@@ -89,6 +89,9 @@ struct Counters {
     unsigned long long sphere_tests;
     unsigned long long wave_iters; // COUNT builds: sum over waves of walk-loop iterations
     unsigned long long walk_hist[2][64];  // COUNT builds: box tests per segment, [miss, hit]
+    unsigned long long lane_hist[65];     // COUNT builds: segment-loop iterations by tracing lanes
+    unsigned long long t_first, t_dry, t_last;   // LBVH kernel: s_memrealtime of the first wave's
+                                                 // start, of the pixel queue running dry, of the last exit
     unsigned long long stamp[8];   // diagnostic builds only (-DRT_STAMPS): cycles per phase
 };
 
@@ -108,6 +111,8 @@ struct TraceParams {
     uint32_t tiles_x;              // ceil(band_w / 8)
     uint32_t n_units;              // tiles_x * ceil(band_h / 8) * 64
     const uint32_t* rows;          // optional global row per band row
+    const uint32_t* tile_order;    // optional: hand-out rank -> 8x8 tile index (null: row-major)
+    uint32_t* tile_cost;           // optional: traced segments per 8x8 tile (zeroed by the host)
     // scene
     uint32_t n_spheres;
     const GeomRec* geom;

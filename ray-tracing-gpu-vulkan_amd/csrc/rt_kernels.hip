@@ -233,6 +233,7 @@ struct Path {
     uint32_t seed;         // LCG state (random.glsl)
     uint32_t s;            // samples done for this pixel
     uint32_t depth;        // segments traced in this sample
+    uint32_t segs;         // segments traced for this pixel (tile cost for the hand-out order)
     V3 thr;                // reflectedColor (shader.rgen:71)
     double sx, sy, sz;     // dvec3 sum (shader.rgen:55)
 };
@@ -251,7 +252,7 @@ __device__ __forceinline__ void refill(const rt::TraceParams& P, uint32_t lane, 
     if (st != ST_NEED_PIXEL) return;
     const uint32_t u = base + __popcll(need & ((1ull << lane) - 1ull));
     if (u >= P.n_units) { st = ST_RETIRED; return; }
-    const uint32_t t = u >> 6, w = u & 63u;
+    const uint32_t t = P.tile_order ? P.tile_order[u >> 6] : (u >> 6), w = u & 63u;
     const uint32_t lx = (t % P.tiles_x) * 8u + (w & 7u);
     const uint32_t ly = (t / P.tiles_x) * 8u + (w >> 3);
     if (lx >= P.band_w || ly >= P.band_h) return;   // ragged edge: stays NEED_PIXEL, refetches
@@ -262,6 +263,7 @@ __device__ __forceinline__ void refill(const rt::TraceParams& P, uint32_t lane, 
     ps.pixel_seed = tea(tea(P.seed_local ? lx : gx, P.seed_local ? ly : gy), P.number);
     ps.seed = ps.pixel_seed;
     ps.s = 0;
+    ps.segs = 0;
     if (P.accumulate) {  // shader.rgen:53-55
         const float4 acc = reinterpret_cast<const float4*>(P.accum)[size_t(ly) * P.band_w + lx];
         ps.sx = acc.x; ps.sy = acc.y; ps.sz = acc.z;
@@ -673,16 +675,33 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
     Ray r{};
     uint32_t n_seg = 0, n_smp = 0, n_box = 0, n_sph = 0;
     unsigned long long wave_iters = 0;
+    bool saw_dry = false;
+    // launch telemetry (3 atomics per wave): first start, pixel queue dry, last exit
+    if (lane == 0) atomicMin(&P.counters->t_first, __builtin_amdgcn_s_memrealtime());
     STAMP_DECL;
     for (;;) {
         STAMP(0);
         refill(P, lane, st, ps);
+        if (!saw_dry && __ballot(st == ST_RETIRED)) {   // this wave saw the queue run dry
+            saw_dry = true;
+            if (lane == 0) atomicMin(&P.counters->t_dry, __builtin_amdgcn_s_memrealtime());
+        }
         if (st == ST_NEED_SAMPLE) {
-            if (start_sample(P, cam, ps, r.o, r.d)) { st = ST_TRACING; n_smp++; }
-            else st = ST_NEED_PIXEL;
+            if (start_sample(P, cam, ps, r.o, r.d)) {
+                st = ST_TRACING;
+                n_smp++;
+            } else {   // pixel done: its traced segments feed the next launch's hand-out order
+                st = ST_NEED_PIXEL;
+                if (P.tile_cost) {
+                    const uint32_t lx = ps.px & 0xffffu, ly = ps.px >> 16;
+                    atomicAdd(&P.tile_cost[(ly >> 3) * P.tiles_x + (lx >> 3)], ps.segs);
+                }
+            }
         }
         if (__ballot(st == ST_NEED_PIXEL)) continue;   // refill before the next trace
-        if (!__ballot(st == ST_TRACING)) break;         // every lane retired
+        const unsigned long long tracing = __ballot(st == ST_TRACING);
+        if (!tracing) break;                            // every lane retired
+        if (COUNT && lane == 0) atomicAdd(&P.counters->lane_hist[__popcll(tracing)], 1ull);
         STAMP(1);
         if (st == ST_TRACING) setup_ray(P, r, n_sph);
         STAMP(2);
@@ -705,12 +724,14 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
         STAMP(3);
         if (st == ST_TRACING) {
             n_seg++;
+            ps.segs++;
             if (!shade(P, geom4, mat4, ps, r.bi, r.best, r.o, r.d)) st = ST_NEED_SAMPLE;
         }
     }
     STAMP_FLUSH;
     atomicAdd(&P.counters->segments, (unsigned long long)n_seg);
     atomicAdd(&P.counters->samples, (unsigned long long)n_smp);
+    if (lane == 0) atomicMax(&P.counters->t_last, __builtin_amdgcn_s_memrealtime());
     if (COUNT) {
         atomicAdd(&P.counters->box_tests, (unsigned long long)n_box);
         atomicAdd(&P.counters->sphere_tests, (unsigned long long)n_sph);
@@ -752,11 +773,11 @@ __global__ __launch_bounds__(BLOCK, RT_TRACE_WAVES_PER_SIMD) void rt_trace_lbvh_
             geom4 = lds + base;
             mat4 = lds + base + ng;
         }
-        __syncthreads();
         nodes4 = lds;
         leaf4 = lds + n_node4;
         leaf_ids = reinterpret_cast<const uint32_t*>(lds + n_node4 + n_leaf4);
     }
+    if (LDS) __syncthreads();
     lbvh_classic<COUNT, NODE16>(P, nodes4, leaf4, leaf_ids, geom4, mat4);
 }
 

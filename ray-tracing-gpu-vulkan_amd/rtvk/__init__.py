@@ -143,6 +143,16 @@ class Renderer:
         check(fn(self._ctx, spheres_dev.data_ptr() if n else None, n, st))
         self.sphere_count = n
 
+    def tile_costs(self) -> np.ndarray:
+        """Traced segments per 8x8 tile of the last LBVH launch (row-major tiles; empty before
+        the first launch): the costs the next launch hands tiles out by."""
+        n = ctypes.c_uint64(0)
+        check(self._lib.rt_debug_tile_cost(self._ctx, None, 0, ctypes.byref(n)))
+        out = np.zeros(n.value, np.uint32)
+        if n.value:
+            check(self._lib.rt_debug_tile_cost(self._ctx, out.ctypes.data, n.value, ctypes.byref(n)))
+        return out
+
     _SCENE_DTYPES = {0: (np.float32, 4), 1: (np.float32, 1), 2: (np.uint8, 32), 3: (np.uint32, 1),
                      4: (np.uint8, 32), 5: (np.uint8, 32), 6: (np.float32, 4), 7: (np.uint32, 1)}
 

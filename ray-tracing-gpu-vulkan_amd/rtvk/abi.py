@@ -114,6 +114,8 @@ EXPORTS = {
     "rt_debug_math": (_I, [_I, _I, _P, _P, _U32]),
     "rt_debug_stamps": (_I, [_P, _P]),
     "rt_debug_walk_hist": (_I, [_P, _P]),
+    "rt_debug_lane_hist": (_I, [_P, _P]),
+    "rt_debug_tile_cost": (_I, [_P, _P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     "rt_debug_scene": (_I, [_P, _U32, _P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     "ray_trace": (None, [_U32, ctypes.c_bool, _U32, _U32, _U32]),
 }
