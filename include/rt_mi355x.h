@@ -176,9 +176,9 @@ int rt_debug_walk_hist(rt_context* ctx, uint64_t* out128);
  * (0..64) of the wave tracing in that iteration (the persistent kernel's lane occupancy), then
  * three s_memrealtime stamps (100 MHz): first wave start, pixel queue dry, last wave exit. */
 int rt_debug_lane_hist(rt_context* ctx, uint64_t* out68);
-/* Diagnostic: traced segments per 8x8 tile of ctx's last LBVH launch (the costs its next launch
- * over the same band geometry hands tiles out by); *count = tiles (ceil(W/8) x ceil(H/8),
- * row-major), 0 before the first launch. */
+/* Diagnostic: per 8x8 tile of ctx's last LBVH launch, the traced segments of its most expensive
+ * pixel (the key its next launch over the same band geometry hands tiles out by, longest
+ * first); *count = tiles (ceil(W/8) x ceil(H/8), row-major), 0 before the first launch. */
 int rt_debug_tile_cost(rt_context* ctx, uint32_t* out, uint64_t capacity, uint64_t* count);
 
 /* Diagnostic (tests): copies one scene array of ctx to host memory. what: 0 geometry records,

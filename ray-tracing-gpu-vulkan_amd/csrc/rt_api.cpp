@@ -687,8 +687,9 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
             ctx->padded_for = ctx->pad_radius;
         }
     }
-    // Longest-processing-time-first hand-out from the last launch of this band geometry
-    // (RT_SCHEDULE=rowmajor disables it, A/B only); this launch records the next costs.
+    // Longest-processing-time-first hand-out from the last launch of this band geometry: tiles
+    // in descending order of their longest pixel chain (RT_SCHEDULE=rowmajor | sum: A/B only);
+    // this launch records the next costs.
     if (accel == rt::ACCEL_LBVH || accel == rt::ACCEL_LBVH_LDS || accel == rt::ACCEL_LBVH16_LDS ||
         accel == rt::ACCEL_LBVH_LDS_SCENE) {   // the escape-walk kernels record tile costs
         rt::TileSchedule& sc = ctx->sched;
@@ -701,6 +702,7 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
         }
         RT_HIP(hipMemsetAsync(sc.cost[sc.cur], 0, size_t(sc.n) * 4, st));
         P.tile_cost = sc.cost[sc.cur];
+        P.tile_cost_sum = (e && std::strcmp(e, "sum") == 0) ? 1u : 0u;
     }
     RT_HIP(hipMemsetAsync(ctx->counters, 0, sizeof(rt::Counters), st));
     // first-time stamps start at the maximum (atomicMin); 0xff bytes = ~0ull

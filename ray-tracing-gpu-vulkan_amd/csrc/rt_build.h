@@ -61,9 +61,10 @@ hipError_t build_scene_gpu(BuildWorkspace& ws, const Sphere* d_spheres, uint32_t
 
 // Pixel hand-out order of the persistent trace kernel (longest-processing-time first). A lane
 // runs one pixel's samples as one sequential chain (the per-pixel LCG stream), so the frame ends
-// with every lane finishing its last pixel alone; handing out expensive tiles first and cheap
-// ones last shortens that tail. Costs are the previous launch's traced segments per 8x8 tile
-// over the same band geometry, recorded by the kernel itself (one atomic per finished pixel).
+// with every lane finishing its last pixel alone, and the frame ends with the longest chain still
+// running. Tiles are handed out in descending order of their most expensive pixel (traced
+// segments) in the previous launch over the same band geometry, recorded by the kernel itself
+// (one atomicMax per finished pixel), so long chains start early and the last ones are short.
 struct TileSchedule {
     uint32_t n = 0;                // tiles of the geometry the tables belong to
     uint32_t* cost[2] = {nullptr, nullptr};   // ping-pong: the launch being recorded, the last one

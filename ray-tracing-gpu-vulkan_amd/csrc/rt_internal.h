@@ -112,7 +112,9 @@ struct TraceParams {
     uint32_t n_units;              // tiles_x * ceil(band_h / 8) * 64
     const uint32_t* rows;          // optional global row per band row
     const uint32_t* tile_order;    // optional: hand-out rank -> 8x8 tile index (null: row-major)
-    uint32_t* tile_cost;           // optional: traced segments per 8x8 tile (zeroed by the host)
+    uint32_t* tile_cost;           // optional: per 8x8 tile, traced segments of its most expensive
+                                   // pixel (zeroed by the host)
+    uint32_t tile_cost_sum;        // A/B only: record the tile's total instead
     // scene
     uint32_t n_spheres;
     const GeomRec* geom;

@@ -690,11 +690,12 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
             if (start_sample(P, cam, ps, r.o, r.d)) {
                 st = ST_TRACING;
                 n_smp++;
-            } else {   // pixel done: its traced segments feed the next launch's hand-out order
+            } else {   // pixel done: its chain length feeds the next launch's hand-out order
                 st = ST_NEED_PIXEL;
                 if (P.tile_cost) {
                     const uint32_t lx = ps.px & 0xffffu, ly = ps.px >> 16;
-                    atomicAdd(&P.tile_cost[(ly >> 3) * P.tiles_x + (lx >> 3)], ps.segs);
+                    uint32_t* c = &P.tile_cost[(ly >> 3) * P.tiles_x + (lx >> 3)];
+                    if (P.tile_cost_sum) atomicAdd(c, ps.segs); else atomicMax(c, ps.segs);
                 }
             }
         }

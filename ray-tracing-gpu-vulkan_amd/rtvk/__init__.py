@@ -144,8 +144,9 @@ class Renderer:
         self.sphere_count = n
 
     def tile_costs(self) -> np.ndarray:
-        """Traced segments per 8x8 tile of the last LBVH launch (row-major tiles; empty before
-        the first launch): the costs the next launch hands tiles out by."""
+        """Per 8x8 tile of the last LBVH launch, the traced segments of its most expensive pixel
+        (row-major tiles; empty before the first launch): the key the next launch hands tiles out
+        by, longest first."""
         n = ctypes.c_uint64(0)
         check(self._lib.rt_debug_tile_cost(self._ctx, None, 0, ctypes.byref(n)))
         out = np.zeros(n.value, np.uint32)

@@ -1,5 +1,5 @@
-"""Diagnostic: persistent-kernel tail with and without the LPT hand-out order on the canonical
-1080p frame (RT_SCHEDULE=rowmajor disables it). Reports frame time and the launch telemetry:
+"""Diagnostic: persistent-kernel tail by pixel hand-out order on the canonical 1080p frame:
+row-major, tiles by total cost (RT_SCHEDULE=sum), tiles by longest pixel chain (default, "lpt"). Reports frame time and the launch telemetry:
 when the pixel queue ran dry and how long the tail after it took. Images must be identical."""
 import ctypes
 import os
@@ -21,12 +21,12 @@ acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
 out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
 rci = rtvk.canonical_render_call_info(spp, W, H)
 imgs = {}
-for rep in range(4):
-    for mode in ("rowmajor", "lpt"):
-        if mode == "rowmajor":
-            os.environ["RT_SCHEDULE"] = "rowmajor"
-        else:
+for rep in range(3):
+    for mode in ("rowmajor", "sum", "lpt"):
+        if mode == "lpt":
             os.environ.pop("RT_SCHEDULE", None)
+        else:
+            os.environ["RT_SCHEDULE"] = mode
         ts, tails, drys = [], [], []
         for i in range(8):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -43,5 +43,5 @@ for rep in range(4):
         imgs[mode] = out.cpu()
         print(f"{mode:8s}: frame {np.median(ts):.2f} ms (min {min(ts):.2f}), queue dry at "
               f"{np.median(drys):.2f} ms, tail {np.median(tails):.2f} ms", flush=True)
-assert torch.equal(imgs["rowmajor"], imgs["lpt"])
+assert all(torch.equal(imgs["rowmajor"], v) for v in imgs.values())
 print("images identical")

@@ -248,17 +248,17 @@ def test_band_split_invariance_full_size(rtvk, renderer, torch, oracle):
 
 
 def test_lpt_schedule_same_image(rtvk, renderer, torch, oracle):
-    """The second launch over a band geometry hands tiles out in descending cost of the first
-    (longest-processing-time first): per-tile costs sum to the traced segments, the image and the
-    counts are unchanged, and equal the oracle."""
+    """The second launch over a band geometry hands tiles out longest pixel chain first (the
+    first launch's costs): every tile's key is a real chain length (spp .. spp x depth
+    segments), and the image and the counts are unchanged and equal the oracle."""
     sc = oracle.generate_scene()
-    W, H = 100, 60   # ragged 8x8 tiles
-    rci = oracle.render_call_info(3, W, H)
+    W, H, spp = 100, 60, 3   # ragged 8x8 tiles
+    rci = oracle.render_call_info(spp, W, H)
     ra, ro, rst = oracle.render(sc, rci, W, H)
     a0, o0, s0 = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH)
     cost = renderer.tile_costs()
     assert cost.shape == (((W + 7) // 8) * ((H + 7) // 8),)
-    assert int(cost.sum()) == s0.segments and len(np.unique(cost)) > 4
+    assert (cost >= spp).all() and (cost <= spp * 50).all() and len(np.unique(cost)) > 4
     a1, o1, s1 = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH)
     assert_same(a0, o0, ra, ro)
     assert_same(a1, o1, ra, ro)
