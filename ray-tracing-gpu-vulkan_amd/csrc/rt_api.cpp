@@ -30,6 +30,7 @@ hipError_t launch_trace(const TraceParams& P, uint32_t accel, bool count, int gr
                         hipStream_t st);
 hipError_t trace_occupancy(uint32_t accel, bool count, size_t lds_bytes, int* blocks_per_cu);
 uint32_t block_size(uint32_t accel);
+size_t pool_bytes(uint32_t accel);
 hipError_t launch_scatter_rows(const float* src_acc, const uint8_t* src_px, const uint32_t* rows,
                                uint32_t n_rows, uint32_t width, float* dst_acc, uint8_t* dst_px,
                                hipStream_t st);
@@ -127,6 +128,8 @@ static constexpr size_t kMaxLdsBvhBytes = 24 * 1024;
 // LBVH + per-sphere geometry/material records staged together up to this size (512-thread
 // blocks: 3 blocks = 24 waves per CU fit in the 160 KiB LDS).
 static constexpr size_t kMaxLdsSceneBytes = 52 * 1024;
+// LDS-scene staging + the tail-compaction pool of a 1024-thread block (one block per CU).
+static constexpr size_t kMaxLdsPoolBytes = 156 * 1024;
 // Ordered-walk LBVH staged in LDS up to this size (plus the per-lane stacks).
 static constexpr size_t kMaxLdsBvh2Bytes = 40 * 1024;
 
@@ -587,7 +590,9 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     if (opt) o = *opt;
     // reserved[1] (internal, A/B only): LBVH walk form, 0 = default (stackless escape-link walk
     // over 32-B nodes), 2 = ordered two-wide walk with an LDS stack, 4 = escape-link walk over
-    // compact 16-B binary16 nodes (both slower on the canonical scene)
+    // compact 16-B binary16 nodes (both slower on the canonical scene), 5 = scene
+    // records from global memory, 7 = LDS scene + tail-compaction pool (at 4 waves per SIMD the
+    // tail is already short: the pool measured 1 ms slower)
     const bool escape_walk = o.reserved[1] != 2u;
     if (!escape_walk && ctx->gpu_tree && ctx->scene.n_nodes)
         return fail(RT_ERR_INVALID_ARGUMENT, "the ordered walk needs a host-built tree (RT_BVH_BUILD=sah or morton)");
@@ -600,6 +605,10 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     } else if (escape_walk && allow16 && ctx->lds16_bytes) {
         accel = rt::ACCEL_LBVH16_LDS;
         lds = ctx->lds16_bytes;
+    } else if (escape_walk && ctx->lds_scene_bytes && o.reserved[1] == 7u &&
+               ctx->lds_scene_bytes + rt::pool_bytes(rt::ACCEL_LBVH_POOL) <= kMaxLdsPoolBytes) {
+        accel = rt::ACCEL_LBVH_POOL;   // A/B: tail compaction through the block's LDS pool
+        lds = ctx->lds_scene_bytes + rt::pool_bytes(rt::ACCEL_LBVH_POOL);
     } else if (escape_walk && ctx->lds_scene_bytes && o.reserved[1] != 5u) {
         accel = rt::ACCEL_LBVH_LDS_SCENE;
         lds = ctx->lds_scene_bytes;
@@ -653,8 +662,13 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     P.leaf_ids = d.leaf_ids;
     // Node-cull slack: a candidate's AABB entry lies at most
     // 2.75 r + 1.15e-3 t beyond its reported t.
+#ifdef RT_CULL_ABS_AB   // A/B experiments only (scripts/perf_variants.py --inexact)
+    P.cull_abs = RT_CULL_ABS_AB;
+    P.cull_rel = RT_CULL_REL_AB;
+#else
     P.cull_abs = 3.0f * d.small_rmax + 1e-3f;
     P.cull_rel = 2e-3f;
+#endif
 
     P.accum = accum;
     P.out = reinterpret_cast<uint32_t*>(out);
@@ -691,7 +705,7 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     // in descending order of their longest pixel chain (RT_SCHEDULE=rowmajor | sum: A/B only);
     // this launch records the next costs.
     if (accel == rt::ACCEL_LBVH || accel == rt::ACCEL_LBVH_LDS || accel == rt::ACCEL_LBVH16_LDS ||
-        accel == rt::ACCEL_LBVH_LDS_SCENE) {   // the escape-walk kernels record tile costs
+        accel == rt::ACCEL_LBVH_LDS_SCENE || accel == rt::ACCEL_LBVH_POOL) {   // escape-walk kernels record tile costs
         rt::TileSchedule& sc = ctx->sched;
         RT_HIP(rt::schedule_reserve(sc, uint32_t(tiles_x * tiles_y), st));
         const char* e = std::getenv("RT_SCHEDULE");

@@ -77,7 +77,8 @@ struct DeviceScene {
     float small_rmax = 0.0f;       // largest radius in the tree
 };
 
-enum : uint32_t { ACCEL_BRUTE = 1, ACCEL_LBVH = 2, ACCEL_LBVH_LDS = 3, ACCEL_LBVH2 = 4, ACCEL_LBVH2_LDS = 5, ACCEL_LBVH16_LDS = 6, ACCEL_LBVH_LDS_SCENE = 7 };
+enum : uint32_t { ACCEL_BRUTE = 1, ACCEL_LBVH = 2, ACCEL_LBVH_LDS = 3, ACCEL_LBVH2 = 4, ACCEL_LBVH2_LDS = 5, ACCEL_LBVH16_LDS = 6, ACCEL_LBVH_LDS_SCENE = 7,
+       ACCEL_LBVH_POOL = 8 /* LBVH_LDS_SCENE + tail-compaction pool, 1024-thread blocks */ };
 
 // Counters block (device memory, zeroed before each launch by the host).
 struct Counters {

@@ -616,8 +616,14 @@ __device__ __forceinline__ void walk_escape16(const rt::TraceParams& P, const ui
     }
 }
 
+// Waves per SIMD the register budget is sized for. Brute force: 6 (71 VGPRs, no spills). LBVH:
+// 4 (128 VGPRs): at 6 the 80-VGPR budget spilled ~34 VGPRs of path state around every walk, and
+// 4 waves of the unspilled kernel measured 8 % faster.
+#ifndef RT_BRUTE_WAVES_PER_SIMD
+#define RT_BRUTE_WAVES_PER_SIMD 6
+#endif
 #ifndef RT_TRACE_WAVES_PER_SIMD
-#define RT_TRACE_WAVES_PER_SIMD 6
+#define RT_TRACE_WAVES_PER_SIMD 4
 #endif
 
 // ---------------------------------------------------------------------------------------------
@@ -625,7 +631,7 @@ __device__ __forceinline__ void walk_escape16(const rt::TraceParams& P, const ui
 // wave-uniform, so there is no traversal divergence to manage).
 // ---------------------------------------------------------------------------------------------
 template <bool COUNT>
-__global__ __launch_bounds__(256, RT_TRACE_WAVES_PER_SIMD) void rt_trace_brute_kernel(const rt::TraceParams P) {
+__global__ __launch_bounds__(256, RT_BRUTE_WAVES_PER_SIMD) void rt_trace_brute_kernel(const rt::TraceParams P) {
     const uint32_t lane = lane_id();
     const Camera cam = load_camera(P);
     uint32_t st = ST_NEED_PIXEL;
@@ -658,16 +664,115 @@ __global__ __launch_bounds__(256, RT_TRACE_WAVES_PER_SIMD) void rt_trace_brute_k
 }
 
 // ---------------------------------------------------------------------------------------------
+// Tail compaction pool (block-local, LDS). Once the device pixel queue has run dry, lanes whose
+// pixel ends stay empty, and a wave keeps paying full issue cost for a shrinking set of paths
+// (the per-pixel sample stream is sequential, so the last pixels cannot be split). Waves that
+// fall below RT_POOL_T active lanes donate their in-flight paths (pixel state + next ray) to a
+// block-wide LDS pool and go idle; waves with empty lanes refill from it. The block's paths thus
+// concentrate in few, full waves, and idle waves sleep (s_sleep) instead of issuing.
+//
+// Protocol (one LDS spin lock, taken by one lane per wave):
+//   count   paths in the pool (LIFO stack of `cap` slots, SoA: field f of slot i at f*cap+i);
+//           read and written only under the lock
+//   working waves holding at least one path; changed ONLY by atomics (a wave whose last path
+//           ends decrements it without the lock), increments happen under the lock
+// A wave donates only while another wave is working (so someone drains the pool); an idle wave
+// takes paths when at least RT_POOL_T are waiting or no wave is working; it exits when, under
+// the lock, working == 0 and count == 0: no path exists any more, and none can appear.
+// Capacity: every path is in exactly one lane or slot, so count <= paths in block <= cap.
+// ---------------------------------------------------------------------------------------------
+#ifndef RT_POOL_T
+#define RT_POOL_T 32
+#endif
+constexpr uint32_t kPoolFields = 22;   // st, px, pixel_seed, seed, s, depth, segs, thr3, o3, d3, 3 x f64
+
+struct PoolCtl { uint32_t lock, count, working, pad; };
+
+__device__ __forceinline__ void pool_lock(PoolCtl* c) {
+    while (atomicCAS(&c->lock, 0u, 1u) != 0u) __builtin_amdgcn_s_sleep(1);
+    __threadfence_block();
+}
+__device__ __forceinline__ void pool_unlock(PoolCtl* c) {
+    __threadfence_block();
+    atomicExch(&c->lock, 0u);
+}
+__device__ __forceinline__ uint32_t pool_peek(const PoolCtl* c, uint32_t f) {   // lock-free hint
+    return __hip_atomic_load(reinterpret_cast<const uint32_t*>(c) + f, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ void pool_put(uint32_t* pool, uint32_t cap, uint32_t i, uint32_t st,
+                                         const Path& ps, const Ray& r) {
+    const uint32_t v[kPoolFields] = {
+        st, ps.px, ps.pixel_seed, ps.seed, ps.s, ps.depth, ps.segs,
+        __float_as_uint(ps.thr.x), __float_as_uint(ps.thr.y), __float_as_uint(ps.thr.z),
+        __float_as_uint(r.o.x), __float_as_uint(r.o.y), __float_as_uint(r.o.z),
+        __float_as_uint(r.d.x), __float_as_uint(r.d.y), __float_as_uint(r.d.z),
+        uint32_t(__double_as_longlong(ps.sx)), uint32_t(__double_as_longlong(ps.sx) >> 32),
+        uint32_t(__double_as_longlong(ps.sy)), uint32_t(__double_as_longlong(ps.sy) >> 32),
+        uint32_t(__double_as_longlong(ps.sz)), uint32_t(__double_as_longlong(ps.sz) >> 32)};
+#pragma unroll
+    for (uint32_t f = 0; f < kPoolFields; ++f) pool[f * cap + i] = v[f];
+}
+
+__device__ __forceinline__ void pool_get(const uint32_t* pool, uint32_t cap, uint32_t i, uint32_t& st,
+                                         Path& ps, Ray& r) {
+    uint32_t v[kPoolFields];
+#pragma unroll
+    for (uint32_t f = 0; f < kPoolFields; ++f) v[f] = pool[f * cap + i];
+    st = v[0]; ps.px = v[1]; ps.pixel_seed = v[2]; ps.seed = v[3]; ps.s = v[4]; ps.depth = v[5]; ps.segs = v[6];
+    ps.thr = v3(__uint_as_float(v[7]), __uint_as_float(v[8]), __uint_as_float(v[9]));
+    r.o = v3(__uint_as_float(v[10]), __uint_as_float(v[11]), __uint_as_float(v[12]));
+    r.d = v3(__uint_as_float(v[13]), __uint_as_float(v[14]), __uint_as_float(v[15]));
+    ps.sx = __longlong_as_double((long long)(uint64_t(v[16]) | uint64_t(v[17]) << 32));
+    ps.sy = __longlong_as_double((long long)(uint64_t(v[18]) | uint64_t(v[19]) << 32));
+    ps.sz = __longlong_as_double((long long)(uint64_t(v[20]) | uint64_t(v[21]) << 32));
+}
+
+// Take up to `want` paths from the pool into the lanes of `vacant` (caller holds nothing; the
+// leader takes the lock). `idle`: the wave holds no path yet, so it takes only when at least
+// RT_POOL_T paths wait or no wave is working, and counts itself working when it takes any.
+// Returns the number taken (wave-uniform).
+__device__ __forceinline__ uint32_t pool_take(PoolCtl* ctl, uint32_t* pool, uint32_t cap, uint32_t lane,
+                                              unsigned long long vacant, bool idle, uint32_t& st,
+                                              Path& ps, Ray& r) {
+    const int leader = __ffsll(vacant) - 1;
+    uint32_t base = 0, k = 0;
+    if (int(lane) == leader) {
+        pool_lock(ctl);
+        const uint32_t c = ctl->count;
+        if (!idle || c >= RT_POOL_T || pool_peek(ctl, 2) == 0u) {
+            k = min(c, (uint32_t)__popcll(vacant));
+            base = c - k;
+        }
+        if (k == 0u) pool_unlock(ctl);
+    }
+    k = __shfl(k, leader);
+    if (k == 0u) return 0u;
+    base = __shfl(base, leader);
+    const uint32_t rank = __popcll(vacant & ((1ull << lane) - 1ull));
+    if (((vacant >> lane) & 1ull) && rank < k) pool_get(pool, cap, base + rank, st, ps, r);
+    __threadfence_block();   // every lane's reads are back before the slots can be reused
+    if (int(lane) == leader) {
+        ctl->count = base;
+        if (idle) atomicAdd(&ctl->working, 1u);
+        pool_unlock(ctl);
+    }
+    return k;
+}
+
+// ---------------------------------------------------------------------------------------------
 // LBVH kernel, classic form: one segment per lane per loop iteration; the wave's walk loop runs
 // until its longest walk ends. Stamp slots: 0 refill+sample start, 1 ray setup (big spheres),
-// 2 LBVH walk, 3 shading, 7 other.
+// 2 LBVH walk, 3 shading, 7 other. POOL: tail compaction through the block's LDS pool.
 // ---------------------------------------------------------------------------------------------
-template <bool COUNT, bool NODE16>
+template <bool COUNT, bool NODE16, bool POOL>
 __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const float4* __restrict__ nodes4,
                                              const float4* __restrict__ leaf4,
                                              const uint32_t* __restrict__ leaf_ids,
                                              const float4* __restrict__ geom4,
-                                             const float4* __restrict__ mat4) {
+                                             const float4* __restrict__ mat4,
+                                             PoolCtl* ctl, uint32_t* pool, uint32_t cap) {
     const uint32_t lane = lane_id();
     const Camera cam = load_camera(P);
     uint32_t st = ST_NEED_PIXEL;
@@ -681,10 +786,67 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
     STAMP_DECL;
     for (;;) {
         STAMP(0);
-        refill(P, lane, st, ps);
+        if (!POOL || !saw_dry) {
+            refill(P, lane, st, ps);
+        } else if (st == ST_NEED_PIXEL) {
+            st = ST_RETIRED;   // the queue never refills once dry
+        }
         if (!saw_dry && __ballot(st == ST_RETIRED)) {   // this wave saw the queue run dry
             saw_dry = true;
             if (lane == 0) atomicMin(&P.counters->t_dry, __builtin_amdgcn_s_memrealtime());
+            if (POOL && st == ST_NEED_PIXEL) st = ST_RETIRED;
+        }
+        if (POOL && saw_dry) {
+            const unsigned long long held = __ballot(st == ST_TRACING || st == ST_NEED_SAMPLE);
+            uint32_t n_held = __popcll(held);
+            if (n_held != 0u && n_held < RT_POOL_T) {   // donate, if another wave keeps working
+                const int leader = __ffsll(held) - 1;
+                uint32_t base = 0, ok = 0;
+                if (int(lane) == leader) {
+                    pool_lock(ctl);
+                    ok = pool_peek(ctl, 2) > 1u ? 1u : 0u;
+                    base = ctl->count;
+                    if (!ok) pool_unlock(ctl);
+                }
+                if (__shfl(ok, leader)) {
+                    base = __shfl(base, leader);
+                    if ((held >> lane) & 1ull) {
+                        pool_put(pool, cap, base + __popcll(held & ((1ull << lane) - 1ull)), st, ps, r);
+                        st = ST_RETIRED;
+                    }
+                    __threadfence_block();   // slots written before the count publishes them
+                    if (int(lane) == leader) {
+                        ctl->count = base + n_held;
+                        atomicSub(&ctl->working, 1u);
+                        pool_unlock(ctl);
+                    }
+                    n_held = 0u;
+                }   // refused (the only working wave): keep the paths, top up below
+
+            } else if (n_held == 0u) {   // idle since the last iteration: stop counting as working
+                if (lane == 0) atomicSub(&ctl->working, 1u);
+            }
+            if (n_held == 0u) {   // idle: wait for paths, or for the block's end
+                bool done = false;
+                for (;;) {
+                    const uint32_t c = pool_peek(ctl, 1), w = pool_peek(ctl, 2);
+                    if (c >= RT_POOL_T || (c != 0u && w == 0u)) {
+                        if (pool_take(ctl, pool, cap, lane, ~0ull, true, st, ps, r)) break;
+                    } else if (c == 0u && w == 0u) {
+                        uint32_t fin = 0;
+                        if (lane == 0) {
+                            pool_lock(ctl);
+                            fin = (ctl->count == 0u && pool_peek(ctl, 2) == 0u) ? 1u : 0u;
+                            pool_unlock(ctl);
+                        }
+                        if (__shfl(fin, 0)) { done = true; break; }
+                    }
+                    __builtin_amdgcn_s_sleep(8);
+                }
+                if (done) break;
+            } else if (n_held < 64u && pool_peek(ctl, 1) != 0u) {   // top up empty lanes
+                pool_take(ctl, pool, cap, lane, ~held, false, st, ps, r);
+            }
         }
         if (st == ST_NEED_SAMPLE) {
             if (start_sample(P, cam, ps, r.o, r.d)) {
@@ -701,7 +863,10 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
         }
         if (__ballot(st == ST_NEED_PIXEL)) continue;   // refill before the next trace
         const unsigned long long tracing = __ballot(st == ST_TRACING);
-        if (!tracing) break;                            // every lane retired
+        if (!tracing) {                                 // every lane retired
+            if (POOL && saw_dry) continue;              // the pool stage decides idle / exit
+            break;
+        }
         if (COUNT && lane == 0) atomicAdd(&P.counters->lane_hist[__popcll(tracing)], 1ull);
         STAMP(1);
         if (st == ST_TRACING) setup_ray(P, r, n_sph);
@@ -746,16 +911,19 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
 
 // LBVH kernel. LDS: stage the tree (nodes, leaf spheres, leaf ids) and, when SCENE_LDS, the
 // per-sphere geometry + material records read by shading, once per persistent block. Blocks of
-// RT_LBVH_BLOCK threads share one staged copy.
-template <bool LDS, bool COUNT, bool NODE16, bool SCENE_LDS, uint32_t BLOCK>
+// BLOCK threads share one staged copy. POOL: the tail-compaction pool (BLOCK slots x
+// kPoolFields words) follows the staged data.
+template <bool LDS, bool COUNT, bool NODE16, bool SCENE_LDS, bool POOL, uint32_t BLOCK>
 __global__ __launch_bounds__(BLOCK, RT_TRACE_WAVES_PER_SIMD) void rt_trace_lbvh_kernel(const rt::TraceParams P) {
     extern __shared__ float4 lds[];
+    __shared__ PoolCtl ctl;
     const float4* nodes4 = NODE16 ? reinterpret_cast<const float4*>(P.nodes16)
                                   : reinterpret_cast<const float4*>(P.nodes);
     const float4* leaf4 = reinterpret_cast<const float4*>(P.leaf_geom);
     const uint32_t* leaf_ids = P.leaf_ids;
     const float4* geom4 = reinterpret_cast<const float4*>(P.geom);
     const float4* mat4 = reinterpret_cast<const float4*>(P.mat);
+    uint32_t staged4 = 0;
     if (LDS) {
         const uint32_t n_node4 = (NODE16 ? 1u : 2u) * P.n_nodes, n_leaf4 = P.n_leaf, n_id4 = (P.n_leaf + 3u) / 4u;
         for (uint32_t i = threadIdx.x; i < n_node4; i += BLOCK) lds[i] = nodes4[i];
@@ -767,19 +935,28 @@ __global__ __launch_bounds__(BLOCK, RT_TRACE_WAVES_PER_SIMD) void rt_trace_lbvh_
                                                      __uint_as_float(v.z), __uint_as_float(v.w));
         }
         const uint32_t base = n_node4 + n_leaf4 + n_id4;
+        staged4 = base;
         if (SCENE_LDS) {
             const uint32_t ng = P.n_spheres, nm = 2u * P.n_spheres;
             for (uint32_t i = threadIdx.x; i < ng; i += BLOCK) lds[base + i] = geom4[i];
             for (uint32_t i = threadIdx.x; i < nm; i += BLOCK) lds[base + ng + i] = mat4[i];
             geom4 = lds + base;
             mat4 = lds + base + ng;
+            staged4 = base + ng + nm;
         }
         nodes4 = lds;
         leaf4 = lds + n_node4;
         leaf_ids = reinterpret_cast<const uint32_t*>(lds + n_node4 + n_leaf4);
     }
-    if (LDS) __syncthreads();
-    lbvh_classic<COUNT, NODE16>(P, nodes4, leaf4, leaf_ids, geom4, mat4);
+    if (POOL && threadIdx.x == 0) {
+        ctl.lock = 0u;
+        ctl.count = 0u;
+        ctl.working = BLOCK / 64u;   // every wave enters the loop holding (or about to hold) paths
+        ctl.pad = 0u;
+    }
+    if (LDS || POOL) __syncthreads();
+    lbvh_classic<COUNT, NODE16, POOL>(P, nodes4, leaf4, leaf_ids, geom4, mat4, &ctl,
+                                      reinterpret_cast<uint32_t*>(lds + staged4), BLOCK);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -903,7 +1080,13 @@ constexpr uint32_t kLbvh2Block = RT_LBVH2_BLOCK;
 
 constexpr uint32_t kLbvhBlock = RT_LBVH_BLOCK;
 
-#define RT_LBVH_FN(L, C, N16, S) reinterpret_cast<const void*>(rt_trace_lbvh_kernel<L, C, N16, S, kLbvhBlock>)
+#ifndef RT_POOL_BLOCK
+#define RT_POOL_BLOCK 1024
+#endif
+constexpr uint32_t kPoolBlock = RT_POOL_BLOCK;   // one block per CU: the pool spans all 16 waves
+
+#define RT_LBVH_FN(L, C, N16, S) reinterpret_cast<const void*>(rt_trace_lbvh_kernel<L, C, N16, S, false, kLbvhBlock>)
+#define RT_POOL_FN(C) reinterpret_cast<const void*>(rt_trace_lbvh_kernel<true, C, false, true, true, kPoolBlock>)
 static const void* pick(uint32_t accel, bool count) {
     switch (accel) {
         case ACCEL_BRUTE:
@@ -913,6 +1096,8 @@ static const void* pick(uint32_t accel, bool count) {
             return count ? RT_LBVH_FN(true, true, false, false) : RT_LBVH_FN(true, false, false, false);
         case ACCEL_LBVH_LDS_SCENE:
             return count ? RT_LBVH_FN(true, true, false, true) : RT_LBVH_FN(true, false, false, true);
+        case ACCEL_LBVH_POOL:
+            return count ? RT_POOL_FN(true) : RT_POOL_FN(false);
         case ACCEL_LBVH16_LDS:
             return count ? RT_LBVH_FN(true, true, true, false) : RT_LBVH_FN(true, false, true, false);
         case ACCEL_LBVH2:
@@ -926,11 +1111,13 @@ static const void* pick(uint32_t accel, bool count) {
     }
 }
 #undef RT_LBVH_FN
+#undef RT_POOL_FN
 
 uint32_t block_size(uint32_t accel) {
     switch (accel) {
         case ACCEL_LBVH2: case ACCEL_LBVH2_LDS: return kLbvh2Block;
         case ACCEL_BRUTE: return 256u;
+        case ACCEL_LBVH_POOL: return kPoolBlock;
         default: return kLbvhBlock;
     }
 }
@@ -939,6 +1126,10 @@ hipError_t launch_trace(const TraceParams& P, uint32_t accel, bool count, int gr
                         hipStream_t st) {
     void* args[] = {const_cast<TraceParams*>(&P)};
     return hipLaunchKernel(pick(accel, count), dim3(grid), dim3(block_size(accel)), args, lds_bytes, st);
+}
+
+size_t pool_bytes(uint32_t accel) {
+    return accel == ACCEL_LBVH_POOL ? size_t(kPoolBlock) * kPoolFields * 4u : 0u;
 }
 
 hipError_t trace_occupancy(uint32_t accel, bool count, size_t lds_bytes, int* blocks_per_cu) {

@@ -20,7 +20,9 @@ GOLDEN = Path(__file__).resolve().parent / "golden"
 BRUTE, LBVH = 1, 2
 LBVH_ORDERED = 3   # test-only alias: accel LBVH with the ordered two-wide walk (options.reserved[1] = 2)
 LBVH_COMPACT = 4   # test-only alias: accel LBVH, escape-link walk over 16-B nodes (options.reserved[1] = 4)
-WALK_FORM = {LBVH_ORDERED: 2, LBVH_COMPACT: 4}
+LBVH_POOL = 5      # test-only alias: accel LBVH, LDS scene + tail-compaction pool (options.reserved[1] = 7)
+WALK_FORM = {LBVH_ORDERED: 2, LBVH_COMPACT: 4, LBVH_POOL: 7}
+HOST_TREE_FORMS = (LBVH_ORDERED, LBVH_COMPACT)
 
 
 @contextlib.contextmanager
@@ -63,7 +65,7 @@ def renderer(rtvk):
 def gpu_render(rtvk, renderer, torch, spheres, rci_u32, band_w, band_h, rows=None, accel=LBVH,
                max_depth=50, seed_mode=0, rng_mode=0, accumulate=False, sample_base=0, accum=None,
                count=False, builder=None):
-    with tree_builder(builder or ("sah" if accel in WALK_FORM else None)):
+    with tree_builder(builder or ("sah" if accel in HOST_TREE_FORMS else None)):
         renderer.set_scene(np.ascontiguousarray(spheres, np.uint8).reshape(-1, 80))
     rci = rtvk.RenderCallInfo.from_buffer_copy(np.ascontiguousarray(rci_u32).tobytes())
     acc = (torch.zeros((band_h, band_w, 4), dtype=torch.float32, device="cuda") if accum is None
@@ -129,7 +131,7 @@ def test_math_primitives_bit_exact(rtvk, torch, oracle, op):
 
 
 # ---- golden fixtures --------------------------------------------------------------------------
-@pytest.mark.parametrize("accel", [BRUTE, LBVH, LBVH_ORDERED, LBVH_COMPACT])
+@pytest.mark.parametrize("accel", [BRUTE, LBVH, LBVH_ORDERED, LBVH_COMPACT, LBVH_POOL])
 @pytest.mark.parametrize("case", ["g64x36_spp4", "g48x32_spp3_depth3_local", "g40x24_spp2_counter"])
 def test_golden(rtvk, renderer, torch, oracle, case, accel):
     m = json.loads((GOLDEN / f"{case}.json").read_text())
@@ -155,7 +157,7 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("accel", [BRUTE, LBVH, LBVH_ORDERED, LBVH_COMPACT])
+@pytest.mark.parametrize("accel", [BRUTE, LBVH, LBVH_ORDERED, LBVH_COMPACT, LBVH_POOL])
 @pytest.mark.parametrize("case", range(len(CASES)))
 def test_vs_oracle(rtvk, renderer, torch, oracle, case, accel):
     W, H, oy, bh, spp, t, K, kw = CASES[case]
@@ -171,7 +173,7 @@ def test_empty_and_single_sphere(rtvk, renderer, torch, oracle):
     rci = oracle.render_call_info(2, 20, 10)
     for sc in (np.zeros((0, 80), np.uint8), oracle.generate_scene()[:1], oracle.generate_scene()[3:4]):
         ra, ro, _ = oracle.render(sc, rci, 20, 10)
-        for accel in (BRUTE, LBVH, LBVH_ORDERED, LBVH_COMPACT):
+        for accel in (BRUTE, LBVH, LBVH_ORDERED, LBVH_COMPACT, LBVH_POOL):
             a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, 20, 10, accel=accel)
             assert_same(a, o, ra, ro)
 
@@ -232,7 +234,7 @@ def test_lbvh_equals_brute_full_size(rtvk, renderer, torch, oracle, W, H, spp, K
         al, ol, sl = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH, builder=builder)
         assert_same(al, ol, ab, ob)
         assert sb.segments == sl.segments
-    for form in (LBVH_ORDERED, LBVH_COMPACT):
+    for form in (LBVH_ORDERED, LBVH_COMPACT, LBVH_POOL):
         ao, oo, so = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=form)
         assert_same(ao, oo, ab, ob)
 
