@@ -591,8 +591,9 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     // reserved[1] (internal, A/B only): LBVH walk form, 0 = default (stackless escape-link walk
     // over 32-B nodes), 2 = ordered two-wide walk with an LDS stack, 4 = escape-link walk over
     // compact 16-B binary16 nodes (both slower on the canonical scene), 5 = scene
-    // records from global memory, 7 = LDS scene + tail-compaction pool (at 4 waves per SIMD the
-    // tail is already short: the pool measured 1 ms slower)
+    // records from global memory, 6 = LDS scene with one node copy, 7 = that + the tail-compaction
+    // pool (at 4 waves per SIMD the tail is already short: the pool measured 1 ms slower), 8 =
+    // octant-specialised node copies (the default whenever they fit in LDS)
     const bool escape_walk = o.reserved[1] != 2u;
     if (!escape_walk && ctx->gpu_tree && ctx->scene.n_nodes)
         return fail(RT_ERR_INVALID_ARGUMENT, "the ordered walk needs a host-built tree (RT_BVH_BUILD=sah or morton)");
@@ -605,6 +606,10 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     } else if (escape_walk && allow16 && ctx->lds16_bytes) {
         accel = rt::ACCEL_LBVH16_LDS;
         lds = ctx->lds16_bytes;
+    } else if (escape_walk && ctx->lds_scene_bytes && (o.reserved[1] == 0u || o.reserved[1] == 8u) &&
+               ctx->lds_scene_bytes + size_t(14u) * ds.n_nodes * 16u <= kMaxLdsPoolBytes) {
+        accel = rt::ACCEL_LBVH_OCT;   // default when it fits: octant-specialised node copies in LDS
+        lds = ctx->lds_scene_bytes + size_t(14u) * ds.n_nodes * 16u;
     } else if (escape_walk && ctx->lds_scene_bytes && o.reserved[1] == 7u &&
                ctx->lds_scene_bytes + rt::pool_bytes(rt::ACCEL_LBVH_POOL) <= kMaxLdsPoolBytes) {
         accel = rt::ACCEL_LBVH_POOL;   // A/B: tail compaction through the block's LDS pool
@@ -705,7 +710,7 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     // in descending order of their longest pixel chain (RT_SCHEDULE=rowmajor | sum: A/B only);
     // this launch records the next costs.
     if (accel == rt::ACCEL_LBVH || accel == rt::ACCEL_LBVH_LDS || accel == rt::ACCEL_LBVH16_LDS ||
-        accel == rt::ACCEL_LBVH_LDS_SCENE || accel == rt::ACCEL_LBVH_POOL) {   // escape-walk kernels record tile costs
+        accel == rt::ACCEL_LBVH_LDS_SCENE || accel == rt::ACCEL_LBVH_POOL || accel == rt::ACCEL_LBVH_OCT) {   // escape-walk kernels record tile costs
         rt::TileSchedule& sc = ctx->sched;
         RT_HIP(rt::schedule_reserve(sc, uint32_t(tiles_x * tiles_y), st));
         const char* e = std::getenv("RT_SCHEDULE");

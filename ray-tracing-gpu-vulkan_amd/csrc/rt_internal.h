@@ -78,7 +78,8 @@ struct DeviceScene {
 };
 
 enum : uint32_t { ACCEL_BRUTE = 1, ACCEL_LBVH = 2, ACCEL_LBVH_LDS = 3, ACCEL_LBVH2 = 4, ACCEL_LBVH2_LDS = 5, ACCEL_LBVH16_LDS = 6, ACCEL_LBVH_LDS_SCENE = 7,
-       ACCEL_LBVH_POOL = 8 /* LBVH_LDS_SCENE + tail-compaction pool, 1024-thread blocks */ };
+       ACCEL_LBVH_POOL = 8 /* LBVH_LDS_SCENE + tail-compaction pool, 1024-thread blocks */,
+       ACCEL_LBVH_OCT = 9  /* LBVH_LDS_SCENE with 8 octant-specialised node copies, 1024-thread blocks */ };
 
 // Counters block (device memory, zeroed before each launch by the host).
 struct Counters {

@@ -387,7 +387,7 @@ __device__ __forceinline__ bool shade(const rt::TraceParams& P, const float4* __
 // LBVH traversal state and the one-node step.
 // ---------------------------------------------------------------------------------------------
 struct Ray {
-    V3 o, d, inv, oi;      // origin, direction, 1/d, o * (1/d)
+    V3 o, d, inv;          // origin, direction, 1/d (the AABB gate's own reciprocals)
     float a;               // dot(d, d)
     float limit;           // node cull limit: min(best + cull_abs + cull_rel * best, tmax)
     float best;
@@ -396,11 +396,55 @@ struct Ray {
 constexpr uint32_t END = 0xffffffffu;
 constexpr uint32_t kLeafFlagD = 0x80000000u;
 
+// Node slab test: one fma per plane, t = fma(plane, inv, -o * inv) (a sub-then-mul form is exact
+// in the gate's own arithmetic but costs twice the issue cycles: packed f32 ops take 4 cycles on
+// gfx950). Node boxes are padded at build time by 12u x (scene + camera radius),
+// which covers the rounding of this form against the spheres' AABB gates.
+// A zero (or denormal) direction component makes 1/d infinite; the fma form would then produce
+// inf - inf = NaN for a plane on the far side of the origin and cull a box the ray runs inside, so
+// the node reciprocal is clamped to +-2^100: the slab then spans (-huge, +huge) exactly when the
+// origin lies inside the padded slab, which is what the gate's (plane - o) * inf gives.
+// Node layout "AB" (LDS): A = (x0, y0, x1, y1), B = (z0, z1, escape, leaf). OCT: the node copy
+// is specialised to the ray's direction octant, (x0, y0, z0) are the near planes and (x1, y1,
+// z1) the far ones, so no per-axis min/max is needed.
+struct RayBox { V3 inv, oi; };
+
+__device__ __forceinline__ float node_inv(float inv) {
+    return __builtin_isinf(inv) ? __builtin_copysignf(0x1p100f, inv) : inv;
+}
+__device__ __forceinline__ RayBox ray_box(const V3 o, const V3 inv) {
+    const V3 n = v3(node_inv(inv.x), node_inv(inv.y), node_inv(inv.z));
+    return RayBox{n, v3(o.x * n.x, o.y * n.y, o.z * n.z)};
+}
+
+template <bool OCT>
+__device__ __forceinline__ bool node_hit(const float4 A, const float4 B, const RayBox& q, float limit) {
+    const float tx0 = __builtin_fmaf(A.x, q.inv.x, -q.oi.x), ty0 = __builtin_fmaf(A.y, q.inv.y, -q.oi.y);
+    const float tx1 = __builtin_fmaf(A.z, q.inv.x, -q.oi.x), ty1 = __builtin_fmaf(A.w, q.inv.y, -q.oi.y);
+    const float tz0 = __builtin_fmaf(B.x, q.inv.z, -q.oi.z), tz1 = __builtin_fmaf(B.y, q.inv.z, -q.oi.z);
+    float tn, tf;
+    if (OCT) {
+        tn = fmaxf(fmaxf(tx0, ty0), fmaxf(tz0, T_MIN));
+        tf = fminf(fminf(tx1, ty1), tz1);
+    } else {
+        tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), T_MIN));
+        tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+    }
+    // == tn <= min(tf, limit): limit is never NaN, so splitting the min into a second compare
+    // gives the same answer without re-canonicalising the loop-invariant limit every visit.
+    return tn <= tf && tn <= limit;
+}
+
+// Octant of a direction: bit k set when component k is negative (sign bit, so -0 -> 1/d = -inf
+// counts as negative, matching the copy whose near plane is the box's high side).
+__device__ __forceinline__ uint32_t octant(const V3 d) {
+    return (__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 31) << 1) | ((__float_as_uint(d.z) >> 31) << 2);
+}
+
 // New segment: hoisted per-ray terms, the exhaustive big spheres, walk from the root.
 __device__ __forceinline__ void setup_ray(const rt::TraceParams& P, Ray& r, uint32_t& n_sph) {
     r.a = dot(r.d, r.d);
     r.inv = v3(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
-    r.oi = v3(r.o.x * r.inv.x, r.o.y * r.inv.y, r.o.z * r.inv.z);
     r.best = T_MAX_SUCC;
     r.bi = 0xffffffffu;
     typedef const __attribute__((address_space(4))) uint32_t* ConstU;
@@ -443,15 +487,8 @@ __device__ __forceinline__ void visit_node(const rt::TraceParams& P, const float
     const float4 n0 = nodes4[2 * r.ni];
     const float4 n1 = nodes4[2 * r.ni + 1];
     if (COUNT) n_box++;
-    const float tx0 = __builtin_fmaf(n0.x, r.inv.x, -r.oi.x), tx1 = __builtin_fmaf(n1.x, r.inv.x, -r.oi.x);
-    const float ty0 = __builtin_fmaf(n0.y, r.inv.y, -r.oi.y), ty1 = __builtin_fmaf(n1.y, r.inv.y, -r.oi.y);
-    const float tz0 = __builtin_fmaf(n0.z, r.inv.z, -r.oi.z), tz1 = __builtin_fmaf(n1.z, r.inv.z, -r.oi.z);
-    const float tnear = fmaxf(fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1)), T_MIN);
-    // Node boxes are padded at build time by 12u x (scene + camera radius), which covers the
-    // rounding of this one-fma slab form against the exact form of the spheres' AABB gates
-    // (DESIGN.md §4.3), so the comparison needs no tolerance term.
-    const float tfar = fminf(fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1)), r.limit);
-    const bool hit = tnear <= tfar;
+    const bool hit = node_hit<false>(make_float4(n0.x, n0.y, n1.x, n1.y), make_float4(n0.z, n1.z, 0.0f, 0.0f),
+                                     ray_box(r.o, r.inv), r.limit);
     const uint32_t fc = __float_as_uint(n1.w);
     if (hit && fc != 0u) {   // leaf: always 4 slots (dummy-padded), loads issued together
         const uint32_t first = fc >> 4;
@@ -479,9 +516,10 @@ __device__ __forceinline__ void leaf_block(const rt::TraceParams& P, uint32_t re
 }
 
 __device__ __forceinline__ float slab_near(float4 lo, float4 hi, const Ray& r, float& tfar_out) {
-    const float tx0 = __builtin_fmaf(lo.x, r.inv.x, -r.oi.x), tx1 = __builtin_fmaf(hi.x, r.inv.x, -r.oi.x);
-    const float ty0 = __builtin_fmaf(lo.y, r.inv.y, -r.oi.y), ty1 = __builtin_fmaf(hi.y, r.inv.y, -r.oi.y);
-    const float tz0 = __builtin_fmaf(lo.z, r.inv.z, -r.oi.z), tz1 = __builtin_fmaf(hi.z, r.inv.z, -r.oi.z);
+    const RayBox q = ray_box(r.o, r.inv);   // (hoisted by the compiler: loop-invariant)
+    const float tx0 = __builtin_fmaf(lo.x, q.inv.x, -q.oi.x), tx1 = __builtin_fmaf(hi.x, q.inv.x, -q.oi.x);
+    const float ty0 = __builtin_fmaf(lo.y, q.inv.y, -q.oi.y), ty1 = __builtin_fmaf(hi.y, q.inv.y, -q.oi.y);
+    const float tz0 = __builtin_fmaf(lo.z, q.inv.z, -q.oi.z), tz1 = __builtin_fmaf(hi.z, q.inv.z, -q.oi.z);
     tfar_out = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
     return fmaxf(fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1)), T_MIN);
 }
@@ -537,15 +575,15 @@ __device__ __forceinline__ void walk_ordered(const rt::TraceParams& P, const flo
     }
 }
 
-// The whole escape-link walk of one segment. With RT_PREFETCH both possible successors of the
-// current node (index + 1 and its escape) are loaded before the current box test, so the next
-// visit's LDS latency overlaps this visit's arithmetic (one dependent round trip per visit
-// instead of two).
-template <bool COUNT>
+// The whole escape-link walk of one segment. LAYOUT: 0 = BvhNode pairs (global memory), 1 = AB
+// layout (LDS), 2 = AB layout specialised to the ray's octant (LDS, `nodes4` already offset to the
+// ray's copy).
+template <bool COUNT, int LAYOUT>
 __device__ __forceinline__ void walk_escape(const rt::TraceParams& P, const float4* __restrict__ nodes4,
                                             const float4* __restrict__ leaf4,
                                             const uint32_t* __restrict__ leaf_ids, Ray& r,
                                             uint32_t& n_box, uint32_t& n_sph) {
+    const RayBox q = ray_box(r.o, r.inv);
 #ifdef RT_LEAF_INLINE
     while (r.ni != END) visit_node<COUNT>(P, nodes4, leaf4, leaf_ids, r, n_box, n_sph);
 #else
@@ -553,35 +591,63 @@ __device__ __forceinline__ void walk_escape(const rt::TraceParams& P, const floa
     // found a hit leaf (postponed in `pending`) or finished its walk; then all pending leaves are
     // tested together, so the 4-sphere leaf block runs once per batch instead of in every visit
     // in which any lane of the wave happens to be at a leaf.
-    uint32_t pending = 0u;
-    for (;;) {
-        while (r.ni != END && pending == 0u) {
-            const float4 n0 = nodes4[2 * r.ni];
-            const float4 n1 = nodes4[2 * r.ni + 1];
-            if (COUNT) n_box++;
-            const float tx0 = __builtin_fmaf(n0.x, r.inv.x, -r.oi.x), tx1 = __builtin_fmaf(n1.x, r.inv.x, -r.oi.x);
-            const float ty0 = __builtin_fmaf(n0.y, r.inv.y, -r.oi.y), ty1 = __builtin_fmaf(n1.y, r.inv.y, -r.oi.y);
-            const float tz0 = __builtin_fmaf(n0.z, r.inv.z, -r.oi.z), tz1 = __builtin_fmaf(n1.z, r.inv.z, -r.oi.z);
-            const float tnear = fmaxf(fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1)), T_MIN);
-            const float tfar = fminf(fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1)), r.limit);
-            const bool hit = tnear <= tfar;
-            const uint32_t fc = __float_as_uint(n1.w);
-            if (hit && fc != 0u) pending = fc;
-            r.ni = (hit && fc == 0u) ? r.ni + 1u : __float_as_uint(n0.w);
+    if (LAYOUT == 0) {   // BvhNode pairs: escape in lo.w, leaf field (first << 4 | count, 0 = inner) in hi.w
+        uint32_t pending = 0u;
+        for (;;) {
+            while (r.ni != END && pending == 0u) {
+                const float4 n0 = nodes4[2 * r.ni];
+                const float4 n1 = nodes4[2 * r.ni + 1];
+                if (COUNT) n_box++;
+                const bool hit = node_hit<false>(make_float4(n0.x, n0.y, n1.x, n1.y),
+                                                 make_float4(n0.z, n1.z, 0.0f, 0.0f), q, r.limit);
+                const uint32_t fc = __float_as_uint(n1.w);
+                if (hit && fc != 0u) pending = fc;
+                r.ni = (hit && fc == 0u) ? r.ni + 1u : __float_as_uint(n0.w);
+            }
+            if (pending == 0u) break;   // walk finished with no leaf left to test
+            const uint32_t first = pending >> 4;
+            const float4 s0 = leaf4[first], s1 = leaf4[first + 1], s2 = leaf4[first + 2], s3 = leaf4[first + 3];
+            test4(s0, s1, s2, s3, [&](uint32_t k) { return leaf_ids[first + k]; }, r.o, r.d, r.inv, r.a,
+                  r.best, r.bi, r.limit, P.cull_abs, P.cull_rel);
+            if (COUNT) n_sph += pending & 15u;
+            pending = 0u;
         }
-        if (pending == 0u) break;   // walk finished with no leaf left to test
-        const uint32_t first = pending >> 4;
-        const float4 s0 = leaf4[first], s1 = leaf4[first + 1], s2 = leaf4[first + 2], s3 = leaf4[first + 3];
-        test4(s0, s1, s2, s3, [&](uint32_t k) { return leaf_ids[first + k]; }, r.o, r.d, r.inv, r.a,
-              r.best, r.bi, r.limit, P.cull_abs, P.cull_rel);
-        if (COUNT) n_sph += pending & 15u;
-        pending = 0u;
+    } else {
+        // AB layout: B.z = escape, B.w = next index when the box is hit (inner node) or, with
+        // bit 31 set, the leaf field. A lane leaves the inner loop AT a hit leaf (r.ni stays
+        // on it), so the loop carries no pending register; the leaf's field is re-read after.
+        for (;;) {
+            uint32_t ni = r.ni;
+            bool go = ni != END;
+            while (go) {
+                const float4 A = nodes4[2 * ni];
+                const float4 B = nodes4[2 * ni + 1];
+                if (COUNT) n_box++;
+                const bool hit = node_hit<LAYOUT == 2>(A, B, q, r.limit);
+                const uint32_t link = __float_as_uint(B.w);
+                const bool at_leaf = hit && int32_t(link) < 0;   // stop here, test the leaf below
+                const uint32_t nxt = hit ? link : __float_as_uint(B.z);
+                ni = at_leaf ? ni : nxt;
+                go = !at_leaf && nxt != END;
+            }
+            r.ni = ni;
+            if (!__ballot(ni != END)) break;   // no lane stopped at a leaf: all walks done
+            if (ni != END) {
+                const float4 B = nodes4[2 * ni + 1];
+                const uint32_t fc = __float_as_uint(B.w) & 0x7fffffffu, first = fc >> 4;
+                const float4 s0 = leaf4[first], s1 = leaf4[first + 1], s2 = leaf4[first + 2], s3 = leaf4[first + 3];
+                test4(s0, s1, s2, s3, [&](uint32_t k) { return leaf_ids[first + k]; }, r.o, r.d, r.inv, r.a,
+                      r.best, r.bi, r.limit, P.cull_abs, P.cull_rel);
+                if (COUNT) n_sph += fc & 15u;
+                r.ni = __float_as_uint(B.z);
+            }
+        }
     }
 #endif
 }
 
 // Escape-link walk over compact 16-B nodes (BvhNode16): one ds_read_b128 per visit; the binary16
-// bounds enter the slab fmas directly through v_fma_mix_f32 (exact f16 -> f32 widening).
+// bounds are widened exactly to f32 (v_fma_mix_f32) and enter the one-fma slab test.
 __device__ __forceinline__ float h_lo(uint32_t v) {
     return (float)__builtin_bit_cast(_Float16, (unsigned short)(v & 0xffffu));
 }
@@ -595,12 +661,13 @@ __device__ __forceinline__ void walk_escape16(const rt::TraceParams& P, const ui
                                               const uint32_t* __restrict__ leaf_ids, Ray& r,
                                               uint32_t& n_box, uint32_t& n_sph) {
     uint32_t ni = (P.n_nodes != 0u) ? 0u : 0xffffu;
+    const RayBox q = ray_box(r.o, r.inv);
     while (ni != 0xffffu) {
         const uint4 n = nodes[ni];
         if (COUNT) n_box++;
-        const float tx0 = __builtin_fmaf(h_lo(n.x), r.inv.x, -r.oi.x), tx1 = __builtin_fmaf(h_hi(n.y), r.inv.x, -r.oi.x);
-        const float ty0 = __builtin_fmaf(h_hi(n.x), r.inv.y, -r.oi.y), ty1 = __builtin_fmaf(h_lo(n.z), r.inv.y, -r.oi.y);
-        const float tz0 = __builtin_fmaf(h_lo(n.y), r.inv.z, -r.oi.z), tz1 = __builtin_fmaf(h_hi(n.z), r.inv.z, -r.oi.z);
+        const float tx0 = __builtin_fmaf(h_lo(n.x), q.inv.x, -q.oi.x), tx1 = __builtin_fmaf(h_hi(n.y), q.inv.x, -q.oi.x);
+        const float ty0 = __builtin_fmaf(h_hi(n.x), q.inv.y, -q.oi.y), ty1 = __builtin_fmaf(h_lo(n.z), q.inv.y, -q.oi.y);
+        const float tz0 = __builtin_fmaf(h_lo(n.y), q.inv.z, -q.oi.z), tz1 = __builtin_fmaf(h_hi(n.z), q.inv.z, -q.oi.z);
         const float tnear = fmaxf(fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1)), T_MIN);
         const float tfar = fminf(fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1)), r.limit);
         const bool hit = tnear <= tfar;
@@ -766,7 +833,7 @@ __device__ __forceinline__ uint32_t pool_take(PoolCtl* ctl, uint32_t* pool, uint
 // until its longest walk ends. Stamp slots: 0 refill+sample start, 1 ray setup (big spheres),
 // 2 LBVH walk, 3 shading, 7 other. POOL: tail compaction through the block's LDS pool.
 // ---------------------------------------------------------------------------------------------
-template <bool COUNT, bool NODE16, bool POOL>
+template <bool COUNT, bool NODE16, bool POOL, int LAYOUT>
 __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const float4* __restrict__ nodes4,
                                              const float4* __restrict__ leaf4,
                                              const uint32_t* __restrict__ leaf_ids,
@@ -876,7 +943,8 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
             if (NODE16)
                 walk_escape16<COUNT>(P, reinterpret_cast<const uint4*>(nodes4), leaf4, leaf_ids, r, n_box, n_sph);
             else
-                walk_escape<COUNT>(P, nodes4, leaf4, leaf_ids, r, n_box, n_sph);
+                walk_escape<COUNT, LAYOUT>(P, LAYOUT == 2 ? nodes4 + octant(r.d) * 2u * P.n_nodes : nodes4,
+                                           leaf4, leaf_ids, r, n_box, n_sph);
         }
         if (COUNT && st == ST_TRACING) {   // walk-length histogram (diagnostic, COUNT builds only)
             const uint32_t len = min(n_box - box0, 63u);
@@ -911,9 +979,10 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
 
 // LBVH kernel. LDS: stage the tree (nodes, leaf spheres, leaf ids) and, when SCENE_LDS, the
 // per-sphere geometry + material records read by shading, once per persistent block. Blocks of
-// BLOCK threads share one staged copy. POOL: the tail-compaction pool (BLOCK slots x
+// BLOCK threads share one staged copy. Staged nodes use the AB layout (node_hit); OCT stages 8
+// copies, one per ray direction octant. POOL: the tail-compaction pool (BLOCK slots x
 // kPoolFields words) follows the staged data.
-template <bool LDS, bool COUNT, bool NODE16, bool SCENE_LDS, bool POOL, uint32_t BLOCK>
+template <bool LDS, bool COUNT, bool NODE16, bool SCENE_LDS, bool POOL, bool OCT, uint32_t BLOCK>
 __global__ __launch_bounds__(BLOCK, RT_TRACE_WAVES_PER_SIMD) void rt_trace_lbvh_kernel(const rt::TraceParams P) {
     extern __shared__ float4 lds[];
     __shared__ PoolCtl ctl;
@@ -925,8 +994,30 @@ __global__ __launch_bounds__(BLOCK, RT_TRACE_WAVES_PER_SIMD) void rt_trace_lbvh_
     const float4* mat4 = reinterpret_cast<const float4*>(P.mat);
     uint32_t staged4 = 0;
     if (LDS) {
-        const uint32_t n_node4 = (NODE16 ? 1u : 2u) * P.n_nodes, n_leaf4 = P.n_leaf, n_id4 = (P.n_leaf + 3u) / 4u;
-        for (uint32_t i = threadIdx.x; i < n_node4; i += BLOCK) lds[i] = nodes4[i];
+        const uint32_t n_node4 = (NODE16 ? 1u : (OCT ? 16u : 2u)) * P.n_nodes, n_leaf4 = P.n_leaf,
+                       n_id4 = (P.n_leaf + 3u) / 4u;
+        if (NODE16) {
+            for (uint32_t i = threadIdx.x; i < n_node4; i += BLOCK) lds[i] = nodes4[i];
+        } else {
+            for (uint32_t i = threadIdx.x; i < P.n_nodes; i += BLOCK) {
+                const float4 lo = nodes4[2 * i], hi = nodes4[2 * i + 1];   // BvhNode: lo.xyz esc, hi.xyz leaf
+                // B.w: inner node -> i + 1 (next on hit), leaf -> 0x80000000 | first << 4 | count
+                const uint32_t fc = __float_as_uint(hi.w);
+                const float link = __uint_as_float(fc ? (fc | 0x80000000u) : i + 1u);
+                if (!OCT) {
+                    lds[2 * i] = make_float4(lo.x, lo.y, hi.x, hi.y);
+                    lds[2 * i + 1] = make_float4(lo.z, hi.z, lo.w, link);
+                } else {
+#pragma unroll
+                    for (uint32_t o = 0; o < 8; ++o) {   // bit k of o: axis k runs negative, near = hi
+                        const bool nx = o & 1u, ny = o & 2u, nz = o & 4u;
+                        const size_t b = (size_t(o) * P.n_nodes + i) * 2u;
+                        lds[b] = make_float4(nx ? hi.x : lo.x, ny ? hi.y : lo.y, nx ? lo.x : hi.x, ny ? lo.y : hi.y);
+                        lds[b + 1] = make_float4(nz ? hi.z : lo.z, nz ? lo.z : hi.z, lo.w, link);
+                    }
+                }
+            }
+        }
         for (uint32_t i = threadIdx.x; i < n_leaf4; i += BLOCK) lds[n_node4 + i] = leaf4[i];
         const uint4* ids4 = reinterpret_cast<const uint4*>(P.leaf_ids);
         for (uint32_t i = threadIdx.x; i < n_id4; i += BLOCK) {
@@ -955,8 +1046,8 @@ __global__ __launch_bounds__(BLOCK, RT_TRACE_WAVES_PER_SIMD) void rt_trace_lbvh_
         ctl.pad = 0u;
     }
     if (LDS || POOL) __syncthreads();
-    lbvh_classic<COUNT, NODE16, POOL>(P, nodes4, leaf4, leaf_ids, geom4, mat4, &ctl,
-                                      reinterpret_cast<uint32_t*>(lds + staged4), BLOCK);
+    lbvh_classic<COUNT, NODE16, POOL, (LDS && !NODE16) ? (OCT ? 2 : 1) : 0>(
+        P, nodes4, leaf4, leaf_ids, geom4, mat4, &ctl, reinterpret_cast<uint32_t*>(lds + staged4), BLOCK);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1085,8 +1176,9 @@ constexpr uint32_t kLbvhBlock = RT_LBVH_BLOCK;
 #endif
 constexpr uint32_t kPoolBlock = RT_POOL_BLOCK;   // one block per CU: the pool spans all 16 waves
 
-#define RT_LBVH_FN(L, C, N16, S) reinterpret_cast<const void*>(rt_trace_lbvh_kernel<L, C, N16, S, false, kLbvhBlock>)
-#define RT_POOL_FN(C) reinterpret_cast<const void*>(rt_trace_lbvh_kernel<true, C, false, true, true, kPoolBlock>)
+#define RT_LBVH_FN(L, C, N16, S) reinterpret_cast<const void*>(rt_trace_lbvh_kernel<L, C, N16, S, false, false, kLbvhBlock>)
+#define RT_POOL_FN(C) reinterpret_cast<const void*>(rt_trace_lbvh_kernel<true, C, false, true, true, false, kPoolBlock>)
+#define RT_OCT_FN(C) reinterpret_cast<const void*>(rt_trace_lbvh_kernel<true, C, false, true, false, true, kPoolBlock>)
 static const void* pick(uint32_t accel, bool count) {
     switch (accel) {
         case ACCEL_BRUTE:
@@ -1098,6 +1190,8 @@ static const void* pick(uint32_t accel, bool count) {
             return count ? RT_LBVH_FN(true, true, false, true) : RT_LBVH_FN(true, false, false, true);
         case ACCEL_LBVH_POOL:
             return count ? RT_POOL_FN(true) : RT_POOL_FN(false);
+        case ACCEL_LBVH_OCT:
+            return count ? RT_OCT_FN(true) : RT_OCT_FN(false);
         case ACCEL_LBVH16_LDS:
             return count ? RT_LBVH_FN(true, true, true, false) : RT_LBVH_FN(true, false, true, false);
         case ACCEL_LBVH2:
@@ -1112,12 +1206,13 @@ static const void* pick(uint32_t accel, bool count) {
 }
 #undef RT_LBVH_FN
 #undef RT_POOL_FN
+#undef RT_OCT_FN
 
 uint32_t block_size(uint32_t accel) {
     switch (accel) {
         case ACCEL_LBVH2: case ACCEL_LBVH2_LDS: return kLbvh2Block;
         case ACCEL_BRUTE: return 256u;
-        case ACCEL_LBVH_POOL: return kPoolBlock;
+        case ACCEL_LBVH_POOL: case ACCEL_LBVH_OCT: return kPoolBlock;
         default: return kLbvhBlock;
     }
 }

@@ -21,7 +21,8 @@ BRUTE, LBVH = 1, 2
 LBVH_ORDERED = 3   # test-only alias: accel LBVH with the ordered two-wide walk (options.reserved[1] = 2)
 LBVH_COMPACT = 4   # test-only alias: accel LBVH, escape-link walk over 16-B nodes (options.reserved[1] = 4)
 LBVH_POOL = 5      # test-only alias: accel LBVH, LDS scene + tail-compaction pool (options.reserved[1] = 7)
-WALK_FORM = {LBVH_ORDERED: 2, LBVH_COMPACT: 4, LBVH_POOL: 7}
+LBVH_OCT = 6       # test-only alias: accel LBVH, octant-specialised node copies in LDS (options.reserved[1] = 8)
+WALK_FORM = {LBVH_ORDERED: 2, LBVH_COMPACT: 4, LBVH_POOL: 7, LBVH_OCT: 8}
 HOST_TREE_FORMS = (LBVH_ORDERED, LBVH_COMPACT)
 
 
@@ -131,7 +132,7 @@ def test_math_primitives_bit_exact(rtvk, torch, oracle, op):
 
 
 # ---- golden fixtures --------------------------------------------------------------------------
-@pytest.mark.parametrize("accel", [BRUTE, LBVH, LBVH_ORDERED, LBVH_COMPACT, LBVH_POOL])
+@pytest.mark.parametrize("accel", [BRUTE, LBVH, LBVH_ORDERED, LBVH_COMPACT, LBVH_POOL, LBVH_OCT])
 @pytest.mark.parametrize("case", ["g64x36_spp4", "g48x32_spp3_depth3_local", "g40x24_spp2_counter"])
 def test_golden(rtvk, renderer, torch, oracle, case, accel):
     m = json.loads((GOLDEN / f"{case}.json").read_text())
@@ -157,7 +158,7 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("accel", [BRUTE, LBVH, LBVH_ORDERED, LBVH_COMPACT, LBVH_POOL])
+@pytest.mark.parametrize("accel", [BRUTE, LBVH, LBVH_ORDERED, LBVH_COMPACT, LBVH_POOL, LBVH_OCT])
 @pytest.mark.parametrize("case", range(len(CASES)))
 def test_vs_oracle(rtvk, renderer, torch, oracle, case, accel):
     W, H, oy, bh, spp, t, K, kw = CASES[case]
@@ -173,7 +174,7 @@ def test_empty_and_single_sphere(rtvk, renderer, torch, oracle):
     rci = oracle.render_call_info(2, 20, 10)
     for sc in (np.zeros((0, 80), np.uint8), oracle.generate_scene()[:1], oracle.generate_scene()[3:4]):
         ra, ro, _ = oracle.render(sc, rci, 20, 10)
-        for accel in (BRUTE, LBVH, LBVH_ORDERED, LBVH_COMPACT, LBVH_POOL):
+        for accel in (BRUTE, LBVH, LBVH_ORDERED, LBVH_COMPACT, LBVH_POOL, LBVH_OCT):
             a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, 20, 10, accel=accel)
             assert_same(a, o, ra, ro)
 
@@ -234,7 +235,7 @@ def test_lbvh_equals_brute_full_size(rtvk, renderer, torch, oracle, W, H, spp, K
         al, ol, sl = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH, builder=builder)
         assert_same(al, ol, ab, ob)
         assert sb.segments == sl.segments
-    for form in (LBVH_ORDERED, LBVH_COMPACT, LBVH_POOL):
+    for form in (LBVH_ORDERED, LBVH_COMPACT, LBVH_POOL, LBVH_OCT):
         ao, oo, so = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=form)
         assert_same(ao, oo, ab, ob)
 
@@ -315,3 +316,18 @@ def test_scatter_rows_reassembles_strips(rtvk, renderer, torch, oracle):
         renderer.scatter_rows(a, o, rows, full_a, full_o)
     torch.cuda.synchronize()
     assert_same(full_a.cpu().numpy(), full_o.cpu().numpy(), ra, ro)
+
+
+@pytest.mark.parametrize("form", [LBVH, LBVH_OCT, LBVH_POOL])
+def test_lbvh_equals_brute_bench_workload(rtvk, renderer, torch, oracle, form):
+    """The bench frame itself (1920x1080, 100 spp, canonical scene): ~5.9e8 traced segments, so
+    rare rays (a direction component that is exactly zero, grazing hits) all occur; every
+    accumulator float and rgba8 byte of the LBVH walk equals brute force."""
+    sc = oracle.generate_scene()
+    rci = oracle.render_call_info(100, 1920, 1080)
+    ab, ob, sb = gpu_render(rtvk, renderer, torch, sc, rci, 1920, 1080, accel=BRUTE)
+    al, ol, sl = gpu_render(rtvk, renderer, torch, sc, rci, 1920, 1080, accel=form)
+    bad = np.argwhere(np.any(al != ab, axis=-1))
+    assert bad.size == 0, f"{len(bad)} pixels differ from brute force, first {bad[:4].tolist()}"
+    np.testing.assert_array_equal(ol, ob)
+    assert (sl.segments, sl.samples) == (sb.segments, sb.samples)
