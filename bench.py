@@ -65,6 +65,14 @@ def cpu_baseline(width: int, height: int, target_s: float = 15.0) -> dict:
             "config1_frame_s": round(t1, 3)}
 
 
+def _pmc_record(path: Path, key: str):
+    """A committed rocprofv3 --pmc summary (scripts/pmc_to_json.py) for this workload, or None."""
+    try:
+        return json.loads(path.read_text()).get(key)
+    except (OSError, ValueError):
+        return None
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--gpus", type=int, default=1)
@@ -78,6 +86,9 @@ def main() -> int:
     ap.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=None,
                     help="BASELINE.json config preset: 2/3/4 = 1920x1080 at 100/10000/10000 spp, "
                          "5 = 3840x2160, 99 860 spheres, 1000 spp (overrides --width/--height/--spp/--grid)")
+    ap.add_argument("--count-spp", type=int, default=100,
+                    help="spp of the instrumented (test-counting) launch; its counts are scaled to --spp "
+                         "(per-sample statistics are stationary: same scene, same per-pixel streams)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-brute-line", action="store_true", help="skip the brute-force side measurement")
     ap.add_argument("--profile", action="store_true", help="short run for rocprofv3 (no side legs)")
@@ -183,16 +194,19 @@ def main() -> int:
     local_rows = len(dr.rows_np)
     cnt_opts = rtvk.make_options(accel=accel, count_tests=True)
     cnt_opts.reserved[1] = args.walk
+    cnt_spp = max(1, min(spp, args.count_spp))
     if local_rows:
         acc = torch.zeros((local_rows, W, 4), dtype=torch.float32, device=dev)
         out = torch.zeros((local_rows, W, 4), dtype=torch.uint8, device=dev)
-        renderer.render_device(rci, acc, out, rows=dr.rows, options=cnt_opts)
+        renderer.render_device(rtvk.canonical_render_call_info(cnt_spp, W, H), acc, out, rows=dr.rows,
+                               options=cnt_opts)
         torch.cuda.synchronize()
         cs = renderer.stats()
         del acc, out
     else:
         cs = rtvk.Stats()
-    flops = cs.box_tests * FLOP_PER_BOX_TEST + cs.sphere_tests * FLOP_PER_SPHERE_TEST
+    scale = spp / cnt_spp
+    flops = (cs.box_tests * FLOP_PER_BOX_TEST + cs.sphere_tests * FLOP_PER_SPHERE_TEST) * scale
     achieved = flops / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
 
     result = None
@@ -208,12 +222,17 @@ def main() -> int:
                 traffic = None
         roof = {"bound": "valu-fp32", "achieved": round(achieved, 3), "peak": VALU_FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / VALU_FP32_PEAK_TFLOPS, 4), "traffic": traffic,
-                "kernel": "rt_trace_lbvh_kernel<LDS,false>" if accel == 2 else "rt_trace_brute_kernel<false>",
+                "kernel": "rt_trace_lbvh_kernel (octant LDS walk)" if accel == 2 else "rt_trace_brute_kernel",
                 "kernel_ms": round(kernel_ms, 4),
-                "flop_per_launch": int(flops), "box_tests": int(cs.box_tests),
-                "sphere_tests": int(cs.sphere_tests),
+                "flop_per_launch": int(flops), "box_tests": int(cs.box_tests * scale),
+                "sphere_tests": int(cs.sphere_tests * scale),
                 "flop_model": "20/box test + 23/sphere test (SURVEY.md 8(d)); counts from the "
-                              "instrumented build of the same kernel"}
+                              f"instrumented build of the same kernel at {cnt_spp} spp"
+                              + (f", x{scale:g}" if scale != 1 else "")}
+        valu = _pmc_record(ROOT / "profiles" / "pmc_valu.json", f"{args.accel}-{W}x{H}-{spp}spp-grid{args.grid}-n{world}")
+        if valu:
+            roof["valu_issue_busy"] = valu.get("valu_issue_busy")
+            roof["lane_util"] = valu.get("lane_util")
         result = {
             "metric": "Msamples/s (1920x1080 RTIOW scene, depth 50)",
             "value": round(value, 2),

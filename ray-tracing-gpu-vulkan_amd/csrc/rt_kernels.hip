@@ -578,8 +578,11 @@ __device__ __forceinline__ void walk_ordered(const rt::TraceParams& P, const flo
 // The whole escape-link walk of one segment. LAYOUT: 0 = BvhNode pairs (global memory), 1 = AB
 // layout (LDS), 2 = AB layout specialised to the ray's octant (LDS, `nodes4` already offset to the
 // ray's copy).
+#ifndef RT_WALK_CAP
+#define RT_WALK_CAP 0   // node visits per lane per segment-loop iteration (0: walk to the end)
+#endif
 template <bool COUNT, int LAYOUT>
-__device__ __forceinline__ void walk_escape(const rt::TraceParams& P, const float4* __restrict__ nodes4,
+__device__ __forceinline__ bool walk_escape(const rt::TraceParams& P, const float4* __restrict__ nodes4,
                                             const float4* __restrict__ leaf4,
                                             const uint32_t* __restrict__ leaf_ids, Ray& r,
                                             uint32_t& n_box, uint32_t& n_sph) {
@@ -616,23 +619,29 @@ __device__ __forceinline__ void walk_escape(const rt::TraceParams& P, const floa
         // AB layout: B.z = escape, B.w = next index when the box is hit (inner node) or, with
         // bit 31 set, the leaf field. A lane leaves the inner loop AT a hit leaf (r.ni stays
         // on it), so the loop carries no pending register; the leaf's field is re-read after.
+        // RT_WALK_CAP: a lane walks at most that many nodes per segment-loop iteration and
+        // resumes from r.ni in the next one, so one long walk does not hold the whole wave.
+        uint32_t budget = RT_WALK_CAP ? RT_WALK_CAP : 0xffffffffu;
         for (;;) {
             uint32_t ni = r.ni;
-            bool go = ni != END;
+            bool go = ni != END && budget != 0u, stop_leaf = false;
             while (go) {
                 const float4 A = nodes4[2 * ni];
                 const float4 B = nodes4[2 * ni + 1];
                 if (COUNT) n_box++;
+                if (RT_WALK_CAP) budget--;
                 const bool hit = node_hit<LAYOUT == 2>(A, B, q, r.limit);
                 const uint32_t link = __float_as_uint(B.w);
                 const bool at_leaf = hit && int32_t(link) < 0;   // stop here, test the leaf below
                 const uint32_t nxt = hit ? link : __float_as_uint(B.z);
                 ni = at_leaf ? ni : nxt;
-                go = !at_leaf && nxt != END;
+                stop_leaf = at_leaf;
+                go = !at_leaf && nxt != END && (!RT_WALK_CAP || budget != 0u);
             }
             r.ni = ni;
-            if (!__ballot(ni != END)) break;   // no lane stopped at a leaf: all walks done
-            if (ni != END) {
+            if (!RT_WALK_CAP) stop_leaf = ni != END;
+            if (!__ballot(stop_leaf)) break;   // no lane stopped at a leaf: walks done or paused
+            if (stop_leaf) {
                 const float4 B = nodes4[2 * ni + 1];
                 const uint32_t fc = __float_as_uint(B.w) & 0x7fffffffu, first = fc >> 4;
                 const float4 s0 = leaf4[first], s1 = leaf4[first + 1], s2 = leaf4[first + 2], s3 = leaf4[first + 3];
@@ -644,6 +653,7 @@ __device__ __forceinline__ void walk_escape(const rt::TraceParams& P, const floa
         }
     }
 #endif
+    return r.ni == END;
 }
 
 // Escape-link walk over compact 16-B nodes (BvhNode16): one ds_read_b128 per visit; the binary16
@@ -848,6 +858,7 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
     uint32_t n_seg = 0, n_smp = 0, n_box = 0, n_sph = 0;
     unsigned long long wave_iters = 0;
     bool saw_dry = false;
+    bool walking = false;   // RT_WALK_CAP: this lane's walk is paused mid-tree (r holds its state)
     // launch telemetry (3 atomics per wave): first start, pixel queue dry, last exit
     if (lane == 0) atomicMin(&P.counters->t_first, __builtin_amdgcn_s_memrealtime());
     STAMP_DECL;
@@ -880,6 +891,7 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
                     if ((held >> lane) & 1ull) {
                         pool_put(pool, cap, base + __popcll(held & ((1ull << lane) - 1ull)), st, ps, r);
                         st = ST_RETIRED;
+                        walking = false;   // a paused walk restarts from its ray where it lands
                     }
                     __threadfence_block();   // slots written before the count publishes them
                     if (int(lane) == leader) {
@@ -936,16 +948,18 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
         }
         if (COUNT && lane == 0) atomicAdd(&P.counters->lane_hist[__popcll(tracing)], 1ull);
         STAMP(1);
-        if (st == ST_TRACING) setup_ray(P, r, n_sph);
+        if (st == ST_TRACING && !walking) setup_ray(P, r, n_sph);
         STAMP(2);
         const uint32_t box0 = n_box;
+        bool walked = true;   // walk finished this iteration (RT_WALK_CAP may pause it)
         if (st == ST_TRACING) {
             if (NODE16)
                 walk_escape16<COUNT>(P, reinterpret_cast<const uint4*>(nodes4), leaf4, leaf_ids, r, n_box, n_sph);
             else
-                walk_escape<COUNT, LAYOUT>(P, LAYOUT == 2 ? nodes4 + octant(r.d) * 2u * P.n_nodes : nodes4,
-                                           leaf4, leaf_ids, r, n_box, n_sph);
+                walked = walk_escape<COUNT, LAYOUT>(P, LAYOUT == 2 ? nodes4 + octant(r.d) * 2u * P.n_nodes : nodes4,
+                                                    leaf4, leaf_ids, r, n_box, n_sph);
         }
+        walking = RT_WALK_CAP && st == ST_TRACING && !walked;
         if (COUNT && st == ST_TRACING) {   // walk-length histogram (diagnostic, COUNT builds only)
             const uint32_t len = min(n_box - box0, 63u);
             atomicAdd(&P.counters->walk_hist[r.bi != 0xffffffffu ? 1 : 0][len], 1ull);
@@ -956,7 +970,7 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
             if (lane == 0) wave_iters += m;
         }
         STAMP(3);
-        if (st == ST_TRACING) {
+        if (st == ST_TRACING && !walking) {
             n_seg++;
             ps.segs++;
             if (!shade(P, geom4, mat4, ps, r.bi, r.best, r.o, r.d)) st = ST_NEED_SAMPLE;

@@ -13,7 +13,8 @@ import sys
 from pathlib import Path
 
 
-def per_dispatch(d, counter, match="rt_trace", exclude="true>"):
+def per_dispatch(d, counter, match="rt_trace_lbvh_kernel", exclude="<true, true"):
+    """Production launches only: the instrumented (COUNT) build is <LDS=true, COUNT=true, ...>."""
     vals = []
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
