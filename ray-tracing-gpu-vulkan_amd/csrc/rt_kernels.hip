@@ -435,6 +435,13 @@ __device__ __forceinline__ bool node_hit(const float4 A, const float4 B, const R
     return tn <= tf && tn <= limit;
 }
 
+// 16-B load from an LDS address held in a register (ds_read_b128 addr, no base add).
+typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 lds_f4(uint32_t addr) {
+    const f4v v = *(const __attribute__((address_space(3))) f4v*)(uintptr_t)addr;
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
 // Octant of a direction: bit k set when component k is negative (sign bit, so -0 -> 1/d = -inf
 // counts as negative, matching the copy whose near plane is the box's high side).
 __device__ __forceinline__ uint32_t octant(const V3 d) {
@@ -578,11 +585,8 @@ __device__ __forceinline__ void walk_ordered(const rt::TraceParams& P, const flo
 // The whole escape-link walk of one segment. LAYOUT: 0 = BvhNode pairs (global memory), 1 = AB
 // layout (LDS), 2 = AB layout specialised to the ray's octant (LDS, `nodes4` already offset to the
 // ray's copy).
-#ifndef RT_WALK_CAP
-#define RT_WALK_CAP 0   // node visits per lane per segment-loop iteration (0: walk to the end)
-#endif
 template <bool COUNT, int LAYOUT>
-__device__ __forceinline__ bool walk_escape(const rt::TraceParams& P, const float4* __restrict__ nodes4,
+__device__ __forceinline__ void walk_escape(const rt::TraceParams& P, const float4* __restrict__ nodes4,
                                             const float4* __restrict__ leaf4,
                                             const uint32_t* __restrict__ leaf_ids, Ray& r,
                                             uint32_t& n_box, uint32_t& n_sph) {
@@ -616,44 +620,37 @@ __device__ __forceinline__ bool walk_escape(const rt::TraceParams& P, const floa
             pending = 0u;
         }
     } else {
-        // AB layout: B.z = escape, B.w = next index when the box is hit (inner node) or, with
-        // bit 31 set, the leaf field. A lane leaves the inner loop AT a hit leaf (r.ni stays
-        // on it), so the loop carries no pending register; the leaf's field is re-read after.
-        // RT_WALK_CAP: a lane walks at most that many nodes per segment-loop iteration and
-        // resumes from r.ni in the next one, so one long walk does not hold the whole wave.
-        uint32_t budget = RT_WALK_CAP ? RT_WALK_CAP : 0xffffffffu;
+        // AB layout (staged in LDS by the kernel, see rt_trace_lbvh_kernel): links are LDS
+        // addresses of the node, so a visit needs no address arithmetic;
+        // B.z = link when the box is missed, B.w = link when it is hit: the next node (inner
+        // node) or, bit 31 set, a leaf word (escape node | leaf index | count - 1). END and leaf
+        // words are negative, so `continue` is one sign test. A lane leaves the inner loop at a
+        // hit leaf holding its leaf word; the leaves are tested together after the loop.
+        typedef const __attribute__((address_space(3))) float4* LdsF4;
+        const uint32_t nbase = uint32_t(reinterpret_cast<uintptr_t>((LdsF4)nodes4));   // LDS address of node 0
+        uint32_t ni = r.ni == END ? END : nbase + (LAYOUT == 2 ? octant(r.d) * P.n_nodes * 32u : 0u);
         for (;;) {
-            uint32_t ni = r.ni;
-            bool go = ni != END && budget != 0u, stop_leaf = false;
-            while (go) {
-                const float4 A = nodes4[2 * ni];
-                const float4 B = nodes4[2 * ni + 1];
+            while (int32_t(ni) >= 0) {
+                const float4 A = lds_f4(ni);         // links are LDS addresses:
+                const float4 B = lds_f4(ni + 16u);   // no address arithmetic per visit
                 if (COUNT) n_box++;
-                if (RT_WALK_CAP) budget--;
                 const bool hit = node_hit<LAYOUT == 2>(A, B, q, r.limit);
-                const uint32_t link = __float_as_uint(B.w);
-                const bool at_leaf = hit && int32_t(link) < 0;   // stop here, test the leaf below
-                const uint32_t nxt = hit ? link : __float_as_uint(B.z);
-                ni = at_leaf ? ni : nxt;
-                stop_leaf = at_leaf;
-                go = !at_leaf && nxt != END && (!RT_WALK_CAP || budget != 0u);
+                ni = __float_as_uint(hit ? B.w : B.z);
             }
-            r.ni = ni;
-            if (!RT_WALK_CAP) stop_leaf = ni != END;
-            if (!__ballot(stop_leaf)) break;   // no lane stopped at a leaf: walks done or paused
-            if (stop_leaf) {
-                const float4 B = nodes4[2 * ni + 1];
-                const uint32_t fc = __float_as_uint(B.w) & 0x7fffffffu, first = fc >> 4;
+            const bool at_leaf = ni != END;
+            if (!__ballot(at_leaf)) break;   // no lane stopped at a leaf: all walks done
+            if (at_leaf) {
+                const uint32_t first = ((ni >> 2) & 1023u) * 4u, esc = (ni >> 12) & 0x7ffffu;
                 const float4 s0 = leaf4[first], s1 = leaf4[first + 1], s2 = leaf4[first + 2], s3 = leaf4[first + 3];
                 test4(s0, s1, s2, s3, [&](uint32_t k) { return leaf_ids[first + k]; }, r.o, r.d, r.inv, r.a,
                       r.best, r.bi, r.limit, P.cull_abs, P.cull_rel);
-                if (COUNT) n_sph += fc & 15u;
-                r.ni = __float_as_uint(B.z);
+                if (COUNT) n_sph += (ni & 3u) + 1u;
+                ni = esc == 0x7ffffu ? END : nbase + esc * 32u;
             }
         }
+        r.ni = END;
     }
 #endif
-    return r.ni == END;
 }
 
 // Escape-link walk over compact 16-B nodes (BvhNode16): one ds_read_b128 per visit; the binary16
@@ -858,7 +855,6 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
     uint32_t n_seg = 0, n_smp = 0, n_box = 0, n_sph = 0;
     unsigned long long wave_iters = 0;
     bool saw_dry = false;
-    bool walking = false;   // RT_WALK_CAP: this lane's walk is paused mid-tree (r holds its state)
     // launch telemetry (3 atomics per wave): first start, pixel queue dry, last exit
     if (lane == 0) atomicMin(&P.counters->t_first, __builtin_amdgcn_s_memrealtime());
     STAMP_DECL;
@@ -891,7 +887,6 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
                     if ((held >> lane) & 1ull) {
                         pool_put(pool, cap, base + __popcll(held & ((1ull << lane) - 1ull)), st, ps, r);
                         st = ST_RETIRED;
-                        walking = false;   // a paused walk restarts from its ray where it lands
                     }
                     __threadfence_block();   // slots written before the count publishes them
                     if (int(lane) == leader) {
@@ -948,18 +943,15 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
         }
         if (COUNT && lane == 0) atomicAdd(&P.counters->lane_hist[__popcll(tracing)], 1ull);
         STAMP(1);
-        if (st == ST_TRACING && !walking) setup_ray(P, r, n_sph);
+        if (st == ST_TRACING) setup_ray(P, r, n_sph);
         STAMP(2);
         const uint32_t box0 = n_box;
-        bool walked = true;   // walk finished this iteration (RT_WALK_CAP may pause it)
         if (st == ST_TRACING) {
             if (NODE16)
                 walk_escape16<COUNT>(P, reinterpret_cast<const uint4*>(nodes4), leaf4, leaf_ids, r, n_box, n_sph);
             else
-                walked = walk_escape<COUNT, LAYOUT>(P, LAYOUT == 2 ? nodes4 + octant(r.d) * 2u * P.n_nodes : nodes4,
-                                                    leaf4, leaf_ids, r, n_box, n_sph);
+                walk_escape<COUNT, LAYOUT>(P, nodes4, leaf4, leaf_ids, r, n_box, n_sph);
         }
-        walking = RT_WALK_CAP && st == ST_TRACING && !walked;
         if (COUNT && st == ST_TRACING) {   // walk-length histogram (diagnostic, COUNT builds only)
             const uint32_t len = min(n_box - box0, 63u);
             atomicAdd(&P.counters->walk_hist[r.bi != 0xffffffffu ? 1 : 0][len], 1ull);
@@ -970,7 +962,7 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
             if (lane == 0) wave_iters += m;
         }
         STAMP(3);
-        if (st == ST_TRACING && !walking) {
+        if (st == ST_TRACING) {
             n_seg++;
             ps.segs++;
             if (!shade(P, geom4, mat4, ps, r.bi, r.best, r.o, r.d)) st = ST_NEED_SAMPLE;
@@ -1013,22 +1005,28 @@ __global__ __launch_bounds__(BLOCK, RT_TRACE_WAVES_PER_SIMD) void rt_trace_lbvh_
         if (NODE16) {
             for (uint32_t i = threadIdx.x; i < n_node4; i += BLOCK) lds[i] = nodes4[i];
         } else {
+            typedef const __attribute__((address_space(3))) float4* LdsF4;
+            const uint32_t lbase = uint32_t(reinterpret_cast<uintptr_t>((LdsF4)lds));   // LDS address of lds[0]
             for (uint32_t i = threadIdx.x; i < P.n_nodes; i += BLOCK) {
                 const float4 lo = nodes4[2 * i], hi = nodes4[2 * i + 1];   // BvhNode: lo.xyz esc, hi.xyz leaf
-                // B.w: inner node -> i + 1 (next on hit), leaf -> 0x80000000 | first << 4 | count
-                const uint32_t fc = __float_as_uint(hi.w);
-                const float link = __uint_as_float(fc ? (fc | 0x80000000u) : i + 1u);
-                if (!OCT) {
-                    lds[2 * i] = make_float4(lo.x, lo.y, hi.x, hi.y);
-                    lds[2 * i + 1] = make_float4(lo.z, hi.z, lo.w, link);
-                } else {
+                // Links (walk_escape, AB layout): LDS address of the target node in this copy,
+                // END = ~0; a hit leaf yields 0x80000000 | escape node << 12 |
+                // leaf index << 2 | (count - 1), escape node = 0x7ffff for END. (Trees staged in
+                // LDS have < 2^14 nodes and < 1024 leaves of <= 4 slots, checked by the host.)
+                const uint32_t esc = __float_as_uint(lo.w), fc = __float_as_uint(hi.w);
 #pragma unroll
-                    for (uint32_t o = 0; o < 8; ++o) {   // bit k of o: axis k runs negative, near = hi
-                        const bool nx = o & 1u, ny = o & 2u, nz = o & 4u;
-                        const size_t b = (size_t(o) * P.n_nodes + i) * 2u;
-                        lds[b] = make_float4(nx ? hi.x : lo.x, ny ? hi.y : lo.y, nx ? lo.x : hi.x, ny ? lo.y : hi.y);
-                        lds[b + 1] = make_float4(nz ? hi.z : lo.z, nz ? lo.z : hi.z, lo.w, link);
-                    }
+                for (uint32_t o = 0; o < (OCT ? 8u : 1u); ++o) {   // bit k of o: axis k runs negative, near = hi
+                    const bool nx = o & 1u, ny = o & 2u, nz = o & 4u;
+                    const uint32_t cb = o * P.n_nodes;   // first node of copy o
+                    const uint32_t miss = esc == END ? END : lbase + (cb + esc) * 32u;
+                    // (kept as separate statements: one combined expression crashed the ROCm 7.2
+                    // instruction selector)
+                    const uint32_t escf = esc == END ? 0x7ffffu : cb + esc;
+                    const uint32_t leafw = 0x80000000u + (escf << 12) + ((fc >> 6) << 2) + ((fc - 1u) & 3u);
+                    const uint32_t hit = fc ? leafw : lbase + (cb + i + 1u) * 32u;
+                    const size_t b = size_t(cb + i) * 2u;
+                    lds[b] = make_float4(nx ? hi.x : lo.x, ny ? hi.y : lo.y, nx ? lo.x : hi.x, ny ? lo.y : hi.y);
+                    lds[b + 1] = make_float4(nz ? hi.z : lo.z, nz ? lo.z : hi.z, __uint_as_float(miss), __uint_as_float(hit));
                 }
             }
         }
