@@ -298,10 +298,21 @@ __device__ __forceinline__ bool start_sample(const rt::TraceParams& P, const Cam
     uy = uy / P.size_y;
     const float lxr = rnd_pm1(ps.seed);
     const float lyr = rnd_pm1(ps.seed);
-    const float l2 = __builtin_sqrtf(__builtin_fmaf(lyr, lyr, lxr * lxr));
-    const float il = 1.0f / l2;
-    const float rx = P.half_aperture * (lxr * il);
-    const float ry = P.half_aperture * (lyr * il);
+    float rx, ry;
+    if (P.half_aperture != 0.0f) {   // wave-uniform (launch parameter)
+        const float l2 = __builtin_sqrtf(__builtin_fmaf(lyr, lyr, lxr * lxr));
+        const float il = 1.0f / l2;
+        rx = P.half_aperture * (lxr * il);
+        ry = P.half_aperture * (lyr * il);
+    } else {
+        // Pinhole (the reference camera, aperture 0): the same values without the sqrt and the
+        // divide. lxr * il has the sign of lxr (il = 1/l2 > 0), so 0 * it is a zero of sign
+        // sign(aperture) ^ sign(lxr); when lxr = lyr = 0 exactly, il = inf and 0 * (0 * inf) = NaN.
+        const bool nan = lxr == 0.0f && lyr == 0.0f;
+        const uint32_t sa = __float_as_uint(P.half_aperture) & 0x80000000u;
+        rx = nan ? __builtin_nanf("") : __uint_as_float(sa ^ (__float_as_uint(lxr) & 0x80000000u));
+        ry = nan ? __builtin_nanf("") : __uint_as_float(sa ^ (__float_as_uint(lyr) & 0x80000000u));
+    }
     const V3 from = add(cam.lf, add(scale(rx, cam.crt), scale(ry, cam.cup)));
     const V3 to = sub(add(cam.ulc, scale(ux, cam.hor)), scale(uy, cam.ver));
     o = from;
@@ -342,12 +353,16 @@ __device__ __forceinline__ bool shade(const rt::TraceParams& P, const float4* __
             const float sines = sinf_det(6.0f * p.x) * sinf_det(6.0f * p.y) * sinf_det(6.0f * p.z);
             if (!(sines > 0.0f)) att = v3(m1.x, m1.y, m1.z);
         }
+        // diffuse and metal both draw one random unit vector first (shader.rchit:69, :80): one
+        // copy of that code serves a wave holding both materials
+        V3 ru = v3(0.0f, 0.0f, 0.0f);
+        if (mtype < 2u) ru = random_unit_vector(ps.seed);
         if (mtype == 0u) {                       // diffuse, shader.rchit:68-76
-            sd = add(n, random_unit_vector(ps.seed));
+            sd = add(n, ru);
             if (fabsf(sd.x) < 1e-8f && fabsf(sd.y) < 1e-8f && fabsf(sd.z) < 1e-8f) sd = n;
         } else if (mtype == 1u) {                // metal, shader.rchit:78-89
             const V3 refl = reflect(d, n);
-            const V3 fuzz = scale(m0.w, random_unit_vector(ps.seed));
+            const V3 fuzz = scale(m0.w, ru);
             const V3 sc = normalize(add(refl, fuzz));
             if (dot(sc, n) > 0.0f) sd = sc;
         } else if (mtype == 2u) {                // dielectric, shader.rchit:91-100,125-133
