@@ -44,9 +44,10 @@ struct rt_context {
     std::vector<void*> scene_allocs;
     rt::Counters* counters = nullptr;   // device
     hipStream_t last_stream = nullptr;
-    // occupancy cache per kernel (accel id 1..5) and count flag, valid for occ_lds bytes of LDS
-    int occ[8][2] = {};
-    size_t occ_lds[8][2] = {};
+    // occupancy cache per kernel (accel id < kAccelIds) and count flag, valid for occ_lds bytes
+    static constexpr uint32_t kAccelIds = 16;
+    int occ[kAccelIds][2] = {};
+    size_t occ_lds[kAccelIds][2] = {};
     size_t lds_bytes = 0;                        // LBVH_LDS staging size of the current scene
     size_t lds2_bytes = 0;                       // LBVH2_LDS staging size (0: does not fit)
     size_t lds16_bytes = 0;                      // compact-node LBVH staging size (0: not used)
@@ -727,6 +728,7 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     // first-time stamps start at the maximum (atomicMin); 0xff bytes = ~0ull
     RT_HIP(hipMemsetAsync(&ctx->counters->t_first, 0xff, 2 * sizeof(unsigned long long), st));
     const int ci = count ? 1 : 0;
+    static_assert(rt::ACCEL_LBVH_OCT < rt_context::kAccelIds, "occupancy cache too small for the accel ids");
     if (ctx->occ_lds[accel][ci] != lds) {
         int b = 0;
         RT_HIP(rt::trace_occupancy(accel, count, lds, &b));

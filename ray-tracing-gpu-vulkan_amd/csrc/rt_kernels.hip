@@ -432,13 +432,13 @@ __device__ __forceinline__ RayBox ray_box(const V3 o, const V3 inv) {
     return RayBox{n, v3(o.x * n.x, o.y * n.y, o.z * n.z)};
 }
 
-template <bool OCT>
+template <uint32_t NOCT>   // node copies per ray direction class: 1 (none) or 8 (octants)
 __device__ __forceinline__ bool node_hit(const float4 A, const float4 B, const RayBox& q, float limit) {
     const float tx0 = __builtin_fmaf(A.x, q.inv.x, -q.oi.x), ty0 = __builtin_fmaf(A.y, q.inv.y, -q.oi.y);
     const float tx1 = __builtin_fmaf(A.z, q.inv.x, -q.oi.x), ty1 = __builtin_fmaf(A.w, q.inv.y, -q.oi.y);
     const float tz0 = __builtin_fmaf(B.x, q.inv.z, -q.oi.z), tz1 = __builtin_fmaf(B.y, q.inv.z, -q.oi.z);
     float tn, tf;
-    if (OCT) {
+    if (NOCT == 8) {
         tn = fmaxf(fmaxf(tx0, ty0), fmaxf(tz0, T_MIN));
         tf = fminf(fminf(tx1, ty1), tz1);
     } else {
@@ -509,7 +509,7 @@ __device__ __forceinline__ void visit_node(const rt::TraceParams& P, const float
     const float4 n0 = nodes4[2 * r.ni];
     const float4 n1 = nodes4[2 * r.ni + 1];
     if (COUNT) n_box++;
-    const bool hit = node_hit<false>(make_float4(n0.x, n0.y, n1.x, n1.y), make_float4(n0.z, n1.z, 0.0f, 0.0f),
+    const bool hit = node_hit<1>(make_float4(n0.x, n0.y, n1.x, n1.y), make_float4(n0.z, n1.z, 0.0f, 0.0f),
                                      ray_box(r.o, r.inv), r.limit);
     const uint32_t fc = __float_as_uint(n1.w);
     if (hit && fc != 0u) {   // leaf: always 4 slots (dummy-padded), loads issued together
@@ -598,8 +598,7 @@ __device__ __forceinline__ void walk_ordered(const rt::TraceParams& P, const flo
 }
 
 // The whole escape-link walk of one segment. LAYOUT: 0 = BvhNode pairs (global memory), 1 = AB
-// layout (LDS), 2 = AB layout specialised to the ray's octant (LDS, `nodes4` already offset to the
-// ray's copy).
+// layout (LDS), 2 = AB layout with one node copy per ray direction octant.
 template <bool COUNT, int LAYOUT>
 __device__ __forceinline__ void walk_escape(const rt::TraceParams& P, const float4* __restrict__ nodes4,
                                             const float4* __restrict__ leaf4,
@@ -620,7 +619,7 @@ __device__ __forceinline__ void walk_escape(const rt::TraceParams& P, const floa
                 const float4 n0 = nodes4[2 * r.ni];
                 const float4 n1 = nodes4[2 * r.ni + 1];
                 if (COUNT) n_box++;
-                const bool hit = node_hit<false>(make_float4(n0.x, n0.y, n1.x, n1.y),
+                const bool hit = node_hit<1>(make_float4(n0.x, n0.y, n1.x, n1.y),
                                                  make_float4(n0.z, n1.z, 0.0f, 0.0f), q, r.limit);
                 const uint32_t fc = __float_as_uint(n1.w);
                 if (hit && fc != 0u) pending = fc;
@@ -649,7 +648,7 @@ __device__ __forceinline__ void walk_escape(const rt::TraceParams& P, const floa
                 const float4 A = lds_f4(ni);         // links are LDS addresses:
                 const float4 B = lds_f4(ni + 16u);   // no address arithmetic per visit
                 if (COUNT) n_box++;
-                const bool hit = node_hit<LAYOUT == 2>(A, B, q, r.limit);
+                const bool hit = node_hit<LAYOUT == 2 ? 8u : 1u>(A, B, q, r.limit);
                 ni = __float_as_uint(hit ? B.w : B.z);
             }
             const bool at_leaf = ni != END;
@@ -1003,7 +1002,7 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
 // BLOCK threads share one staged copy. Staged nodes use the AB layout (node_hit); OCT stages 8
 // copies, one per ray direction octant. POOL: the tail-compaction pool (BLOCK slots x
 // kPoolFields words) follows the staged data.
-template <bool LDS, bool COUNT, bool NODE16, bool SCENE_LDS, bool POOL, bool OCT, uint32_t BLOCK>
+template <bool LDS, bool COUNT, bool NODE16, bool SCENE_LDS, bool POOL, uint32_t NOCT, uint32_t BLOCK>
 __global__ __launch_bounds__(BLOCK, RT_TRACE_WAVES_PER_SIMD) void rt_trace_lbvh_kernel(const rt::TraceParams P) {
     extern __shared__ float4 lds[];
     __shared__ PoolCtl ctl;
@@ -1015,7 +1014,7 @@ __global__ __launch_bounds__(BLOCK, RT_TRACE_WAVES_PER_SIMD) void rt_trace_lbvh_
     const float4* mat4 = reinterpret_cast<const float4*>(P.mat);
     uint32_t staged4 = 0;
     if (LDS) {
-        const uint32_t n_node4 = (NODE16 ? 1u : (OCT ? 16u : 2u)) * P.n_nodes, n_leaf4 = P.n_leaf,
+        const uint32_t n_node4 = (NODE16 ? 1u : 2u * NOCT) * P.n_nodes, n_leaf4 = P.n_leaf,
                        n_id4 = (P.n_leaf + 3u) / 4u;
         if (NODE16) {
             for (uint32_t i = threadIdx.x; i < n_node4; i += BLOCK) lds[i] = nodes4[i];
@@ -1030,7 +1029,7 @@ __global__ __launch_bounds__(BLOCK, RT_TRACE_WAVES_PER_SIMD) void rt_trace_lbvh_
                 // LDS have < 2^14 nodes and < 1024 leaves of <= 4 slots, checked by the host.)
                 const uint32_t esc = __float_as_uint(lo.w), fc = __float_as_uint(hi.w);
 #pragma unroll
-                for (uint32_t o = 0; o < (OCT ? 8u : 1u); ++o) {   // bit k of o: axis k runs negative, near = hi
+                for (uint32_t o = 0; o < NOCT; ++o) {   // bit k of o: axis k runs negative, near = hi
                     const bool nx = o & 1u, ny = o & 2u, nz = o & 4u;
                     const uint32_t cb = o * P.n_nodes;   // first node of copy o
                     const uint32_t miss = esc == END ? END : lbase + (cb + esc) * 32u;
@@ -1073,7 +1072,7 @@ __global__ __launch_bounds__(BLOCK, RT_TRACE_WAVES_PER_SIMD) void rt_trace_lbvh_
         ctl.pad = 0u;
     }
     if (LDS || POOL) __syncthreads();
-    lbvh_classic<COUNT, NODE16, POOL, (LDS && !NODE16) ? (OCT ? 2 : 1) : 0>(
+    lbvh_classic<COUNT, NODE16, POOL, (LDS && !NODE16) ? (NOCT == 8 ? 2 : 1) : 0>(
         P, nodes4, leaf4, leaf_ids, geom4, mat4, &ctl, reinterpret_cast<uint32_t*>(lds + staged4), BLOCK);
 }
 
@@ -1203,9 +1202,9 @@ constexpr uint32_t kLbvhBlock = RT_LBVH_BLOCK;
 #endif
 constexpr uint32_t kPoolBlock = RT_POOL_BLOCK;   // one block per CU: the pool spans all 16 waves
 
-#define RT_LBVH_FN(L, C, N16, S) reinterpret_cast<const void*>(rt_trace_lbvh_kernel<L, C, N16, S, false, false, kLbvhBlock>)
-#define RT_POOL_FN(C) reinterpret_cast<const void*>(rt_trace_lbvh_kernel<true, C, false, true, true, false, kPoolBlock>)
-#define RT_OCT_FN(C) reinterpret_cast<const void*>(rt_trace_lbvh_kernel<true, C, false, true, false, true, kPoolBlock>)
+#define RT_LBVH_FN(L, C, N16, S) reinterpret_cast<const void*>(rt_trace_lbvh_kernel<L, C, N16, S, false, 1u, kLbvhBlock>)
+#define RT_POOL_FN(C) reinterpret_cast<const void*>(rt_trace_lbvh_kernel<true, C, false, true, true, 1u, kPoolBlock>)
+#define RT_OCT_FN(C) reinterpret_cast<const void*>(rt_trace_lbvh_kernel<true, C, false, true, false, 8u, kPoolBlock>)
 static const void* pick(uint32_t accel, bool count) {
     switch (accel) {
         case ACCEL_BRUTE:
