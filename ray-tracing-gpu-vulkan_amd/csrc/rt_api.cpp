@@ -122,6 +122,47 @@ void pad_nodes(const std::vector<rt::BvhNode>& in, std::vector<rt::BvhNode>& out
         n.l1x -= pad; n.l1y -= pad; n.l1z -= pad; n.h1x += pad; n.h1y += pad; n.h1z += pad;
     }
 }
+
+// Eight re-orderings of an escape-link tree, one per ray direction octant (bit k of the octant:
+// axis k runs negative): each copy lists the nearer child of every inner node first, "nearer"
+// meaning lower along the axis that best separates the two child boxes when the octant runs
+// positive on it (higher when negative). The walk of a ray then reaches close spheres early, so
+// its cull limit shrinks sooner. Escape links are re-derived per copy; leaves keep their slots.
+void make_octant_orders(const std::vector<rt::BvhNode>& n, std::vector<rt::BvhNode>& out) {
+    const uint32_t N = uint32_t(n.size());
+    out.assign(size_t(8) * N, rt::BvhNode{});
+    if (N == 0) return;
+    std::vector<uint32_t> size(N, 1);   // nodes in the subtree rooted at i (children follow i)
+    for (uint32_t i = N; i-- > 0;)
+        if (n[i].first_count == 0) size[i] = 1 + size[i + 1] + size[n[i + 1].escape];
+    for (uint32_t o = 0; o < 8; ++o) {
+        rt::BvhNode* dst = out.data() + size_t(o) * N;
+        uint32_t next = 0;
+        // (node, escape in the new order), depth-first
+        std::vector<std::pair<uint32_t, uint32_t>> stack{{0u, 0xffffffffu}};
+        while (!stack.empty()) {
+            const auto [i, esc] = stack.back();
+            stack.pop_back();
+            const uint32_t at = next++;
+            dst[at] = n[i];
+            dst[at].escape = esc;
+            if (n[i].first_count != 0) continue;
+            const uint32_t L = i + 1, R = n[L].escape;
+            float best = -1.0f;
+            int axis = 0;
+            const float cl[3] = {n[L].lox + n[L].hix, n[L].loy + n[L].hiy, n[L].loz + n[L].hiz};
+            const float cr[3] = {n[R].lox + n[R].hix, n[R].loy + n[R].hiy, n[R].loz + n[R].hiz};
+            for (int k = 0; k < 3; ++k)
+                if (std::fabs(cl[k] - cr[k]) > best) { best = std::fabs(cl[k] - cr[k]); axis = k; }
+            const bool neg = (o >> axis) & 1u;
+            const bool l_first = neg ? cl[axis] >= cr[axis] : cl[axis] <= cr[axis];
+            const uint32_t a = l_first ? L : R, b = l_first ? R : L;
+            // a is emitted at `at + 1`, b right after a's subtree; b inherits this node's escape
+            stack.push_back({b, esc});
+            stack.push_back({a, at + 1 + size[a]});
+        }
+    }
+}
 }  // namespace
 
 // LBVH staged in LDS when its image is at most this large.
@@ -343,7 +384,7 @@ int rt_context_create(int device, rt_context** out) {
     RT_HIP(hipMalloc(&c, sizeof(rt::Counters)));
     RT_HIP(hipMemset(c, 0, sizeof(rt::Counters)));
     ctx->counters = static_cast<rt::Counters*>(c);
-    for (int a = 0; a < 8; a++)
+    for (uint32_t a = 0; a < rt_context::kAccelIds; a++)
         for (int cnt = 0; cnt < 2; cnt++) ctx->occ_lds[a][cnt] = ~size_t(0);
     *out = ctx.release();
     return RT_OK;
@@ -416,6 +457,9 @@ int set_scene_host(rt_context* ctx, const Sphere* spheres, uint32_t count, hipSt
         ctx->nodes_host = bvh.nodes;
         ctx->nodes2_host = bvh.nodes2;
         pad_nodes(ctx->nodes_host, bvh.nodes, ctx->nodes2_host, bvh.nodes2, pad_for(ctx->pad_radius));
+        std::vector<rt::BvhNode> oct;
+        make_octant_orders(bvh.nodes, oct);
+        if (int rc = upload(ctx, oct, &d.nodes_oct, st)) return rc;
         const size_t lds = size_t(2 * d.n_nodes + d.n_leaf + (d.n_leaf + 3) / 4) * 16;
         ctx->lds_bytes = (d.n_nodes && lds <= kMaxLdsBvhBytes) ? lds : 0;
         const size_t lds_scene = lds + size_t(count) * 48u;
@@ -659,6 +703,7 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     P.nodes = d.n_nodes ? d.nodes : nullptr;
     P.n_nodes = d.n_nodes;
     P.nodes16 = d.nodes16;
+    P.nodes_oct = d.nodes_oct;
     P.nodes2 = d.nodes2;   // null when the tree is a single leaf (root2 is then a leaf reference)
     P.n_nodes2 = d.n_nodes2;
     P.root2 = d.root2;
@@ -698,6 +743,11 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
             pad_nodes(ctx->nodes_host, n1, ctx->nodes2_host, n2, pad_for(ctx->pad_radius));
             RT_HIP(hipStreamSynchronize(st));
             if (!n1.empty()) RT_HIP(hipMemcpy(d.nodes, n1.data(), n1.size() * sizeof(n1[0]), hipMemcpyHostToDevice));
+            if (d.nodes_oct) {
+                std::vector<rt::BvhNode> oct;
+                make_octant_orders(n1, oct);
+                RT_HIP(hipMemcpy(d.nodes_oct, oct.data(), oct.size() * sizeof(oct[0]), hipMemcpyHostToDevice));
+            }
             if (!n2.empty()) RT_HIP(hipMemcpy(d.nodes2, n2.data(), n2.size() * sizeof(n2[0]), hipMemcpyHostToDevice));
             std::vector<rt::BvhNode16> n16;
             if (d.nodes16) {

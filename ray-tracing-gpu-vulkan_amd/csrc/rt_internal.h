@@ -70,6 +70,8 @@ struct DeviceScene {
     uint32_t* leaf_ids = nullptr;  // original index of each leaf slot
     uint32_t n_leaf = 0;
     BvhNode16* nodes16 = nullptr;  // compact escape-link nodes (null when the tree is too big)
+    BvhNode* nodes_oct = nullptr;  // host-built trees: 8 x n_nodes, one near-child-first order per
+                                   // ray octant (null: every octant copy uses `nodes`' order)
     Bvh2Node* nodes2 = nullptr;    // ordered-walk layout (same leaves)
     uint32_t n_nodes2 = 0;
     uint32_t root2 = 0;            // root reference (inner index or leaf reference)
@@ -127,6 +129,7 @@ struct TraceParams {
     const BvhNode* nodes;
     uint32_t n_nodes;
     const BvhNode16* nodes16;
+    const BvhNode* nodes_oct;      // optional, see DeviceScene
     const Bvh2Node* nodes2;
     uint32_t n_nodes2, root2, stack_depth;
     uint32_t n_leaf;               // spheres in the tree (leaf slots)

@@ -1021,15 +1021,20 @@ __global__ __launch_bounds__(BLOCK, RT_TRACE_WAVES_PER_SIMD) void rt_trace_lbvh_
         } else {
             typedef const __attribute__((address_space(3))) float4* LdsF4;
             const uint32_t lbase = uint32_t(reinterpret_cast<uintptr_t>((LdsF4)lds));   // LDS address of lds[0]
-            for (uint32_t i = threadIdx.x; i < P.n_nodes; i += BLOCK) {
-                const float4 lo = nodes4[2 * i], hi = nodes4[2 * i + 1];   // BvhNode: lo.xyz esc, hi.xyz leaf
+            for (uint32_t oi = threadIdx.x; oi < NOCT * P.n_nodes; oi += BLOCK) {
+                const uint32_t o = oi / P.n_nodes, i = oi - o * P.n_nodes;   // copy o, node i
+                // BvhNode: lo.xyz escape, hi.xyz leaf. Octant copies come in their own
+                // near-child-first order when the host provides one (escape links per copy).
+                const float4* src = (NOCT == 8 && P.nodes_oct)
+                                        ? reinterpret_cast<const float4*>(P.nodes_oct + size_t(o) * P.n_nodes)
+                                        : nodes4;
+                const float4 lo = src[2 * i], hi = src[2 * i + 1];
                 // Links (walk_escape, AB layout): LDS address of the target node in this copy,
                 // END = ~0; a hit leaf yields 0x80000000 | escape node << 12 |
                 // leaf index << 2 | (count - 1), escape node = 0x7ffff for END. (Trees staged in
                 // LDS have < 2^14 nodes and < 1024 leaves of <= 4 slots, checked by the host.)
                 const uint32_t esc = __float_as_uint(lo.w), fc = __float_as_uint(hi.w);
-#pragma unroll
-                for (uint32_t o = 0; o < NOCT; ++o) {   // bit k of o: axis k runs negative, near = hi
+                {   // bit k of o: axis k runs negative, near = hi
                     const bool nx = o & 1u, ny = o & 2u, nz = o & 4u;
                     const uint32_t cb = o * P.n_nodes;   // first node of copy o
                     const uint32_t miss = esc == END ? END : lbase + (cb + esc) * 32u;
