@@ -94,6 +94,10 @@ def main() -> int:
     ap.add_argument("--profile", action="store_true", help="short run for rocprofv3 (no side legs)")
     ap.add_argument("--walk", type=int, default=0,
                     help="LBVH walk form (A/B only): 0 default escape-link, 2 ordered, 4 compact nodes")
+    ap.add_argument("--split", choices=["samples", "strips"], default="samples",
+                    help="N>1 work split: samples (each rank renders the frame with spp/N samples and "
+                         "stream salt number+rank, row-slice reduction) or strips (8-row strips of the "
+                         "one-GPU frame); identical at N=1")
     args = ap.parse_args()
 
     import numpy as np
@@ -102,7 +106,8 @@ def main() -> int:
 
     import rtvk
     from rtvk import abi
-    from rtvk.dist import DistributedRenderer, hip_assembler, hip_band_renderer
+    from rtvk.dist import (DistributedRenderer, SampleSplitRenderer, hip_assembler, hip_band_renderer,
+                           hip_full_renderer, hip_resolver)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -150,7 +155,20 @@ def main() -> int:
         e1.record(stream)
         ev.append((e0, e1))
 
-    dr = DistributedRenderer(W, H, dev, timed_render, hip_assembler(renderer))
+    split = args.split if world > 1 else "strips"
+    if split == "samples":
+        full_render = hip_full_renderer(renderer, rci, opts)
+
+        def timed_full(number, spp_r, accum, out):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            full_render(number, spp_r, accum, out)
+            e1.record(stream)
+            ev.append((e0, e1))
+
+        dr = SampleSplitRenderer(W, H, spp, rci.number, dev, timed_full, hip_resolver(renderer))
+    else:
+        dr = DistributedRenderer(W, H, dev, timed_render, hip_assembler(renderer))
 
     def barrier():
         torch.cuda.synchronize()
@@ -191,21 +209,25 @@ def main() -> int:
 
     # Algorithmic work of one launch on this rank, counted by the instrumented build of the same
     # kernel (identical image, same traversal; outside the timed region).
-    local_rows = len(dr.rows_np)
+    local_rows = len(dr.rows_np) if split == "strips" else (H if dr.spp_r else 0)
+    local_spp = spp if split == "strips" else dr.spp_r
     cnt_opts = rtvk.make_options(accel=accel, count_tests=True)
     cnt_opts.reserved[1] = args.walk
-    cnt_spp = max(1, min(spp, args.count_spp))
+    cnt_spp = max(1, min(local_spp, args.count_spp))
     if local_rows:
         acc = torch.zeros((local_rows, W, 4), dtype=torch.float32, device=dev)
         out = torch.zeros((local_rows, W, 4), dtype=torch.uint8, device=dev)
-        renderer.render_device(rtvk.canonical_render_call_info(cnt_spp, W, H), acc, out, rows=dr.rows,
+        crci = rtvk.canonical_render_call_info(cnt_spp, W, H)
+        if split == "samples":
+            crci.number = dr.number
+        renderer.render_device(crci, acc, out, rows=dr.rows if split == "strips" else None,
                                options=cnt_opts)
         torch.cuda.synchronize()
         cs = renderer.stats()
         del acc, out
     else:
         cs = rtvk.Stats()
-    scale = spp / cnt_spp
+    scale = local_spp / cnt_spp
     flops = (cs.box_tests * FLOP_PER_BOX_TEST + cs.sphere_tests * FLOP_PER_SPHERE_TEST) * scale
     achieved = flops / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
 
@@ -251,7 +273,9 @@ def main() -> int:
                                    + (f" (BASELINE config {args.config})" if args.config else
                                       " (BASELINE config 2 input)" if (W, H, spp, args.grid) == (1920, 1080, 100, 11) else ""),
                        "width": W, "height": H, "spp": spp, "depth": 50, "spheres": len(scene),
-                       "accel": args.accel, "parallelism": f"row-strips x{world} + rccl gather"},
+                       "accel": args.accel,
+                       "parallelism": (f"sample-split x{world} (number+rank) + rccl all-to-all row reduction "
+                                       "+ gather" if split == "samples" else f"row-strips x{world} + rccl gather")},
             "segments_per_sample": round(st.segments / max(1, st.samples), 4),
             "scene_setup_ms": round(t_scene * 1e3, 2),
             "scene_build_ms_per_step": round(sum(build_s) / max(1, len(build_s)) * 1e3, 3),

@@ -151,6 +151,16 @@ int rt_scatter_rows(rt_context* ctx, const float* src_accum, const uint8_t* src_
                     const uint32_t* rows, uint32_t n_rows, uint32_t width, float* dst_accum,
                     uint8_t* dst_rgba8, void* stream);
 
+/*
+ * Tonemap a summed accumulator to rgba8 on the device, exactly as the trace kernel's store
+ * (shader.rgen:65-66): rgba8 = round(clamp(sqrt(sum / spp), 0, 1) * 255) per channel, alpha 255.
+ * For a frame assembled from several launches (the sample-split multi-GPU frame: rank r renders
+ * spp_r samples with RenderCallInfo.number = r, the float sums are added in rank order).
+ * accum_rgba32f: n_texels float4 (DEVICE); out_rgba8: n_texels x 4 bytes (DEVICE).
+ */
+int rt_resolve_rgba8(rt_context* ctx, const float* accum_rgba32f, uint64_t n_texels, uint32_t spp,
+                     uint8_t* out_rgba8, void* stream);
+
 /* ---- host-pointer convenience ------------------------------------------------------ */
 /*
  * One frame over the full image rci[0].image_size with host buffers. rci_count bands, band i

@@ -44,6 +44,8 @@ def lib() -> ctypes.CDLL:
         l.orc_generate_scene.argtypes = [ctypes.c_float, _U, _P, _U, ctypes.POINTER(_U)]
         l.orc_render.restype = _I
         l.orc_render.argtypes = [_P, _U, _P, _P, _U, _U, _P, _P, _P, _P, _I]
+        l.orc_resolve.restype = _I
+        l.orc_resolve.argtypes = [_P, ctypes.c_uint64, _U, _P]
         _lib = l
     return _lib
 
@@ -116,3 +118,11 @@ def render(spheres, rci, band_w: int, band_h: int, rows=None, opts=None, accum=N
                          st.ctypes.data, threads if threads else (os.cpu_count() or 1))
     assert r == 0
     return acc, out, tuple(int(v) for v in st)
+
+
+def resolve(accum: np.ndarray, spp: int) -> np.ndarray:
+    """rgba8 tonemap of a summed float accumulator [h, w, 4] (checker of rt_resolve_rgba8)."""
+    a = np.ascontiguousarray(accum, np.float32)
+    out = np.zeros(a.shape[:-1] + (4,), np.uint8)
+    assert lib().orc_resolve(a.ctypes.data, a.size // 4, spp, out.ctypes.data) == 0
+    return out

@@ -547,4 +547,16 @@ int orc_render(const Sphere* spheres, uint32_t n, const RenderCallInfo* rci, con
     return 0;
 }
 
+// Tonemap of an already summed accumulator (checker of rt_resolve_rgba8): the same conversion
+// render_pixel applies to a pixel's sum (shader.rgen:65-66).
+int orc_resolve(const float* acc, uint64_t n_texels, uint32_t spp, uint8_t* out) {
+    if (!acc || !out || !spp) return 1;
+    const float fs = float(spp);
+    for (uint64_t i = 0; i < n_texels; i++) {
+        for (int c = 0; c < 3; c++) out[4 * i + c] = to_unorm8(std::sqrt(acc[4 * i + c] / fs));
+        out[4 * i + 3] = 255;
+    }
+    return 0;
+}
+
 }  // extern "C"

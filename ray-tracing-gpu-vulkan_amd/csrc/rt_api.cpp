@@ -29,6 +29,7 @@ namespace rt {
 hipError_t launch_trace(const TraceParams& P, uint32_t accel, bool count, int grid, size_t lds_bytes,
                         hipStream_t st);
 hipError_t trace_occupancy(uint32_t accel, bool count, size_t lds_bytes, int* blocks_per_cu);
+hipError_t launch_resolve(const float* accum, uint64_t n_texels, uint32_t spp, uint8_t* out, hipStream_t st);
 uint32_t block_size(uint32_t accel);
 size_t pool_bytes(uint32_t accel);
 hipError_t launch_scatter_rows(const float* src_acc, const uint8_t* src_px, const uint32_t* rows,
@@ -808,6 +809,17 @@ int rt_get_stats(rt_context* ctx, rt_stats* out) {
     out->samples = c.samples;
     out->box_tests = c.box_tests;
     out->sphere_tests = c.sphere_tests;
+    return RT_OK;
+}
+
+int rt_resolve_rgba8(rt_context* ctx, const float* accum, uint64_t n_texels, uint32_t spp, uint8_t* out,
+                     void* stream) {
+    if (!ctx) return fail(RT_ERR_INVALID_ARGUMENT, "ctx is NULL");
+    if (n_texels == 0) return RT_OK;
+    if (!accum || !out) return fail(RT_ERR_INVALID_ARGUMENT, "accum or out is NULL");
+    if (spp == 0) return fail(RT_ERR_INVALID_ARGUMENT, "spp is zero");
+    DeviceGuard g(ctx->device);
+    RT_HIP(rt::launch_resolve(accum, n_texels, spp, out, static_cast<hipStream_t>(stream)));
     return RT_OK;
 }
 

@@ -32,6 +32,9 @@ namespace {
 
 constexpr uint32_t kLeafMax = 4;
 constexpr uint32_t kBigMax = 64;
+#ifndef RT_BIG_FACTOR
+#define RT_BIG_FACTOR 2.0f   // "big" = radius above this multiple of the median (A/B knob)
+#endif
 
 inline uint32_t expand_bits(uint32_t v) {  // 10 bits -> every third bit of 30
     v = (v * 0x00010001u) & 0xFF0000FFu;
@@ -293,7 +296,7 @@ void build_lbvh_host(const Sphere* sph, uint32_t n, HostBvh& out, bool sah) {
     const float median = sorted[n / 2];
     std::vector<uint32_t> big;
     for (uint32_t i = 0; i < n; i++)
-        if (radii[i] > 2.0f * median) big.push_back(i);
+        if (radii[i] > RT_BIG_FACTOR * median) big.push_back(i);
     if (big.size() > kBigMax) {
         std::stable_sort(big.begin(), big.end(), [&](uint32_t a, uint32_t b) { return radii[a] > radii[b]; });
         big.resize(kBigMax);

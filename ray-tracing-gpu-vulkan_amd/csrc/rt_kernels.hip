@@ -957,9 +957,9 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
         }
         if (COUNT && lane == 0) atomicAdd(&P.counters->lane_hist[__popcll(tracing)], 1ull);
         STAMP(1);
+        const uint32_t box0 = n_box;
         if (st == ST_TRACING) setup_ray(P, r, n_sph);
         STAMP(2);
-        const uint32_t box0 = n_box;
         if (st == ST_TRACING) {
             if (NODE16)
                 walk_escape16<COUNT>(P, reinterpret_cast<const uint4*>(nodes4), leaf4, leaf_ids, r, n_box, n_sph);
@@ -1171,6 +1171,16 @@ __global__ __launch_bounds__(256) void rt_scatter_rows_kernel(const float4* __re
     }
 }
 
+// Tonemap of a summed accumulator (rt_resolve_rgba8): the trace kernel's pixel store, shader.rgen:65-66.
+__global__ __launch_bounds__(256) void rt_resolve_kernel(const float4* __restrict__ acc, uint64_t n,
+                                                         float spp, uint32_t* __restrict__ out) {
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
+        const float4 s = acc[i];
+        out[i] = unorm8(__builtin_sqrtf(s.x / spp)) | (unorm8(__builtin_sqrtf(s.y / spp)) << 8) |
+                 (unorm8(__builtin_sqrtf(s.z / spp)) << 16) | (255u << 24);
+    }
+}
+
 // Diagnostic: device evaluation of contract primitives (tests/test_gpu_parity.py).
 __global__ void rt_debug_math_kernel(int op, const float* __restrict__ in, float* __restrict__ out,
                                      uint32_t n) {
@@ -1272,6 +1282,14 @@ hipError_t launch_scatter_rows(const float* src_acc, const uint8_t* src_px, cons
                        reinterpret_cast<const float4*>(src_acc), reinterpret_cast<const uint32_t*>(src_px),
                        rows, n_rows, width, reinterpret_cast<float4*>(dst_acc),
                        reinterpret_cast<uint32_t*>(dst_px));
+    return hipGetLastError();
+}
+
+hipError_t launch_resolve(const float* accum, uint64_t n_texels, uint32_t spp, uint8_t* out, hipStream_t st) {
+    const uint64_t need = (n_texels + 255) / 256, blocks = need < 65536 ? need : 65536;
+    hipLaunchKernelGGL(rt_resolve_kernel, dim3(uint32_t(blocks)), dim3(256), 0, st,
+                       reinterpret_cast<const float4*>(accum), n_texels, float(spp),
+                       reinterpret_cast<uint32_t*>(out));
     return hipGetLastError();
 }
 

@@ -208,6 +208,14 @@ class Renderer:
                                         dst_accum.data_ptr() if dst_accum is not None else None,
                                         dst_rgba8.data_ptr(), _stream_ptr(stream)))
 
+    def resolve_rgba8(self, accum, spp: int, out, stream=None) -> None:
+        """out = rgba8 tonemap of the summed float4 accumulator `accum` (device tensors), exactly
+        as the trace kernel stores a pixel (rt_resolve_rgba8)."""
+        n = accum.numel() // 4
+        if out.numel() != 4 * n:
+            raise ValueError("out must hold 4 bytes per accumulator texel")
+        check(self._lib.rt_resolve_rgba8(self._ctx, accum.data_ptr(), n, spp, out.data_ptr(), _stream_ptr(stream)))
+
 
 @dataclass
 class RenderResult:

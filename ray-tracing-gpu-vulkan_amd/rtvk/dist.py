@@ -1,4 +1,21 @@
-"""Image tiling across GPUs with a final gather.
+"""Multi-GPU frames: sample split (default) or image strips, one process per GPU.
+
+Sample split (SampleSplitRenderer). A pixel's samples form one sequential chain in the
+reference's RNG (random.glsl: one LCG stream per pixel runs through every sample), so a GPU needs
+several pixels per lane to hide the chain of its most expensive pixel: a 1080p/100-spp frame has
+8 per lane on one MI355X, but only 1 per lane with 8-row strips on 8 GPUs, where the frame time is
+the longest chain (~2000 segments) times the per-segment latency (measured: strips reach 0.9 /
+0.5 / 0.3 of linear at 2 / 4 / 8 GPUs, scripts/scaling_probe.py). Instead, rank r renders the
+whole frame with spp_r of the samples (sum spp_r = spp) and its own stream salt
+RenderCallInfo.number + r (the reference's `number`, src/render_call_info.h:6, which exists to
+decorrelate frames). Every GPU keeps all pixels and short chains; the accumulators are reduced by
+an all-to-all of row slices, each rank adding the N slices of its part in rank order
+(deterministic, so the frame equals the sum in rank order of N single-GPU frames with number =
+r), then the slices are tonemapped (rt_resolve_rgba8) and gathered to rank 0. With one GPU it is
+exactly the reference frame.
+
+Strips (DistributedRenderer): rank r renders the 8-row strips k = r mod N of the one-GPU frame
+(bit-identical to it), gathered to rank 0. Kept for the reference-stream image at any N.
 
 The reference splits the image into contiguous row bands, one per Vulkan device, with the first
 band taking the remainder (src/ray_trace.cpp:74-93), and never moves pixels between GPUs (each
@@ -119,3 +136,127 @@ def hip_assembler(renderer, stream=None):
         if rows.numel():
             renderer.scatter_rows(band_accum, band_out, rows, full_accum, full_out, stream=stream)
     return assemble
+
+
+def split_samples(spp: int, world: int) -> list:
+    """spp_r of every rank: as even as possible, sum = spp (ranks beyond spp get 0)."""
+    return [spp // world + (1 if r < spp % world else 0) for r in range(world)]
+
+
+def row_slices(height: int, world: int) -> list:
+    """Row counts of the all-to-all reduction slices (contiguous, as even as possible)."""
+    return [height // world + (1 if r < height % world else 0) for r in range(world)]
+
+
+class SampleSplitRenderer:
+    """One rank's share of a sample-split multi-GPU frame (module docstring).
+
+    render_full(number, spp_r, accum_dev, out_dev): renders the whole frame with spp_r samples and
+    stream salt `number` into [H, W, 4] buffers (nothing when spp_r == 0: the accumulator is
+    zeroed). resolve(accum, spp, out): rgba8 tonemap of a summed accumulator (rt_resolve_rgba8).
+    """
+
+    def __init__(self, width: int, height: int, spp: int, number: int, device, render_full: Callable,
+                 resolve: Callable):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.rank = dist.get_rank() if dist.is_initialized() else 0
+        self.W, self.H, self.spp, self.device = width, height, spp, device
+        self.spp_r = split_samples(spp, self.world)[self.rank]
+        self.number = number + self.rank
+        self.render_full, self.resolve = render_full, resolve
+        self.accum = torch.zeros((height, width, 4), dtype=torch.float32, device=device)
+        self.out = torch.zeros((height, width, 4), dtype=torch.uint8, device=device)
+        self.rows = row_slices(height, self.world)
+        self.row0 = [sum(self.rows[:r]) for r in range(self.world)]
+        n_mine = self.rows[self.rank]
+        self.recv = torch.empty((self.world * n_mine, width, 4), dtype=torch.float32, device=device)
+        self.part = torch.empty((n_mine, width, 4), dtype=torch.float32, device=device)
+        self.part_out = torch.empty((n_mine, width, 4), dtype=torch.uint8, device=device)
+        self.gloo = self.world > 1 and dist.get_backend() == "gloo"
+        if self.rank == 0 and self.world > 1:
+            self.full_accum = torch.zeros((height, width, 4), dtype=torch.float32, device=device)
+            self.full_out = torch.zeros((height, width, 4), dtype=torch.uint8, device=device)
+
+    def step(self):
+        """Render this rank's samples, reduce, tonemap, gather. Returns (accum, rgba8) of the whole
+        frame on rank 0, None elsewhere."""
+        torch, dist = self.torch, self.dist
+        if self.spp_r:
+            self.render_full(self.number, self.spp_r, self.accum, self.out)
+        else:
+            self.accum.zero_()
+        if self.world == 1:
+            return self.accum, self.out
+        W, r, n_mine = self.W, self.rank, self.rows[self.rank]
+        # all-to-all: rank q receives row slice q of every rank's accumulator
+        send = [self.accum[self.row0[q]: self.row0[q] + self.rows[q]] for q in range(self.world)]
+        recv = [self.recv[q * n_mine: (q + 1) * n_mine] for q in range(self.world)]
+        if self.gloo:   # rehearsal backend: host staging, same data movement
+            n_max = max(self.rows)   # gloo scatter needs equal sizes: pad every slice to n_max rows
+            hs = []
+            for t in send:
+                h = torch.zeros((n_max, W, 4), dtype=torch.float32)
+                h[: t.shape[0]].copy_(t)
+                hs.append(h)
+            hr = [torch.empty((n_max, W, 4), dtype=torch.float32) for _ in recv]
+            for q in range(self.world):   # gloo has no all_to_all: scatter from every root
+                dist.scatter(hr[q], hs if q == r else None, src=q)
+            for t, h in zip(recv, hr):
+                t.copy_(h[:n_mine])
+        else:
+            dist.all_to_all(recv, [t.contiguous() for t in send])
+        part = self.part
+        part.copy_(recv[0])
+        for q in range(1, self.world):   # float sums in rank order: deterministic
+            part.add_(recv[q])
+        self.resolve(part, self.spp, self.part_out)
+        if r == 0:
+            ga = [self.full_accum[self.row0[q]: self.row0[q] + self.rows[q]] for q in range(self.world)]
+            go = [self.full_out[self.row0[q]: self.row0[q] + self.rows[q]] for q in range(self.world)]
+        self._gather(part, ga if r == 0 else None)
+        self._gather(self.part_out, go if r == 0 else None)
+        return (self.full_accum, self.full_out) if r == 0 else None
+
+    def _gather(self, t, glist):
+        """Gather equal-or-smaller slices to rank 0 (slices may differ by one row)."""
+        torch, dist = self.torch, self.dist
+        n_max = max(self.rows)
+        buf = torch.zeros((n_max,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        buf[: t.shape[0]].copy_(t)
+        bl = None
+        if self.rank == 0:
+            bl = [torch.empty_like(buf) for _ in range(self.world)]
+        if self.gloo:
+            hb = buf.cpu()
+            hl = [torch.empty_like(hb) for _ in range(self.world)] if self.rank == 0 else None
+            dist.gather(hb, hl, dst=0)
+            if self.rank == 0:
+                for b, h in zip(bl, hl):
+                    b.copy_(h)
+        else:
+            dist.gather(buf, bl, dst=0)
+        if self.rank == 0:
+            for q in range(self.world):
+                glist[q].copy_(bl[q][: self.rows[q]])
+
+
+def hip_full_renderer(renderer, rci, options, stream=None):
+    """render_full backed by librt_mi355x.so: the whole frame with spp_r samples, salt `number`."""
+    import copy
+
+    def render_full(number, spp_r, accum, out):
+        rc = copy.copy(rci)
+        rc.number = number
+        rc.samplesPerRenderCall = spp_r
+        renderer.render_device(rc, accum, out, options=options, stream=stream)
+    return render_full
+
+
+def hip_resolver(renderer, stream=None):
+    """resolve backed by rt_resolve_rgba8."""
+    def resolve(accum, spp, out):
+        renderer.resolve_rgba8(accum, spp, out, stream=stream)
+    return resolve

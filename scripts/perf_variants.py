@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--accels", default="2,1")
     ap.add_argument("--walk", default="0", help="LBVH walk forms to sweep (0 default/ordered, 1 escape-link)")
     ap.add_argument("--count", action="store_true", help="also report box / sphere tests per segment")
+    ap.add_argument("--rng", default="0", help="rng modes to sweep (0 pixel stream, 1 sample counter)")
     ap.add_argument("--inexact", action="store_true",
                     help="report differing pixels instead of failing (experiments that relax exactness)")
     args = ap.parse_args()
@@ -52,9 +53,10 @@ def main():
     configs = []
     for accel in [int(a) for a in args.accels.split(",")]:
         for c in ([int(x) for x in args.walk.split(",")] if accel == 2 else [0]):
-            opt = rtvk.make_options(accel=accel)
-            opt.reserved[1] = c
-            configs.append((accel, c, opt))
+            for rng in [int(x) for x in args.rng.split(",")]:
+                opt = rtvk.make_options(accel=accel, rng_mode=rng)
+                opt.reserved[1] = c
+                configs.append((accel * 10 + rng, c, opt))
     for accel, cth, opt in configs:
         for r in range(args.rounds + 1):
             for lp, lib, ctx in ctxs:
@@ -66,7 +68,7 @@ def main():
                 assert rc == 0, lib.rt_last_error()
                 torch.cuda.synchronize()
                 if r == 0 and args.count:
-                    copt = rtvk.make_options(accel=accel, count_tests=True)
+                    copt = rtvk.make_options(accel=accel // 10, count_tests=True, rng_mode=accel % 10)
                     copt.reserved[1] = cth
                     assert lib.rt_render_device(ctx, ctypes.byref(rci), None, W, H, acc.data_ptr(), out.data_ptr(),
                                                 ctypes.byref(copt), stream.cuda_stream) == 0

@@ -71,3 +71,65 @@ def test_gather_reassembly_world2(tmp_path, oracle):
     ref_a, ref_o, _ = oracle.render(oracle.generate_scene(), oracle.render_call_info(SPP, W, H), W, H)
     np.testing.assert_array_equal(got["accum"], ref_a)
     np.testing.assert_array_equal(got["rgba8"], ref_o)
+
+
+def test_sample_split_partition():
+    from rtvk.dist import row_slices, split_samples
+    for spp in (1, 3, 100, 1000):
+        for world in (1, 2, 3, 8):
+            s = split_samples(spp, world)
+            assert sum(s) == spp and max(s) - min(s) <= 1
+    for h in (1, 27, 1080):
+        for world in (1, 2, 8):
+            r = row_slices(h, world)
+            assert sum(r) == h and max(r) - min(r) <= 1
+
+
+SPLIT_SPP = 5
+
+
+def _split_worker(rank, world, port, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle
+    from rtvk.dist import SampleSplitRenderer
+
+    sc = oracle.generate_scene()
+
+    def render_full(number, spp_r, accum, out):
+        a, o, _ = oracle.render(sc, oracle.render_call_info(spp_r, W, H, number=number), W, H, threads=2)
+        accum.copy_(torch.from_numpy(a))
+        out.copy_(torch.from_numpy(o))
+
+    def resolve(accum, spp, out):
+        out.copy_(torch.from_numpy(oracle.resolve(accum.numpy(), spp)))
+
+    sr = SampleSplitRenderer(W, H, SPLIT_SPP, 7, torch.device("cpu"), render_full, resolve)
+    res = sr.step()
+    if rank == 0:
+        np.savez(out_path, accum=res[0].numpy(), rgba8=res[1].numpy())
+    else:
+        assert res is None
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sample_split_world(tmp_path, oracle, world):
+    """Rank r renders split_samples(spp)[r] samples with number = 7 + r; the reduced frame equals
+    the rank-ordered float sum of those sub-frames, tonemapped with the full spp."""
+    from rtvk.dist import split_samples
+    port = _free_port()
+    out = str(tmp_path / "img.npz")
+    mp.start_processes(_split_worker, args=(world, port, out), nprocs=world, join=True, start_method="spawn")
+    got = np.load(out)
+    sc = oracle.generate_scene()
+    ref = None
+    for r, s in enumerate(split_samples(SPLIT_SPP, world)):
+        a, _, _ = oracle.render(sc, oracle.render_call_info(s, W, H, number=7 + r), W, H)
+        ref = a if ref is None else ref + a
+    np.testing.assert_array_equal(got["accum"], ref)
+    np.testing.assert_array_equal(got["rgba8"], oracle.resolve(ref, SPLIT_SPP))
+    # one rank: exactly the reference frame
+    a1, o1, _ = oracle.render(sc, oracle.render_call_info(SPLIT_SPP, W, H, number=7), W, H)
+    assert not np.array_equal(got["accum"], a1)  # other ranks' salts do change the noise

@@ -331,3 +331,47 @@ def test_lbvh_equals_brute_bench_workload(rtvk, renderer, torch, oracle, form):
     assert bad.size == 0, f"{len(bad)} pixels differ from brute force, first {bad[:4].tolist()}"
     np.testing.assert_array_equal(ol, ob)
     assert (sl.segments, sl.samples) == (sb.segments, sb.samples)
+
+
+def test_resolve_rgba8_edge_values(rtvk, renderer, torch, oracle):
+    """rt_resolve_rgba8 against the oracle's tonemap on edge accumulators: negative, zero,
+    subnormal, > spp, inf and NaN sums (UNORM clamp, NaN -> 0)."""
+    rng = np.random.default_rng(5)
+    a = rng.standard_normal((37, 53, 4)).astype(np.float32) * 40
+    special = np.array([0.0, -0.0, 1e-45, -1e-45, np.inf, -np.inf, np.nan, 99.5, 100.0, 1e30], np.float32)
+    a.reshape(-1)[: special.size * 7] = np.tile(special, 7)
+    for spp in (1, 3, 100):
+        out = torch.zeros((37, 53, 4), dtype=torch.uint8, device="cuda")
+        renderer.resolve_rgba8(torch.from_numpy(a).cuda(), spp, out)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(out.cpu().numpy(), oracle.resolve(a, spp))
+    with pytest.raises(rtvk.RtError):
+        renderer.resolve_rgba8(torch.from_numpy(a).cuda(), 0, out)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sample_split_subframes(rtvk, renderer, torch, oracle, world):
+    """The sample-split multi-GPU frame (rtvk.dist.SampleSplitRenderer) on one device: the sub-frame
+    of each simulated rank (spp_r samples, number = 7 + r), summed in rank order and resolved with
+    rt_resolve_rgba8, equals the oracle's sub-frames summed the same way, bit for bit."""
+    from rtvk.dist import split_samples
+    W, H, spp = 72, 40, 5
+    sc = oracle.generate_scene()
+    renderer.set_scene(sc)
+    tot = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+    ref = None
+    for r, s in enumerate(split_samples(spp, world)):
+        rci = oracle.render_call_info(s, W, H, number=7 + r)
+        a = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        o = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+        renderer.render_device(rtvk.RenderCallInfo.from_buffer_copy(rci.tobytes()), a, o,
+                               options=rtvk.make_options())
+        tot.add_(a)
+        ra, ro, _ = oracle.render(sc, rci, W, H)
+        torch.cuda.synchronize()
+        assert_same(a.cpu().numpy(), o.cpu().numpy(), ra, ro)
+        ref = ra if ref is None else ref + ra
+    out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+    renderer.resolve_rgba8(tot, spp, out)
+    torch.cuda.synchronize()
+    assert_same(tot.cpu().numpy(), out.cpu().numpy(), ref, oracle.resolve(ref, spp))
