@@ -790,6 +790,14 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     const uint64_t full = uint64_t(ctx->cu_count) * ctx->occ[accel][ci];
     const uint64_t by_work = (uint64_t(P.n_units) + blk - 1) / blk;
     const int grid = int(std::max<uint64_t>(1, std::min(full, by_work)));
+    {   // chunked refill (escape-walk kernels): the last `reserve` units go out
+        // pixel by pixel. Measured (scripts/refill_ab.py, 1080p): 0 to 32 Ki are within 1 %, one
+        // pixel per lane of the grid (262 Ki) is 10-15 % slower at 13-50 spp.
+        uint64_t reserve = 8192;
+        if (const char* e = std::getenv("RT_REFILL_RESERVE")) reserve = std::strtoull(e, nullptr, 10);
+        P.n_chunk_units = 0;
+        if (P.tile_cost && P.n_units > reserve) P.n_chunk_units = uint32_t((P.n_units - reserve) & ~uint64_t(63));
+    }
     RT_HIP(rt::launch_trace(P, accel, count, grid, lds, st));
     ctx->last_stream = st;
     if (P.tile_cost) {

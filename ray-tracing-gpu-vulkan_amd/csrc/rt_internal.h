@@ -85,8 +85,8 @@ enum : uint32_t { ACCEL_BRUTE = 1, ACCEL_LBVH = 2, ACCEL_LBVH_LDS = 3, ACCEL_LBV
 
 // Counters block (device memory, zeroed before each launch by the host).
 struct Counters {
-    uint32_t work_head;            // next unit (pixel) to hand out
-    uint32_t _pad;
+    uint32_t work_head;            // next unit (pixel) to hand out; chunked refill: next 64-unit chunk
+    uint32_t work_tail;            // chunked refill: next unit past n_chunk_units (per-lane hand-out)
     unsigned long long segments;
     unsigned long long samples;
     unsigned long long box_tests;
@@ -114,6 +114,8 @@ struct TraceParams {
     uint32_t band_w, band_h;
     uint32_t tiles_x;              // ceil(band_w / 8)
     uint32_t n_units;              // tiles_x * ceil(band_h / 8) * 64
+    uint32_t n_chunk_units;        // LBVH kernels: units [0, n_chunk_units) go out as whole 8x8 tiles
+                                   // (one atomic per 64 pixels per wave), the rest pixel by pixel
     const uint32_t* rows;          // optional global row per band row
     const uint32_t* tile_order;    // optional: hand-out rank -> 8x8 tile index (null: row-major)
     uint32_t* tile_cost;           // optional: per 8x8 tile, traced segments of its most expensive

@@ -375,3 +375,26 @@ def test_sample_split_subframes(rtvk, renderer, torch, oracle, world):
     renderer.resolve_rgba8(tot, spp, out)
     torch.cuda.synchronize()
     assert_same(tot.cpu().numpy(), out.cpu().numpy(), ref, oracle.resolve(ref, spp))
+
+
+@pytest.mark.parametrize("reserve", ["0", "100", str(1 << 40)])
+def test_chunked_refill_same_image(rtvk, renderer, torch, oracle, reserve):
+    """Pixel hand-out by whole tiles (RT_REFILL_RESERVE=0), tiles then single pixels (100), and
+    single pixels only (huge reserve) render the same image as the oracle, on a ragged frame
+    (width and height not multiples of 8) so tiles with missing pixels go through the tile path."""
+    W, H = 203, 117
+    sc = oracle.generate_scene()
+    rci = oracle.render_call_info(3, W, H)
+    ra, ro, rs = oracle.render(sc, rci, W, H)
+    prev = os.environ.get("RT_REFILL_RESERVE")
+    os.environ["RT_REFILL_RESERVE"] = reserve
+    try:
+        for _ in range(2):   # second launch runs with the LPT hand-out order
+            a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH_OCT)
+            assert_same(a, o, ra, ro)
+            assert (st.segments, st.samples) == (rs[0], rs[1])
+    finally:
+        if prev is None:
+            os.environ.pop("RT_REFILL_RESERVE", None)
+        else:
+            os.environ["RT_REFILL_RESERVE"] = prev
