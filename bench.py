@@ -107,7 +107,7 @@ def main() -> int:
     import rtvk
     from rtvk import abi
     from rtvk.dist import (DistributedRenderer, SampleSplitRenderer, hip_assembler, hip_band_renderer,
-                           hip_full_renderer, hip_resolver)
+                           hip_full_renderer, hip_reducer)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -166,7 +166,7 @@ def main() -> int:
             e1.record(stream)
             ev.append((e0, e1))
 
-        dr = SampleSplitRenderer(W, H, spp, rci.number, dev, timed_full, hip_resolver(renderer))
+        dr = SampleSplitRenderer(W, H, spp, rci.number, dev, timed_full, hip_reducer(renderer))
     else:
         dr = DistributedRenderer(W, H, dev, timed_render, hip_assembler(renderer))
 

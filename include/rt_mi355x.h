@@ -161,6 +161,15 @@ int rt_scatter_rows(rt_context* ctx, const float* src_accum, const uint8_t* src_
 int rt_resolve_rgba8(rt_context* ctx, const float* accum_rgba32f, uint64_t n_texels, uint32_t spp,
                      uint8_t* out_rgba8, void* stream);
 
+/*
+ * The sample-split reduction in one pass: slices = n_slices consecutive accumulators of n_texels
+ * float4 each (rank order); accum_out (optional, may alias slice 0) = their float sum added in
+ * slice order, alpha 1.0 (shader.rgen:63); out_rgba8 = the tonemap of that sum as
+ * rt_resolve_rgba8. All pointers DEVICE.
+ */
+int rt_reduce_resolve(rt_context* ctx, const float* slices, uint32_t n_slices, uint64_t n_texels,
+                      uint32_t spp, float* accum_out, uint8_t* out_rgba8, void* stream);
+
 /* ---- host-pointer convenience ------------------------------------------------------ */
 /*
  * One frame over the full image rci[0].image_size with host buffers. rci_count bands, band i

@@ -29,7 +29,8 @@ namespace rt {
 hipError_t launch_trace(const TraceParams& P, uint32_t accel, bool count, int grid, size_t lds_bytes,
                         hipStream_t st);
 hipError_t trace_occupancy(uint32_t accel, bool count, size_t lds_bytes, int* blocks_per_cu);
-hipError_t launch_resolve(const float* accum, uint64_t n_texels, uint32_t spp, uint8_t* out, hipStream_t st);
+hipError_t launch_reduce_resolve(const float* slices, uint32_t n_slices, uint64_t n_texels, uint32_t spp,
+                                 float* accum_out, uint8_t* out, hipStream_t st);
 uint32_t block_size(uint32_t accel);
 size_t pool_bytes(uint32_t accel);
 hipError_t launch_scatter_rows(const float* src_acc, const uint8_t* src_px, const uint32_t* rows,
@@ -827,7 +828,19 @@ int rt_resolve_rgba8(rt_context* ctx, const float* accum, uint64_t n_texels, uin
     if (!accum || !out) return fail(RT_ERR_INVALID_ARGUMENT, "accum or out is NULL");
     if (spp == 0) return fail(RT_ERR_INVALID_ARGUMENT, "spp is zero");
     DeviceGuard g(ctx->device);
-    RT_HIP(rt::launch_resolve(accum, n_texels, spp, out, static_cast<hipStream_t>(stream)));
+    RT_HIP(rt::launch_reduce_resolve(accum, 1, n_texels, spp, nullptr, out, static_cast<hipStream_t>(stream)));
+    return RT_OK;
+}
+
+int rt_reduce_resolve(rt_context* ctx, const float* slices, uint32_t n_slices, uint64_t n_texels,
+                      uint32_t spp, float* accum_out, uint8_t* out_rgba8, void* stream) {
+    if (!ctx) return fail(RT_ERR_INVALID_ARGUMENT, "ctx is NULL");
+    if (n_texels == 0) return RT_OK;
+    if (!slices || !out_rgba8) return fail(RT_ERR_INVALID_ARGUMENT, "slices or out_rgba8 is NULL");
+    if (n_slices == 0 || spp == 0) return fail(RT_ERR_INVALID_ARGUMENT, "n_slices or spp is zero");
+    DeviceGuard g(ctx->device);
+    RT_HIP(rt::launch_reduce_resolve(slices, n_slices, n_texels, spp, accum_out, out_rgba8,
+                                     static_cast<hipStream_t>(stream)));
     return RT_OK;
 }
 

@@ -1246,11 +1246,21 @@ __global__ __launch_bounds__(256) void rt_scatter_rows_kernel(const float4* __re
     }
 }
 
-// Tonemap of a summed accumulator (rt_resolve_rgba8): the trace kernel's pixel store, shader.rgen:65-66.
-__global__ __launch_bounds__(256) void rt_resolve_kernel(const float4* __restrict__ acc, uint64_t n,
-                                                         float spp, uint32_t* __restrict__ out) {
+// Sum of ns accumulator slices in slice order, then the trace kernel's pixel store
+// (shader.rgen:63-66) of the sum (rt_reduce_resolve / rt_resolve_rgba8). HBM-bound: ns x 16 B
+// read + 16 B (acc_out) + 4 B written per texel. acc_out may alias slice 0 (same-index update).
+__global__ __launch_bounds__(256) void rt_reduce_resolve_kernel(const float4* slices, uint32_t ns, uint64_t n,
+                                                                float spp, float4* acc_out,
+                                                                uint32_t* __restrict__ out) {
     for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
-        const float4 s = acc[i];
+        float4 s = slices[i];
+        for (uint32_t q = 1; q < ns; ++q) {
+            const float4 v = slices[uint64_t(q) * n + i];
+            s.x = s.x + v.x;
+            s.y = s.y + v.y;
+            s.z = s.z + v.z;
+        }
+        if (acc_out) acc_out[i] = make_float4(s.x, s.y, s.z, 1.0f);
         out[i] = unorm8(__builtin_sqrtf(s.x / spp)) | (unorm8(__builtin_sqrtf(s.y / spp)) << 8) |
                  (unorm8(__builtin_sqrtf(s.z / spp)) << 16) | (255u << 24);
     }
@@ -1360,11 +1370,12 @@ hipError_t launch_scatter_rows(const float* src_acc, const uint8_t* src_px, cons
     return hipGetLastError();
 }
 
-hipError_t launch_resolve(const float* accum, uint64_t n_texels, uint32_t spp, uint8_t* out, hipStream_t st) {
-    const uint64_t need = (n_texels + 255) / 256, blocks = need < 65536 ? need : 65536;
-    hipLaunchKernelGGL(rt_resolve_kernel, dim3(uint32_t(blocks)), dim3(256), 0, st,
-                       reinterpret_cast<const float4*>(accum), n_texels, float(spp),
-                       reinterpret_cast<uint32_t*>(out));
+hipError_t launch_reduce_resolve(const float* slices, uint32_t n_slices, uint64_t n_texels, uint32_t spp,
+                                 float* accum_out, uint8_t* out, hipStream_t st) {
+    const uint64_t need = (n_texels + 255) / 256, blocks = need < 8192 ? need : 8192;
+    hipLaunchKernelGGL(rt_reduce_resolve_kernel, dim3(uint32_t(blocks)), dim3(256), 0, st,
+                       reinterpret_cast<const float4*>(slices), n_slices, n_texels, float(spp),
+                       reinterpret_cast<float4*>(accum_out), reinterpret_cast<uint32_t*>(out));
     return hipGetLastError();
 }
 

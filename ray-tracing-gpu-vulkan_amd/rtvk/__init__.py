@@ -216,6 +216,20 @@ class Renderer:
             raise ValueError("out must hold 4 bytes per accumulator texel")
         check(self._lib.rt_resolve_rgba8(self._ctx, accum.data_ptr(), n, spp, out.data_ptr(), _stream_ptr(stream)))
 
+    def reduce_resolve(self, slices, spp: int, accum_out, out, stream=None) -> None:
+        """accum_out = float sum of slices[0], slices[1], ... in that order (alpha 1), out = its
+        rgba8 tonemap (rt_reduce_resolve). slices: contiguous float32 cuda tensor [n, ..., 4];
+        accum_out (optional) / out: cuda tensors of one slice's texels."""
+        if not slices.is_contiguous() or str(slices.dtype) != "torch.float32" or not slices.is_cuda:
+            raise ValueError("slices must be a contiguous float32 tensor")
+        ns = int(slices.shape[0])
+        n = slices.numel() // (4 * ns)
+        if out.numel() != 4 * n or (accum_out is not None and accum_out.numel() != 4 * n):
+            raise ValueError("accum_out / out must hold one texel per slice texel")
+        check(self._lib.rt_reduce_resolve(self._ctx, slices.data_ptr(), ns, n, spp,
+                                          accum_out.data_ptr() if accum_out is not None else None,
+                                          out.data_ptr(), _stream_ptr(stream)))
+
 
 @dataclass
 class RenderResult:

@@ -110,6 +110,7 @@ EXPORTS = {
     "rt_get_stats": (_I, [_P, ctypes.POINTER(Stats)]),
     "rt_scatter_rows": (_I, [_P, _P, _P, _P, _U32, _U32, _P, _P, _P]),
     "rt_resolve_rgba8": (_I, [_P, _P, ctypes.c_uint64, _U32, _P, _P]),
+    "rt_reduce_resolve": (_I, [_P, _P, _U32, ctypes.c_uint64, _U32, _P, _P, _P]),
     "rt_render": (_I, [_P, _U32, _P, _U32, _P, _P, ctypes.POINTER(Options), ctypes.POINTER(Stats)]),
     "rt_store_ppm": (_I, [ctypes.c_char_p, _P, _U32, _U32]),
     "rt_debug_math": (_I, [_I, _I, _P, _P, _U32]),

@@ -11,7 +11,8 @@ RenderCallInfo.number + r (the reference's `number`, src/render_call_info.h:6, w
 decorrelate frames). Every GPU keeps all pixels and short chains; the accumulators are reduced by
 an all-to-all of row slices, each rank adding the N slices of its part in rank order
 (deterministic, so the frame equals the sum in rank order of N single-GPU frames with number =
-r), then the slices are tonemapped (rt_resolve_rgba8) and gathered to rank 0. With one GPU it is
+r, alpha 1), then the slices are tonemapped (rt_reduce_resolve, fused with the sum) and gathered
+to rank 0. With one GPU it is
 exactly the reference frame.
 
 Strips (DistributedRenderer): rank r renders the 8-row strips k = r mod N of the one-GPU frame
@@ -152,12 +153,12 @@ class SampleSplitRenderer:
     """One rank's share of a sample-split multi-GPU frame (module docstring).
 
     render_full(number, spp_r, accum_dev, out_dev): renders the whole frame with spp_r samples and
-    stream salt `number` into [H, W, 4] buffers (nothing when spp_r == 0: the accumulator is
-    zeroed). resolve(accum, spp, out): rgba8 tonemap of a summed accumulator (rt_resolve_rgba8).
+    stream salt `number` into [H, W, 4] buffers. reduce(slices, spp, accum_out, out): accum_out =
+    float sum of slices[0..N) in order with alpha 1, out = its rgba8 tonemap (rt_reduce_resolve).
     """
 
     def __init__(self, width: int, height: int, spp: int, number: int, device, render_full: Callable,
-                 resolve: Callable):
+                 reduce: Callable):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
@@ -166,81 +167,79 @@ class SampleSplitRenderer:
         self.W, self.H, self.spp, self.device = width, height, spp, device
         self.spp_r = split_samples(spp, self.world)[self.rank]
         self.number = number + self.rank
-        self.render_full, self.resolve = render_full, resolve
+        self.render_full, self.reduce = render_full, reduce
         self.accum = torch.zeros((height, width, 4), dtype=torch.float32, device=device)
         self.out = torch.zeros((height, width, 4), dtype=torch.uint8, device=device)
         self.rows = row_slices(height, self.world)
         self.row0 = [sum(self.rows[:r]) for r in range(self.world)]
+        self.n_max = max(self.rows)
         n_mine = self.rows[self.rank]
-        self.recv = torch.empty((self.world * n_mine, width, 4), dtype=torch.float32, device=device)
-        self.part = torch.empty((n_mine, width, 4), dtype=torch.float32, device=device)
-        self.part_out = torch.empty((n_mine, width, 4), dtype=torch.uint8, device=device)
+        self.recv = torch.empty((self.world, n_mine, width, 4), dtype=torch.float32, device=device)
+        # reduced slice, padded to n_max rows so every rank's gather buffer has one shape
+        self.part = torch.zeros((self.n_max, width, 4), dtype=torch.float32, device=device)
+        self.part_out = torch.zeros((self.n_max, width, 4), dtype=torch.uint8, device=device)
         self.gloo = self.world > 1 and dist.get_backend() == "gloo"
+        self.even = all(n == self.n_max for n in self.rows)
         if self.rank == 0 and self.world > 1:
-            self.full_accum = torch.zeros((height, width, 4), dtype=torch.float32, device=device)
-            self.full_out = torch.zeros((height, width, 4), dtype=torch.uint8, device=device)
+            self.g_accum = torch.zeros((self.world, self.n_max, width, 4), dtype=torch.float32, device=device)
+            self.g_out = torch.zeros((self.world, self.n_max, width, 4), dtype=torch.uint8, device=device)
+            if self.even:   # the gather lands in place
+                self.full_accum = self.g_accum.view(height, width, 4)
+                self.full_out = self.g_out.view(height, width, 4)
+            else:
+                self.full_accum = torch.zeros((height, width, 4), dtype=torch.float32, device=device)
+                self.full_out = torch.zeros((height, width, 4), dtype=torch.uint8, device=device)
 
     def step(self):
         """Render this rank's samples, reduce, tonemap, gather. Returns (accum, rgba8) of the whole
         frame on rank 0, None elsewhere."""
         torch, dist = self.torch, self.dist
+        if self.world == 1:
+            self.render_full(self.number, self.spp_r, self.accum, self.out)
+            return self.accum, self.out
         if self.spp_r:
             self.render_full(self.number, self.spp_r, self.accum, self.out)
         else:
             self.accum.zero_()
-        if self.world == 1:
-            return self.accum, self.out
         W, r, n_mine = self.W, self.rank, self.rows[self.rank]
-        # all-to-all: rank q receives row slice q of every rank's accumulator
-        send = [self.accum[self.row0[q]: self.row0[q] + self.rows[q]] for q in range(self.world)]
-        recv = [self.recv[q * n_mine: (q + 1) * n_mine] for q in range(self.world)]
-        if self.gloo:   # rehearsal backend: host staging, same data movement
-            n_max = max(self.rows)   # gloo scatter needs equal sizes: pad every slice to n_max rows
+        # all-to-all: rank q receives row slice q of every rank's accumulator, in rank order
+        if self.gloo:   # rehearsal backend (no all_to_all): host staging, scatter from every root
             hs = []
-            for t in send:
-                h = torch.zeros((n_max, W, 4), dtype=torch.float32)
-                h[: t.shape[0]].copy_(t)
-                hs.append(h)
-            hr = [torch.empty((n_max, W, 4), dtype=torch.float32) for _ in recv]
-            for q in range(self.world):   # gloo has no all_to_all: scatter from every root
-                dist.scatter(hr[q], hs if q == r else None, src=q)
-            for t, h in zip(recv, hr):
-                t.copy_(h[:n_mine])
-        else:
-            dist.all_to_all(recv, [t.contiguous() for t in send])
-        part = self.part
-        part.copy_(recv[0])
-        for q in range(1, self.world):   # float sums in rank order: deterministic
-            part.add_(recv[q])
-        self.resolve(part, self.spp, self.part_out)
-        if r == 0:
-            ga = [self.full_accum[self.row0[q]: self.row0[q] + self.rows[q]] for q in range(self.world)]
-            go = [self.full_out[self.row0[q]: self.row0[q] + self.rows[q]] for q in range(self.world)]
-        self._gather(part, ga if r == 0 else None)
-        self._gather(self.part_out, go if r == 0 else None)
-        return (self.full_accum, self.full_out) if r == 0 else None
-
-    def _gather(self, t, glist):
-        """Gather equal-or-smaller slices to rank 0 (slices may differ by one row)."""
-        torch, dist = self.torch, self.dist
-        n_max = max(self.rows)
-        buf = torch.zeros((n_max,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-        buf[: t.shape[0]].copy_(t)
-        bl = None
-        if self.rank == 0:
-            bl = [torch.empty_like(buf) for _ in range(self.world)]
-        if self.gloo:
-            hb = buf.cpu()
-            hl = [torch.empty_like(hb) for _ in range(self.world)] if self.rank == 0 else None
-            dist.gather(hb, hl, dst=0)
-            if self.rank == 0:
-                for b, h in zip(bl, hl):
-                    b.copy_(h)
-        else:
-            dist.gather(buf, bl, dst=0)
-        if self.rank == 0:
             for q in range(self.world):
-                glist[q].copy_(bl[q][: self.rows[q]])
+                h = torch.zeros((self.n_max, W, 4), dtype=torch.float32)
+                h[: self.rows[q]].copy_(self.accum[self.row0[q]: self.row0[q] + self.rows[q]])
+                hs.append(h)
+            hr = torch.empty((self.n_max, W, 4), dtype=torch.float32)
+            for q in range(self.world):
+                dist.scatter(hr, hs if q == r else None, src=q)
+                self.recv[q].copy_(hr[:n_mine])
+        else:
+            dist.all_to_all_single(self.recv, self.accum, output_split_sizes=[n_mine] * self.world,
+                                   input_split_sizes=self.rows)
+        self.reduce(self.recv, self.spp, self.part[:n_mine], self.part_out[:n_mine])
+        self._gather(self.part, self.g_accum if r == 0 else None)
+        self._gather(self.part_out, self.g_out if r == 0 else None)
+        if r != 0:
+            return None
+        if not self.even:
+            for q in range(self.world):
+                self.full_accum[self.row0[q]: self.row0[q] + self.rows[q]].copy_(self.g_accum[q, : self.rows[q]])
+                self.full_out[self.row0[q]: self.row0[q] + self.rows[q]].copy_(self.g_out[q, : self.rows[q]])
+        return self.full_accum, self.full_out
+
+    def _gather(self, t, dst):
+        """Gather every rank's [n_max, W, 4] slice into dst[world, n_max, W, 4] on rank 0."""
+        dist = self.dist
+        lst = list(dst.unbind(0)) if dst is not None else None
+        if self.gloo:
+            hb = t.cpu()
+            hl = [self.torch.empty_like(hb) for _ in range(self.world)] if lst is not None else None
+            dist.gather(hb, hl, dst=0)
+            if lst is not None:
+                for d, h in zip(lst, hl):
+                    d.copy_(h)
+        else:
+            dist.gather(t, lst, dst=0)
 
 
 def hip_full_renderer(renderer, rci, options, stream=None):
@@ -255,8 +254,8 @@ def hip_full_renderer(renderer, rci, options, stream=None):
     return render_full
 
 
-def hip_resolver(renderer, stream=None):
-    """resolve backed by rt_resolve_rgba8."""
-    def resolve(accum, spp, out):
-        renderer.resolve_rgba8(accum, spp, out, stream=stream)
-    return resolve
+def hip_reducer(renderer, stream=None):
+    """reduce backed by rt_reduce_resolve (one pass: rank-ordered sum + tonemap)."""
+    def reduce(slices, spp, accum_out, out):
+        renderer.reduce_resolve(slices, spp, accum_out, out, stream=stream)
+    return reduce

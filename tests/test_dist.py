@@ -101,10 +101,15 @@ def _split_worker(rank, world, port, out_path):
         accum.copy_(torch.from_numpy(a))
         out.copy_(torch.from_numpy(o))
 
-    def resolve(accum, spp, out):
-        out.copy_(torch.from_numpy(oracle.resolve(accum.numpy(), spp)))
+    def reduce(slices, spp, accum_out, out):
+        a = slices[0].numpy().copy()
+        for q in range(1, slices.shape[0]):
+            a += slices[q].numpy()
+        a[..., 3] = 1.0
+        accum_out.copy_(torch.from_numpy(a))
+        out.copy_(torch.from_numpy(oracle.resolve(a, spp)))
 
-    sr = SampleSplitRenderer(W, H, SPLIT_SPP, 7, torch.device("cpu"), render_full, resolve)
+    sr = SampleSplitRenderer(W, H, SPLIT_SPP, 7, torch.device("cpu"), render_full, reduce)
     res = sr.step()
     if rank == 0:
         np.savez(out_path, accum=res[0].numpy(), rgba8=res[1].numpy())
@@ -128,6 +133,7 @@ def test_sample_split_world(tmp_path, oracle, world):
     for r, s in enumerate(split_samples(SPLIT_SPP, world)):
         a, _, _ = oracle.render(sc, oracle.render_call_info(s, W, H, number=7 + r), W, H)
         ref = a if ref is None else ref + a
+    ref[..., 3] = 1.0
     np.testing.assert_array_equal(got["accum"], ref)
     np.testing.assert_array_equal(got["rgba8"], oracle.resolve(ref, SPLIT_SPP))
     # one rank: exactly the reference frame

@@ -352,29 +352,34 @@ def test_resolve_rgba8_edge_values(rtvk, renderer, torch, oracle):
 @pytest.mark.parametrize("world", [2, 3])
 def test_sample_split_subframes(rtvk, renderer, torch, oracle, world):
     """The sample-split multi-GPU frame (rtvk.dist.SampleSplitRenderer) on one device: the sub-frame
-    of each simulated rank (spp_r samples, number = 7 + r), summed in rank order and resolved with
-    rt_resolve_rgba8, equals the oracle's sub-frames summed the same way, bit for bit."""
+    of each simulated rank (spp_r samples, number = 7 + r) equals the oracle's, and
+    rt_reduce_resolve of the stacked sub-frames equals their float sum in rank order (alpha 1)
+    and its tonemap, bit for bit."""
     from rtvk.dist import split_samples
     W, H, spp = 72, 40, 5
     sc = oracle.generate_scene()
     renderer.set_scene(sc)
-    tot = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+    slices = torch.zeros((world, H, W, 4), dtype=torch.float32, device="cuda")
     ref = None
     for r, s in enumerate(split_samples(spp, world)):
         rci = oracle.render_call_info(s, W, H, number=7 + r)
-        a = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
         o = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
-        renderer.render_device(rtvk.RenderCallInfo.from_buffer_copy(rci.tobytes()), a, o,
+        renderer.render_device(rtvk.RenderCallInfo.from_buffer_copy(rci.tobytes()), slices[r], o,
                                options=rtvk.make_options())
-        tot.add_(a)
         ra, ro, _ = oracle.render(sc, rci, W, H)
         torch.cuda.synchronize()
-        assert_same(a.cpu().numpy(), o.cpu().numpy(), ra, ro)
+        assert_same(slices[r].cpu().numpy(), o.cpu().numpy(), ra, ro)
         ref = ra if ref is None else ref + ra
+    ref[..., 3] = 1.0
+    acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
     out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
-    renderer.resolve_rgba8(tot, spp, out)
+    renderer.reduce_resolve(slices, spp, acc, out)
     torch.cuda.synchronize()
-    assert_same(tot.cpu().numpy(), out.cpu().numpy(), ref, oracle.resolve(ref, spp))
+    assert_same(acc.cpu().numpy(), out.cpu().numpy(), ref, oracle.resolve(ref, spp))
+    # in place over slice 0 (the accum_out alias the library allows)
+    renderer.reduce_resolve(slices, spp, slices[0], out)
+    torch.cuda.synchronize()
+    assert_same(slices[0].cpu().numpy(), out.cpu().numpy(), ref, oracle.resolve(ref, spp))
 
 
 @pytest.mark.parametrize("reserve", ["0", "100", str(1 << 40)])
