@@ -280,8 +280,19 @@ __device__ __forceinline__ void refill(const rt::TraceParams& P, uint32_t lane, 
 // atomics on the one counter were the cost: 1080p at 13 spp took 10.5 ms with them, 4.8 ms
 // with tiles (scripts/refill_ab.py). `ch_*` are
 // wave-uniform: next unit and end of the wave's current tile, its tile index; `ch_dry` once the
-// tile phase is exhausted.
-struct WaveChunk { uint32_t next = 0, end = 0, tile = 0; bool dry = false; };
+// tile phase is exhausted. `seed` (per lane) is the pixel seed of the tile's pixel `lane`: the
+// 64 seeds of a tile are computed together when the tile is taken (two TEAs, 16 rounds each,
+// with every lane busy) instead of one lane at a time as its pixel starts.
+struct WaveChunk { uint32_t next = 0, end = 0, tile = 0; bool dry = false; uint32_t seed = 0; };
+
+// shader.rgen:40 seed of pixel w (0..63) of 8x8 tile t of the band.
+__device__ __forceinline__ uint32_t tile_pixel_seed(const rt::TraceParams& P, uint32_t t, uint32_t w) {
+    const uint32_t lx = (t % P.tiles_x) * 8u + (w & 7u);
+    const uint32_t ly = (t / P.tiles_x) * 8u + (w >> 3);
+    const uint32_t gx = P.off_x + lx;
+    const uint32_t gy = P.rows ? P.rows[ly < P.band_h ? ly : P.band_h - 1u] : P.off_y + ly;   // ragged edge: unused
+    return tea(tea(P.seed_local ? lx : gx, P.seed_local ? ly : gy), P.number);
+}
 
 __device__ __forceinline__ void refill_chunked(const rt::TraceParams& P, uint32_t lane, uint32_t& st,
                                                Path& ps, WaveChunk& ch) {
@@ -293,6 +304,7 @@ __device__ __forceinline__ void refill_chunked(const rt::TraceParams& P, uint32_
     const int leader = __ffsll(need) - 1;
     uint32_t u = 0, t = 0;
     bool per_lane = false;
+    uint32_t seed = __shfl(ch.seed, int((ch.next + rank) & 63u));   // all lanes: uniform control flow
     if (rank < avail) { u = ch.next + rank; t = ch.tile; }
     if (cnt <= avail) {
         ch.next += cnt;
@@ -309,7 +321,9 @@ __device__ __forceinline__ void refill_chunked(const rt::TraceParams& P, uint32_
             if (nb >= P.n_chunk_units) ch.dry = true;
         }
         if (!ch.dry) {
-            if (rank >= avail) { u = nb + (rank - avail); t = nt; }
+            ch.seed = tile_pixel_seed(P, nt, lane);
+            const uint32_t sn = __shfl(ch.seed, int((rank - avail) & 63u));
+            if (rank >= avail) { u = nb + (rank - avail); t = nt; seed = sn; }
             ch.next = nb + rest;
             ch.end = nb + 64u;
             ch.tile = nt;
@@ -330,10 +344,9 @@ __device__ __forceinline__ void refill_chunked(const rt::TraceParams& P, uint32_
     const uint32_t lx = (t % P.tiles_x) * 8u + (w & 7u);
     const uint32_t ly = (t / P.tiles_x) * 8u + (w >> 3);
     if (lx >= P.band_w || ly >= P.band_h) return;   // ragged edge: stays NEED_PIXEL, refetches
-    const uint32_t gx = P.off_x + lx;   // shader.rgen:40
-    const uint32_t gy = P.rows ? P.rows[ly] : P.off_y + ly;
+    if (per_lane) seed = tile_pixel_seed(P, t, w);
     ps.px = lx | (ly << 16);
-    ps.pixel_seed = tea(tea(P.seed_local ? lx : gx, P.seed_local ? ly : gy), P.number);
+    ps.pixel_seed = seed;
     ps.seed = ps.pixel_seed;
     ps.s = 0;
     ps.segs = 0;

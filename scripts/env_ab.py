@@ -1,0 +1,44 @@
+#!/usr/bin/env python3
+"""A/B of a per-launch environment knob in one process, interleaved rounds, full 1080p frames:
+every setting must render the same image. Usage:
+  python scripts/env_ab.py VAR spp[,spp...] name=value [name=value ...]   (value '-' = unset)"""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, "ray-tracing-gpu-vulkan_amd")
+import torch  # noqa: E402
+import rtvk  # noqa: E402
+
+W, H = 1920, 1080
+var = sys.argv[1]
+spps = [int(x) for x in sys.argv[2].split(",")]
+settings = dict(a.split("=", 1) for a in sys.argv[3:])
+r = rtvk.Renderer(0)
+r.set_scene(rtvk.generateRandomScene())
+acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+for spp in spps:
+    rci = rtvk.canonical_render_call_info(spp, W, H)
+    times = {k: [] for k in settings}
+    ref = None
+    for rnd in range(6):
+        for k, v in settings.items():
+            if v == "-":
+                os.environ.pop(var, None)
+            else:
+                os.environ[var] = v
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            r.render_device(rci, acc, out, options=rtvk.make_options())
+            e1.record()
+            torch.cuda.synchronize()
+            if rnd == 0:
+                img = acc.cpu().numpy()
+                if ref is None:
+                    ref = img
+                assert np.array_equal(img, ref), f"{var}={v} changed the image"
+            else:
+                times[k].append(e0.elapsed_time(e1))
+    print(f"spp {spp}: " + ", ".join(f"{k} {np.median(v):.2f} ms" for k, v in times.items()), flush=True)
