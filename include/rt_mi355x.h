@@ -117,7 +117,9 @@ int rt_context_destroy(rt_context* ctx);
 /* Uploads `count` spheres (host memory) and builds the closest-hit structure: a binned-SAH tree
  * built on the host for scenes of up to 4096 spheres (the cheaper walk), the parallel device
  * LBVH build (rt_build.hip) above that. RT_BVH_BUILD=gpu|sah|morton forces one builder (A/B).
- * Returns after the build. */
+ * `spheres` may be reused as soon as it returns. The new scene is ordered on `stream`: launches
+ * already queued on `stream` render the old one (a host build runs while they execute, the
+ * upload is queued behind them); launches on other streams are waited for first. */
 int rt_set_scene(rt_context* ctx, const Sphere* spheres, uint32_t count, void* stream);
 /* As rt_set_scene, spheres already in DEVICE memory (read during the call only). */
 int rt_set_scene_device(rt_context* ctx, const Sphere* d_spheres, uint32_t count, void* stream);

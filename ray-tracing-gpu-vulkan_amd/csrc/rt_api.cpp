@@ -67,6 +67,17 @@ struct rt_context {
     rt::BuildWorkspace ws;
     Sphere* d_spheres = nullptr;
     uint32_t d_spheres_cap = 0;
+    // Host-built scenes: every device array lives in one device blob, rewritten in stream order
+    // by one copy from a pinned staging buffer (two, alternating, each guarded by the event of
+    // its last copy), so rt_set_scene builds the next frame's tree on the host while the
+    // previous frame still renders (no device-wide sync, no per-frame hipMalloc/hipFree).
+    void* blob = nullptr;
+    size_t blob_cap = 0;
+    void* stage[2] = {nullptr, nullptr};
+    size_t stage_cap[2] = {0, 0};
+    hipEvent_t stage_ev[2] = {nullptr, nullptr};
+    bool stage_used[2] = {false, false};
+    int stage_cur = 0;
 };
 
 namespace {
@@ -211,6 +222,56 @@ void free_scene(rt_context* ctx) {
     ctx->scene_allocs.clear();
     ctx->scene = rt::DeviceScene{};
 }
+
+// One device blob for a host-built scene (rt_context::blob): add() the arrays, then commit()
+// packs them into a pinned staging buffer and issues one stream-ordered copy.
+class BlobUpload {
+  public:
+    template <typename T>
+    void add(const std::vector<T>& v, T** dst) {
+        *dst = nullptr;
+        if (v.empty()) return;
+        parts_.push_back(Part{v.data(), v.size() * sizeof(T), total_, reinterpret_cast<void**>(dst)});
+        total_ += (v.size() * sizeof(T) + 255u) & ~size_t(255);
+    }
+    int commit(rt_context* ctx, hipStream_t st) {
+        if (total_ == 0) return RT_OK;
+        const int k = ctx->stage_cur;
+        if (ctx->stage_used[k]) RT_HIP(hipEventSynchronize(ctx->stage_ev[k]));   // its last copy is done
+        if (ctx->stage_cap[k] < total_) {
+            if (ctx->stage[k]) RT_HIP(hipHostFree(ctx->stage[k]));
+            ctx->stage[k] = nullptr;
+            ctx->stage_cap[k] = 0;
+            const size_t cap = total_ + total_ / 4;
+            RT_HIP(hipHostMalloc(&ctx->stage[k], cap, hipHostMallocDefault));
+            ctx->stage_cap[k] = cap;
+        }
+        if (!ctx->stage_ev[k]) RT_HIP(hipEventCreateWithFlags(&ctx->stage_ev[k], hipEventDisableTiming));
+        uint8_t* h = static_cast<uint8_t*>(ctx->stage[k]);
+        for (const Part& p : parts_) std::memcpy(h + p.off, p.src, p.bytes);
+        if (ctx->blob_cap < total_) {   // grow: the old blob may still be read by earlier launches
+            RT_HIP(hipDeviceSynchronize());
+            if (ctx->blob) RT_HIP(hipFree(ctx->blob));
+            ctx->blob = nullptr;
+            ctx->blob_cap = 0;
+            const size_t cap = total_ + total_ / 4;
+            RT_HIP(hipMalloc(&ctx->blob, cap));
+            ctx->blob_cap = cap;
+        }
+        uint8_t* d = static_cast<uint8_t*>(ctx->blob);
+        RT_HIP(hipMemcpyAsync(d, h, total_, hipMemcpyHostToDevice, st));
+        RT_HIP(hipEventRecord(ctx->stage_ev[k], st));
+        ctx->stage_used[k] = true;
+        ctx->stage_cur = k ^ 1;
+        for (const Part& p : parts_) *p.dst = d + p.off;
+        return RT_OK;
+    }
+
+  private:
+    struct Part { const void* src; size_t bytes, off; void** dst; };
+    std::vector<Part> parts_;
+    size_t total_ = 0;
+};
 
 template <typename T>
 int upload(rt_context* ctx, const std::vector<T>& v, T** dst, hipStream_t st) {
@@ -399,6 +460,11 @@ int rt_context_destroy(rt_context* ctx) {
     free_scene(ctx);
     rt::build_release(ctx->ws);
     rt::schedule_release(ctx->sched);
+    if (ctx->blob) (void)hipFree(ctx->blob);
+    for (int k = 0; k < 2; k++) {
+        if (ctx->stage[k]) (void)hipHostFree(ctx->stage[k]);
+        if (ctx->stage_ev[k]) (void)hipEventDestroy(ctx->stage_ev[k]);
+    }
     if (ctx->d_spheres) (void)hipFree(ctx->d_spheres);
     if (ctx->counters) (void)hipFree(ctx->counters);
     delete ctx;
@@ -413,8 +479,13 @@ namespace {
 // the alternative walk layouts (ordered two-wide, compact binary16 nodes).
 int set_scene_host(rt_context* ctx, const Sphere* spheres, uint32_t count, hipStream_t st, bool sah) {
     try {
-        free_scene(ctx);
+        if (ctx->gpu_tree || !ctx->scene_allocs.empty()) {   // leaving a device-built scene
+            RT_HIP(hipDeviceSynchronize());
+            free_scene(ctx);
+        }
+        ctx->scene = rt::DeviceScene{};
         ctx->gpu_tree = false;
+        BlobUpload up;
         std::vector<rt::GeomRec> geom(count);
         std::vector<float> radius(count);
         std::vector<rt::MatRec> mat(count);
@@ -437,12 +508,12 @@ int set_scene_host(rt_context* ctx, const Sphere* spheres, uint32_t count, hipSt
         rt::build_lbvh_host(spheres, count, bvh, sah);
         rt::DeviceScene& d = ctx->scene;
         d.n_spheres = count;
-        if (int rc = upload(ctx, geom, &d.geom, st)) return rc;
-        if (int rc = upload(ctx, radius, &d.radius, st)) return rc;
+        up.add(geom, &d.geom);
+        up.add(radius, &d.radius);
         d.small_rmax = bvh.small_rmax;
-        if (int rc = upload(ctx, mat, &d.mat, st)) return rc;
+        up.add(mat, &d.mat);
         d.n_big = uint32_t(bvh.big_ids.size());
-        if (int rc = upload(ctx, bvh.big_ids, &d.big_ids, st)) return rc;
+        up.add(bvh.big_ids, &d.big_ids);
         d.n_nodes = uint32_t(bvh.nodes.size());
         d.n_leaf = uint32_t(bvh.leaf_ids.size());
         // leaf ids are read as uint4: pad to a multiple of 4
@@ -461,7 +532,7 @@ int set_scene_host(rt_context* ctx, const Sphere* spheres, uint32_t count, hipSt
         pad_nodes(ctx->nodes_host, bvh.nodes, ctx->nodes2_host, bvh.nodes2, pad_for(ctx->pad_radius));
         std::vector<rt::BvhNode> oct;
         make_octant_orders(bvh.nodes, oct);
-        if (int rc = upload(ctx, oct, &d.nodes_oct, st)) return rc;
+        up.add(oct, &d.nodes_oct);
         const size_t lds = size_t(2 * d.n_nodes + d.n_leaf + (d.n_leaf + 3) / 4) * 16;
         ctx->lds_bytes = (d.n_nodes && lds <= kMaxLdsBvhBytes) ? lds : 0;
         const size_t lds_scene = lds + size_t(count) * 48u;
@@ -470,20 +541,19 @@ int set_scene_host(rt_context* ctx, const Sphere* spheres, uint32_t count, hipSt
         const size_t lds16 = size_t(d.n_nodes + d.n_leaf + (d.n_leaf + 3) / 4) * 16;
         ctx->lds16_bytes = 0;
         if (make_nodes16(bvh.nodes, n16) && lds16 <= kMaxLdsBvhBytes) {
-            if (int rc = upload(ctx, n16, &d.nodes16, st)) return rc;
+            up.add(n16, &d.nodes16);
             ctx->lds16_bytes = lds16;
         }
         d.n_nodes2 = uint32_t(bvh.nodes2.size());
         d.root2 = bvh.root2;
         d.depth2 = bvh.depth2;
-        if (int rc = upload(ctx, bvh.nodes2, &d.nodes2, st)) return rc;
+        up.add(bvh.nodes2, &d.nodes2);
         const size_t lds2 = size_t(4 * d.n_nodes2 + d.n_leaf + (d.n_leaf + 3) / 4) * 16;
         ctx->lds2_bytes = (d.n_leaf && lds2 <= kMaxLdsBvh2Bytes) ? lds2 : 0;
-        if (int rc = upload(ctx, bvh.nodes, &d.nodes, st)) return rc;
-        if (int rc = upload(ctx, bvh.leaf_geom, &d.leaf_geom, st)) return rc;
-        if (int rc = upload(ctx, bvh.leaf_ids, &d.leaf_ids, st)) return rc;
-        RT_HIP(hipStreamSynchronize(st));  // host vectors die at return
-        return RT_OK;
+        up.add(bvh.nodes, &d.nodes);
+        up.add(bvh.leaf_geom, &d.leaf_geom);
+        up.add(bvh.leaf_ids, &d.leaf_ids);
+        return up.commit(ctx, st);   // packs the host vectors before they die
     } catch (const std::exception& e) {
         return fail(RT_ERR_OUT_OF_MEMORY, e.what());
     }
@@ -585,9 +655,12 @@ int rt_set_scene(rt_context* ctx, const Sphere* spheres, uint32_t count, void* s
     if (int rc = check_scene_args(ctx, spheres, count)) return rc;
     DeviceGuard g(ctx->device);
     hipStream_t st = static_cast<hipStream_t>(stream);
-    RT_HIP(hipStreamSynchronize(st));  // previous launches may still read the old scene
+    // Launches on another stream may still read the old scene: wait for them. Launches on `st`
+    // are ordered before the new scene's upload (the host build overlaps them).
+    if (ctx->last_stream != st) RT_HIP(hipStreamSynchronize(ctx->last_stream));
     const Builder b = pick_builder(count);
     if (b != Builder::GPU) return set_scene_host(ctx, spheres, count, st, b == Builder::HOST_SAH);
+    RT_HIP(hipStreamSynchronize(st));  // the device builder frees and rebuilds in place
     if (int rc = stage_spheres(ctx, spheres, count, st)) return rc;
     return set_scene_gpu(ctx, ctx->d_spheres, count, st, false);
 }

@@ -98,34 +98,6 @@ __device__ __forceinline__ void test_sphere(float cx, float cy, float cz, float 
     }
 }
 
-// LBVH leaf sphere: record = (center, radius); r^2 is formed here exactly as the host forms it
-// for brute force (one rounding), so results agree bit for bit. The sphere index is read from
-// ids[slot] only when the quadratic reports (tie-break and result), both in the rare branch.
-__device__ __forceinline__ void test_leaf_sphere(float4 sp, const uint32_t* __restrict__ ids,
-                                                 uint32_t slot, V3 o, V3 d, V3 inv, float a,
-                                                 float& best, uint32_t& bi, float& limit,
-                                                 float cull_abs, float cull_rel) {
-    const float rr = sp.w * sp.w;
-    const float ocx = o.x - sp.x, ocy = o.y - sp.y, ocz = o.z - sp.z;
-    const float b = __builtin_fmaf(ocz, d.z, __builtin_fmaf(ocy, d.y, ocx * d.x));
-    const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - rr;
-    const float D = __builtin_fmaf(b, b, -(a * c));
-    if (D >= 0.0f) {
-        const float sq = __builtin_sqrtf(D);
-        const float t1 = (-b - sq) / a;
-        const float t2 = (-b + sq) / a;
-        const float t = (t1 >= T_MIN) ? t1 : t2;
-        if (t >= T_MIN && t <= best) {
-            const uint32_t id = ids[slot];
-            if ((t < best || id < bi) && aabb_hit(sp.x, sp.y, sp.z, sp.w, o, inv)) {
-                best = t;
-                bi = id;
-                limit = fminf(__builtin_fmaf(t, cull_rel, t + cull_abs), 10000.0f);
-            }
-        }
-    }
-}
-
 // Four spheres at once (a leaf, or a batch of big spheres): the discriminants of all four are
 // computed branch-free, then each lane loops over only ITS candidates (D >= 0). Inside the loop
 // sit the expensive exact parts (correctly rounded sqrt and divide, the AABB gate); t2 is
@@ -170,26 +142,6 @@ __device__ __forceinline__ void test4(const float4 s0, const float4 s1, const fl
                     limit = fminf(__builtin_fmaf(t, cull_rel, t + cull_abs), 10000.0f);
                 }
             }
-        }
-    }
-}
-
-// test_sphere with the radius already in hand (big spheres: loaded through the scalar path).
-__device__ __forceinline__ void test_sphere_r(float cx, float cy, float cz, float rr, float rad, V3 o,
-                                              V3 d, V3 inv, float a, uint32_t id, float& best,
-                                              uint32_t& bi) {
-    const float ocx = o.x - cx, ocy = o.y - cy, ocz = o.z - cz;
-    const float b = __builtin_fmaf(ocz, d.z, __builtin_fmaf(ocy, d.y, ocx * d.x));
-    const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - rr;
-    const float D = __builtin_fmaf(b, b, -(a * c));
-    if (D >= 0.0f) {
-        const float sq = __builtin_sqrtf(D);
-        const float t1 = (-b - sq) / a;
-        const float t2 = (-b + sq) / a;
-        const float t = (t1 >= T_MIN) ? t1 : t2;
-        if (t >= T_MIN && (t < best || (t == best && id < bi)) && aabb_hit(cx, cy, cz, rad, o, inv)) {
-            best = t;
-            bi = id;
         }
     }
 }
