@@ -403,3 +403,23 @@ def test_chunked_refill_same_image(rtvk, renderer, torch, oracle, reserve):
             os.environ.pop("RT_REFILL_RESERVE", None)
         else:
             os.environ["RT_REFILL_RESERVE"] = prev
+
+
+def test_scene_swap_between_queued_frames(rtvk, renderer, torch, oracle):
+    """rt_set_scene does not wait for queued frames: a frame queued before the call renders the
+    old scene, one queued after renders the new one (upload in stream order), over four frames
+    so both pinned staging buffers are reused."""
+    W, H, spp = 96, 64, 2
+    scenes = [oracle.generate_scene(t) for t in (0.0, 1.0, 2.0, 0.5)]
+    rci = oracle.render_call_info(spp, W, H)
+    rci_c = rtvk.RenderCallInfo.from_buffer_copy(rci.tobytes())
+    accs = [torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") for _ in scenes]
+    outs = [torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") for _ in scenes]
+    torch.cuda.synchronize()
+    for sc, a, o in zip(scenes, accs, outs):
+        renderer.set_scene(sc)
+        renderer.render_device(rci_c, a, o, options=rtvk.make_options())
+    torch.cuda.synchronize()
+    for sc, a, o in zip(scenes, accs, outs):
+        ra, ro, _ = oracle.render(sc, rci, W, H)
+        assert_same(a.cpu().numpy(), o.cpu().numpy(), ra, ro)
