@@ -871,6 +871,9 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
         if (const char* e = std::getenv("RT_REFILL_RESERVE")) reserve = std::strtoull(e, nullptr, 10);
         P.n_chunk_units = 0;
         if (P.tile_cost && P.n_units > reserve) P.n_chunk_units = uint32_t((P.n_units - reserve) & ~uint64_t(63));
+        P.first_chunks = uint32_t(std::min<uint64_t>(uint64_t(grid) * blk / 64u, P.n_chunk_units / 64u));
+        if (P.first_chunks) RT_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&ctx->counters->work_head),
+                                                     int(P.first_chunks * 64u), 1, st));
     }
     RT_HIP(rt::launch_trace(P, accel, count, grid, lds, st));
     ctx->last_stream = st;

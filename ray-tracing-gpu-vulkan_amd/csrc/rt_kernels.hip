@@ -35,6 +35,7 @@ __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 // Diagnostic build only (-DRT_STAMPS): wave-level s_memtime phase stamps, summed per wave and
 // added to Counters::stamp[] at exit (cdna_hip_programming.md §7, In-kernel stamps). The shipped
 // build compiles every STAMP() to nothing.
+struct Stamps { unsigned long long acc[8], t; uint32_t cur; };
 #ifdef RT_STAMPS
 #define STAMP(k)                                                                               \
     do {                                                                                       \
@@ -42,24 +43,25 @@ __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
         unsigned long long t_;                                                                 \
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");           \
         __builtin_amdgcn_sched_barrier(0);                                                     \
-        stamp_acc[stamp_cur] += t_ - stamp_t;                                                  \
-        stamp_t = t_;                                                                          \
-        stamp_cur = (k);                                                                       \
+        stamps.acc[stamps.cur] += t_ - stamps.t;                                               \
+        stamps.t = t_;                                                                         \
+        stamps.cur = (k);                                                                      \
     } while (0)
 #define STAMP_DECL                                                                             \
-    unsigned long long stamp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, stamp_t = 0;                   \
-    uint32_t stamp_cur = 7;                                                                    \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_t)::"memory")
+    Stamps stamps = {{0, 0, 0, 0, 0, 0, 0, 0}, 0, 7};                                          \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamps.t)::"memory")
 #define STAMP_FLUSH                                                                            \
     do {                                                                                       \
         STAMP(7);                                                                              \
         if (lane_id() == 0)                                                                    \
-            for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&P.counters->stamp[k_], stamp_acc[k_]);   \
+            for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&P.counters->stamp[k_], stamps.acc[k_]);  \
     } while (0)
+#define STAMP_ARG , stamps
 #else
 #define STAMP(k) do {} while (0)
-#define STAMP_DECL do {} while (0)
+#define STAMP_DECL Stamps stamps
 #define STAMP_FLUSH do {} while (0)
+#define STAMP_ARG , stamps
 #endif
 
 // Driver traversal test for one sphere's AABB (src/ray_trace.cpp:586-596: center -/+ radius)
@@ -190,6 +192,25 @@ struct Path {
     double sx, sy, sz;     // dvec3 sum (shader.rgen:55)
 };
 
+// Global load of a rarely taken branch, waited for at once. vmcnt counts loads and stores alike
+// (gfx9): a load left pending across a branch makes the compiler wait vmcnt(0) at the loop head
+// (the register is reused there), which then also waits for the pixel stores still in flight —
+// about 10 us per finished pixel. Waiting here, inside the branch, keeps the head
+// free of it.
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef const volatile __attribute__((address_space(1))) uint32_t* GlobalVU32;
+typedef const volatile __attribute__((address_space(1))) f4v* GlobalVF4;
+__device__ __forceinline__ uint32_t load_now(const uint32_t* p) {
+    const uint32_t v = *(GlobalVU32)p;
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), expcnt/lgkmcnt untouched
+    return v;
+}
+__device__ __forceinline__ float4 load_now4(const float4* p) {
+    const f4v v = *(GlobalVF4)p;
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
 // Pixel refill: lanes in `st == ST_NEED_PIXEL` take the next units of the device work counter
 // (one atomic per wave, ranks from the ballot). Units are pixels in 8x8-tile order.
 __device__ __forceinline__ void refill(const rt::TraceParams& P, uint32_t lane, uint32_t& st,
@@ -204,20 +225,20 @@ __device__ __forceinline__ void refill(const rt::TraceParams& P, uint32_t lane, 
     if (st != ST_NEED_PIXEL) return;
     const uint32_t u = base + __popcll(need & ((1ull << lane) - 1ull));
     if (u >= P.n_units) { st = ST_RETIRED; return; }
-    const uint32_t t = P.tile_order ? P.tile_order[u >> 6] : (u >> 6), w = u & 63u;
+    const uint32_t t = P.tile_order ? load_now(P.tile_order + (u >> 6)) : (u >> 6), w = u & 63u;
     const uint32_t lx = (t % P.tiles_x) * 8u + (w & 7u);
     const uint32_t ly = (t / P.tiles_x) * 8u + (w >> 3);
     if (lx >= P.band_w || ly >= P.band_h) return;   // ragged edge: stays NEED_PIXEL, refetches
     // shader.rgen:40
     const uint32_t gx = P.off_x + lx;
-    const uint32_t gy = P.rows ? P.rows[ly] : P.off_y + ly;
+    const uint32_t gy = P.rows ? load_now(P.rows + ly) : P.off_y + ly;
     ps.px = lx | (ly << 16);
     ps.pixel_seed = tea(tea(P.seed_local ? lx : gx, P.seed_local ? ly : gy), P.number);
     ps.seed = ps.pixel_seed;
     ps.s = 0;
     ps.segs = 0;
     if (P.accumulate) {  // shader.rgen:53-55
-        const float4 acc = reinterpret_cast<const float4*>(P.accum)[size_t(ly) * P.band_w + lx];
+        const float4 acc = load_now4(reinterpret_cast<const float4*>(P.accum) + size_t(ly) * P.band_w + lx);
         ps.sx = acc.x; ps.sy = acc.y; ps.sz = acc.z;
     } else {
         ps.sx = ps.sy = ps.sz = 0.0;
@@ -235,21 +256,24 @@ __device__ __forceinline__ void refill(const rt::TraceParams& P, uint32_t lane, 
 // tile phase is exhausted. `seed` (per lane) is the pixel seed of the tile's pixel `lane`: the
 // 64 seeds of a tile are computed together when the tile is taken (two TEAs, 16 rounds each,
 // with every lane busy) instead of one lane at a time as its pixel starts.
-struct WaveChunk { uint32_t next = 0, end = 0, tile = 0; bool dry = false; uint32_t seed = 0; };
+// `done` once the pixel-by-pixel units are exhausted too: later refills retire lanes without
+// touching the counter (one address: every atomic on it queues behind the others).
+struct WaveChunk { uint32_t next = 0, end = 0, tile = 0; bool dry = false, done = false; uint32_t seed = 0; };
 
 // shader.rgen:40 seed of pixel w (0..63) of 8x8 tile t of the band.
 __device__ __forceinline__ uint32_t tile_pixel_seed(const rt::TraceParams& P, uint32_t t, uint32_t w) {
     const uint32_t lx = (t % P.tiles_x) * 8u + (w & 7u);
     const uint32_t ly = (t / P.tiles_x) * 8u + (w >> 3);
     const uint32_t gx = P.off_x + lx;
-    const uint32_t gy = P.rows ? P.rows[ly < P.band_h ? ly : P.band_h - 1u] : P.off_y + ly;   // ragged edge: unused
+    const uint32_t gy = P.rows ? load_now(P.rows + (ly < P.band_h ? ly : P.band_h - 1u)) : P.off_y + ly;   // ragged edge: unused
     return tea(tea(P.seed_local ? lx : gx, P.seed_local ? ly : gy), P.number);
 }
 
 __device__ __forceinline__ void refill_chunked(const rt::TraceParams& P, uint32_t lane, uint32_t& st,
-                                               Path& ps, WaveChunk& ch) {
+                                               Path& ps, WaveChunk& ch, Stamps& stamps) {
     const unsigned long long need = __ballot(st == ST_NEED_PIXEL);
     if (!need) return;
+    STAMP(5);
     const uint32_t cnt = __popcll(need);
     const uint32_t rank = __popcll(need & ((1ull << lane) - 1ull));
     const uint32_t avail = ch.end - ch.next;
@@ -261,12 +285,13 @@ __device__ __forceinline__ void refill_chunked(const rt::TraceParams& P, uint32_
     if (cnt <= avail) {
         ch.next += cnt;
     } else {
+        STAMP(6);
         const uint32_t rest = cnt - avail;   // lanes beyond the current tile's pixels
         uint32_t nb = 0xffffffffu, nt = 0;
         if (!ch.dry) {
             if (int(lane) == leader) {
                 nb = atomicAdd(&P.counters->work_head, 64u);
-                if (nb < P.n_chunk_units) nt = P.tile_order ? P.tile_order[nb >> 6] : (nb >> 6);
+                if (nb < P.n_chunk_units) nt = P.tile_order ? load_now(P.tile_order + (nb >> 6)) : (nb >> 6);
             }
             nb = __shfl(nb, leader);
             nt = __shfl(nt, leader);
@@ -280,17 +305,20 @@ __device__ __forceinline__ void refill_chunked(const rt::TraceParams& P, uint32_
             ch.end = nb + 64u;
             ch.tile = nt;
         } else {
-            uint32_t tb = 0;
-            if (int(lane) == leader) tb = atomicAdd(&P.counters->work_tail, rest);
-            tb = __shfl(tb, leader);
-            if (rank >= avail) { u = P.n_chunk_units + tb + (rank - avail); per_lane = true; }
+            uint32_t tb = P.n_units;   // exhausted: the lanes retire
+            if (!ch.done) {
+                if (int(lane) == leader) tb = atomicAdd(&P.counters->work_tail, rest);
+                tb = P.n_chunk_units + __shfl(tb, leader);
+                if (tb + rest >= P.n_units) ch.done = true;
+            }
+            if (rank >= avail) { u = tb + (rank - avail); per_lane = true; }
             ch.next = ch.end;
         }
     }
     if (st != ST_NEED_PIXEL) return;
     if (per_lane) {
         if (u >= P.n_units) { st = ST_RETIRED; return; }
-        t = P.tile_order ? P.tile_order[u >> 6] : (u >> 6);
+        t = P.tile_order ? load_now(P.tile_order + (u >> 6)) : (u >> 6);
     }
     const uint32_t w = u & 63u;
     const uint32_t lx = (t % P.tiles_x) * 8u + (w & 7u);
@@ -303,12 +331,25 @@ __device__ __forceinline__ void refill_chunked(const rt::TraceParams& P, uint32_
     ps.s = 0;
     ps.segs = 0;
     if (P.accumulate) {  // shader.rgen:53-55
-        const float4 acc = reinterpret_cast<const float4*>(P.accum)[size_t(ly) * P.band_w + lx];
+        const float4 acc = load_now4(reinterpret_cast<const float4*>(P.accum) + size_t(ly) * P.band_w + lx);
         ps.sx = acc.x; ps.sy = acc.y; ps.sz = acc.z;
     } else {
         ps.sx = ps.sy = ps.sz = 0.0;
     }
     st = ST_NEED_SAMPLE;
+}
+
+// shader.rgen:61-66: store the finished pixel (dvec3 sum rounded to float, rgba8 resolve).
+__device__ __forceinline__ void store_pixel(const rt::TraceParams& P, const Path& ps) {
+    const uint32_t lx = ps.px & 0xffffu, ly = ps.px >> 16;
+    const float s0 = float(ps.sx), s1 = float(ps.sy), s2 = float(ps.sz);
+    const size_t texel = size_t(ly) * P.band_w + lx;
+    reinterpret_cast<float4*>(P.accum)[texel] = make_float4(s0, s1, s2, 1.0f);
+    const float spp = float(P.spp);
+    const uint32_t r8 = unorm8(__builtin_sqrtf(s0 / spp));
+    const uint32_t g8 = unorm8(__builtin_sqrtf(s1 / spp));
+    const uint32_t b8 = unorm8(__builtin_sqrtf(s2 / spp));
+    P.out[texel] = r8 | (g8 << 8) | (b8 << 16) | (255u << 24);
 }
 
 // shader.rgen:56-58 + 107-115: next camera ray of the lane's pixel. Returns false (and stores
@@ -317,18 +358,11 @@ __device__ __forceinline__ bool start_sample(const rt::TraceParams& P, const Cam
                                              V3& o, V3& d) {
     const uint32_t lx = ps.px & 0xffffu, ly = ps.px >> 16;
     if (ps.s >= P.spp) {
-        const float s0 = float(ps.sx), s1 = float(ps.sy), s2 = float(ps.sz);
-        const size_t texel = size_t(ly) * P.band_w + lx;
-        reinterpret_cast<float4*>(P.accum)[texel] = make_float4(s0, s1, s2, 1.0f);
-        const float spp = float(P.spp);
-        const uint32_t r8 = unorm8(__builtin_sqrtf(s0 / spp));
-        const uint32_t g8 = unorm8(__builtin_sqrtf(s1 / spp));
-        const uint32_t b8 = unorm8(__builtin_sqrtf(s2 / spp));
-        P.out[texel] = r8 | (g8 << 8) | (b8 << 16) | (255u << 24);
+        store_pixel(P, ps);
         return false;
     }
     const uint32_t gx = P.off_x + lx;
-    const uint32_t gy = P.rows ? P.rows[ly] : P.off_y + ly;
+    const uint32_t gy = P.rows ? load_now(P.rows + ly) : P.off_y + ly;
     if (P.rng_counter) ps.seed = tea(ps.pixel_seed, P.sample_base + ps.s);
     float ux = float(gx) + rnd(ps.seed);
     float uy = float(gy) + rnd(ps.seed);
@@ -489,7 +523,6 @@ __device__ __forceinline__ bool node_hit(const float4 A, const float4 B, const R
 }
 
 // 16-B load from an LDS address held in a register (ds_read_b128 addr, no base add).
-typedef float f4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 lds_f4(uint32_t addr) {
     const f4v v = *(const __attribute__((address_space(3))) f4v*)(uintptr_t)addr;
     return make_float4(v.x, v.y, v.z, v.w);
@@ -891,6 +924,14 @@ __device__ __forceinline__ uint32_t pool_take(PoolCtl* ctl, uint32_t* pool, uint
 // LBVH kernel, classic form: one segment per lane per loop iteration; the wave's walk loop runs
 // until its longest walk ends. Stamp slots: 0 refill+sample start, 1 ray setup (big spheres),
 // 2 LBVH walk, 3 shading, 7 other. POOL: tail compaction through the block's LDS pool.
+// Finished pixel: its chain length (traced segments) feeds the next launch's hand-out order.
+__device__ __forceinline__ void record_tile_cost(const rt::TraceParams& P, const Path& ps) {
+    if (!P.tile_cost) return;
+    const uint32_t lx = ps.px & 0xffffu, ly = ps.px >> 16;
+    uint32_t* c = &P.tile_cost[(ly >> 3) * P.tiles_x + (lx >> 3)];
+    if (P.tile_cost_sum) atomicAdd(c, ps.segs); else atomicMax(c, ps.segs);
+}
+
 // ---------------------------------------------------------------------------------------------
 template <bool COUNT, bool NODE16, bool POOL, int LAYOUT>
 __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const float4* __restrict__ nodes4,
@@ -908,13 +949,23 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
     unsigned long long wave_iters = 0;
     bool saw_dry = false;
     WaveChunk ch;
+    {   // the first tiles go out by wave id, not through the counter (host starts it past them):
+        // 16 Ki waves asking one address at once would queue for ~0.1 ms
+        const uint32_t wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+        if (wid < P.first_chunks) {
+            ch.next = wid * 64u;
+            ch.end = ch.next + 64u;
+            ch.tile = P.tile_order ? load_now(P.tile_order + wid) : wid;
+            ch.seed = tile_pixel_seed(P, ch.tile, lane);
+        }
+    }
     // launch telemetry (3 atomics per wave): first start, pixel queue dry, last exit
     if (lane == 0) atomicMin(&P.counters->t_first, __builtin_amdgcn_s_memrealtime());
     STAMP_DECL;
     for (;;) {
         STAMP(0);
         if (!POOL || !saw_dry) {
-            if (P.n_chunk_units) refill_chunked(P, lane, st, ps, ch);
+            if (P.n_chunk_units) refill_chunked(P, lane, st, ps, ch STAMP_ARG);
             else refill(P, lane, st, ps);
         } else if (st == ST_NEED_PIXEL) {
             st = ST_RETIRED;   // the queue never refills once dry
@@ -924,6 +975,7 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
             if (lane == 0) atomicMin(&P.counters->t_dry, __builtin_amdgcn_s_memrealtime());
             if (POOL && st == ST_NEED_PIXEL) st = ST_RETIRED;
         }
+        STAMP(4);
         if (POOL && saw_dry) {
             const unsigned long long held = __ballot(st == ST_TRACING || st == ST_NEED_SAMPLE);
             uint32_t n_held = __popcll(held);
@@ -980,13 +1032,9 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
             if (start_sample(P, cam, ps, r.o, r.d)) {
                 st = ST_TRACING;
                 n_smp++;
-            } else {   // pixel done: its chain length feeds the next launch's hand-out order
+            } else {   // pixel done (spp = 0 only: others finish at their last sample's end)
                 st = ST_NEED_PIXEL;
-                if (P.tile_cost) {
-                    const uint32_t lx = ps.px & 0xffffu, ly = ps.px >> 16;
-                    uint32_t* c = &P.tile_cost[(ly >> 3) * P.tiles_x + (lx >> 3)];
-                    if (P.tile_cost_sum) atomicAdd(c, ps.segs); else atomicMax(c, ps.segs);
-                }
+                record_tile_cost(P, ps);
             }
         }
         if (__ballot(st == ST_NEED_PIXEL)) continue;   // refill before the next trace
@@ -1019,7 +1067,18 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
         if (st == ST_TRACING) {
             n_seg++;
             ps.segs++;
-            if (!shade(P, geom4, mat4, ps, r.bi, r.best, r.o, r.d)) st = ST_NEED_SAMPLE;
+            if (!shade(P, geom4, mat4, ps, r.bi, r.best, r.o, r.d)) {
+                // The sample ended. After the pixel's last one, store it here rather than at the
+                // next sample start: the lane asks for a pixel at the top of the next iteration
+                // directly, instead of costing its wave one extra pass of the loop head.
+                if (ps.s >= P.spp) {
+                    store_pixel(P, ps);
+                    record_tile_cost(P, ps);
+                    st = ST_NEED_PIXEL;
+                } else {
+                    st = ST_NEED_SAMPLE;
+                }
+            }
         }
     }
     STAMP_FLUSH;
