@@ -139,6 +139,9 @@ def hip_assembler(renderer, stream=None):
     return assemble
 
 
+_force_collective = False   # tests: take the RCCL code path with an emulated all_to_all_single
+
+
 def split_samples(spp: int, world: int) -> list:
     """spp_r of every rank: as even as possible, sum = spp (ranks beyond spp get 0)."""
     return [spp // world + (1 if r < spp % world else 0) for r in range(world)]
@@ -174,11 +177,14 @@ class SampleSplitRenderer:
         self.row0 = [sum(self.rows[:r]) for r in range(self.world)]
         self.n_max = max(self.rows)
         n_mine = self.rows[self.rank]
-        self.recv = torch.empty((self.world, n_mine, width, 4), dtype=torch.float32, device=device)
+        # received slices, rank-major: the collective sees [N * rows, W, 4], the reduction [N, rows, W, 4]
+        self.recv_flat = torch.empty((self.world * n_mine, width, 4), dtype=torch.float32, device=device)
+        self.recv = self.recv_flat.view(self.world, n_mine, width, 4)
         # reduced slice, padded to n_max rows so every rank's gather buffer has one shape
         self.part = torch.zeros((self.n_max, width, 4), dtype=torch.float32, device=device)
         self.part_out = torch.zeros((self.n_max, width, 4), dtype=torch.uint8, device=device)
-        self.gloo = self.world > 1 and dist.get_backend() == "gloo"
+        # gloo has no all_to_all: host staging + one scatter per root (rehearsal / CPU tests)
+        self.gloo = self.world > 1 and dist.get_backend() == "gloo" and not _force_collective
         self.even = all(n == self.n_max for n in self.rows)
         if self.rank == 0 and self.world > 1:
             self.g_accum = torch.zeros((self.world, self.n_max, width, 4), dtype=torch.float32, device=device)
@@ -214,7 +220,7 @@ class SampleSplitRenderer:
                 dist.scatter(hr, hs if q == r else None, src=q)
                 self.recv[q].copy_(hr[:n_mine])
         else:
-            dist.all_to_all_single(self.recv, self.accum, output_split_sizes=[n_mine] * self.world,
+            dist.all_to_all_single(self.recv_flat, self.accum, output_split_sizes=[n_mine] * self.world,
                                    input_split_sizes=self.rows)
         self.reduce(self.recv, self.spp, self.part[:n_mine], self.part_out[:n_mine])
         self._gather(self.part, self.g_accum if r == 0 else None)

@@ -88,11 +88,39 @@ def test_sample_split_partition():
 SPLIT_SPP = 5
 
 
-def _split_worker(rank, world, port, out_path):
+def _emulated_all_to_all_single(output, input, output_split_sizes=None, input_split_sizes=None, **_):
+    """torch.distributed.all_to_all_single's dim-0 split semantics, built from gloo scatters (gloo
+    has no all_to_all): rank r's input chunk q lands in rank q's output chunk r."""
+    world, rank = dist.get_world_size(), dist.get_rank()
+    ins = list(torch.split(input, input_split_sizes, dim=0))
+    outs = list(torch.split(output, output_split_sizes, dim=0))
+    sizes = torch.zeros((world, world), dtype=torch.int64)
+    sizes[rank] = torch.tensor(input_split_sizes)
+    dist.all_reduce(sizes)
+    n_max = int(sizes.max())
+    tail = tuple(input.shape[1:])
+    for src in range(world):
+        buf = torch.zeros((n_max,) + tail, dtype=input.dtype)
+        lst = None
+        if src == rank:
+            lst = []
+            for q in range(world):
+                t = torch.zeros((n_max,) + tail, dtype=input.dtype)
+                t[: ins[q].shape[0]] = ins[q]
+                lst.append(t)
+        dist.scatter(buf, lst, src=src)
+        outs[src].copy_(buf[: int(sizes[src, rank])])
+
+
+def _split_worker(rank, world, port, out_path, force_collective=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle import oracle
+    import rtvk.dist as rd
     from rtvk.dist import SampleSplitRenderer
+    if force_collective:   # the RCCL code path (all_to_all_single, in-place gathers)
+        rd._force_collective = True
+        dist.all_to_all_single = _emulated_all_to_all_single
 
     sc = oracle.generate_scene()
 
@@ -119,14 +147,15 @@ def _split_worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sample_split_world(tmp_path, oracle, world):
+@pytest.mark.parametrize("world,force_collective", [(2, False), (3, False), (2, True), (3, True)])
+def test_sample_split_world(tmp_path, oracle, world, force_collective):
     """Rank r renders split_samples(spp)[r] samples with number = 7 + r; the reduced frame equals
     the rank-ordered float sum of those sub-frames, tonemapped with the full spp."""
     from rtvk.dist import split_samples
     port = _free_port()
     out = str(tmp_path / "img.npz")
-    mp.start_processes(_split_worker, args=(world, port, out), nprocs=world, join=True, start_method="spawn")
+    mp.start_processes(_split_worker, args=(world, port, out, force_collective), nprocs=world, join=True,
+                       start_method="spawn")
     got = np.load(out)
     sc = oracle.generate_scene()
     ref = None
