@@ -186,7 +186,8 @@ class SampleSplitRenderer:
         # gloo has no all_to_all: host staging + one scatter per root (rehearsal / CPU tests)
         self.gloo = self.world > 1 and dist.get_backend() == "gloo" and not _force_collective
         self.even = all(n == self.n_max for n in self.rows)
-        if self.rank == 0 and self.world > 1:
+        self.multi = self.world > 1 or _force_collective   # exchange even at N = 1 (tests)
+        if self.rank == 0 and self.multi:
             self.g_accum = torch.zeros((self.world, self.n_max, width, 4), dtype=torch.float32, device=device)
             self.g_out = torch.zeros((self.world, self.n_max, width, 4), dtype=torch.uint8, device=device)
             if self.even:   # the gather lands in place
@@ -200,7 +201,7 @@ class SampleSplitRenderer:
         """Render this rank's samples, reduce, tonemap, gather. Returns (accum, rgba8) of the whole
         frame on rank 0, None elsewhere."""
         torch, dist = self.torch, self.dist
-        if self.world == 1:
+        if not self.multi:
             self.render_full(self.number, self.spp_r, self.accum, self.out)
             return self.accum, self.out
         if self.spp_r:

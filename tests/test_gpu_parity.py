@@ -423,3 +423,33 @@ def test_scene_swap_between_queued_frames(rtvk, renderer, torch, oracle):
     for sc, a, o in zip(scenes, accs, outs):
         ra, ro, _ = oracle.render(sc, rci, W, H)
         assert_same(a.cpu().numpy(), o.cpu().numpy(), ra, ro)
+
+
+def test_sample_split_rccl_world1(rtvk, renderer, torch, oracle):
+    """The RCCL code path of rtvk.dist.SampleSplitRenderer (all_to_all_single into the flat receive
+    buffer, rt_reduce_resolve, in-place gathers) on a one-rank NCCL group: the frame equals the
+    one-GPU render bit for bit."""
+    import socket
+    import torch.distributed as dist
+    import rtvk.dist as rd
+    W, H, spp = 80, 48, 3
+    sc = oracle.generate_scene()
+    renderer.set_scene(sc)
+    rci = rtvk.RenderCallInfo.from_buffer_copy(oracle.render_call_info(spp, W, H).tobytes())
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        rd._force_collective = True
+        sr = rd.SampleSplitRenderer(W, H, spp, 0, torch.device("cuda", 0),
+                                    rd.hip_full_renderer(renderer, rci, rtvk.make_options()),
+                                    rd.hip_reducer(renderer))
+        acc, out = sr.step()
+        torch.cuda.synchronize()
+    finally:
+        rd._force_collective = False
+        dist.destroy_process_group()
+    ra, ro, _ = oracle.render(sc, oracle.render_call_info(spp, W, H), W, H)
+    assert_same(acc.cpu().numpy(), out.cpu().numpy(), ra, ro)
