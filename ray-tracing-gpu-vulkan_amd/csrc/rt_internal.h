@@ -117,6 +117,7 @@ struct TraceParams {
     uint32_t n_chunk_units;        // LBVH kernels: units [0, n_chunk_units) go out as whole 8x8 tiles
                                    // (one atomic per 64 pixels per wave), the rest pixel by pixel
     uint32_t first_chunks;         // tiles [0, first_chunks) start on wave id = tile rank (no atomic)
+    uint32_t isolate_tiles;        // waves of the first LPT tiles take no further work
     const uint32_t* rows;          // optional global row per band row
     const uint32_t* tile_order;    // optional: hand-out rank -> 8x8 tile index (null: row-major)
     uint32_t* tile_cost;           // optional: per 8x8 tile, traced segments of its most expensive

@@ -957,6 +957,7 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
             ch.end = ch.next + 64u;
             ch.tile = P.tile_order ? load_now(P.tile_order + wid) : wid;
             ch.seed = tile_pixel_seed(P, ch.tile, lane);
+            if (wid < P.isolate_tiles) ch.dry = ch.done = true;   // no work beyond its first tile
         }
     }
     // launch telemetry (3 atomics per wave): first start, pixel queue dry, last exit

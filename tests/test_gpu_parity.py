@@ -453,3 +453,32 @@ def test_sample_split_rccl_world1(rtvk, renderer, torch, oracle):
         dist.destroy_process_group()
     ra, ro, _ = oracle.render(sc, oracle.render_call_info(spp, W, H), W, H)
     assert_same(acc.cpu().numpy(), out.cpu().numpy(), ra, ro)
+
+
+@pytest.mark.parametrize("isolate", ["0", "3", "1000000"])
+def test_isolated_tiles_same_image(rtvk, renderer, torch, oracle, isolate):
+    """Waves starting on the longest-chain tiles that take no further pixels (RT_ISOLATE_TILES,
+    including every wave isolated) render the same image as the oracle; the second launch has
+    the LPT order the isolation needs."""
+    W, H = 136, 72
+    sc = oracle.generate_scene()
+    rci = oracle.render_call_info(2, W, H)
+    ra, ro, _ = oracle.render(sc, rci, W, H)
+    prev = {k: os.environ.get(k) for k in ("RT_ISOLATE_TILES", "RT_REFILL_RESERVE")}
+    os.environ["RT_ISOLATE_TILES"] = isolate
+    os.environ["RT_REFILL_RESERVE"] = "0"
+    try:
+        renderer.set_scene(sc)
+        rci_c = rtvk.RenderCallInfo.from_buffer_copy(rci.tobytes())
+        for _ in range(2):
+            a = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+            o = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+            renderer.render_device(rci_c, a, o, options=rtvk.make_options())
+            torch.cuda.synchronize()
+            assert_same(a.cpu().numpy(), o.cpu().numpy(), ra, ro)
+    finally:
+        for k, v in prev.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
