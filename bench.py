@@ -98,6 +98,12 @@ def main() -> int:
                     help="N>1 work split: samples (each rank renders the frame with spp/N samples and "
                          "stream salt number+rank, row-slice reduction) or strips (8-row strips of the "
                          "one-GPU frame); identical at N=1")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="frames in flight: contexts + streams used round robin, so frame k+1's blocks "
+                         "start on the CUs frame k's tail leaves idle (1 = one frame at a time)")
+    ap.add_argument("--exchange-test", action="store_true",
+                    help="test only: one rank on a one-rank NCCL group still runs the sample-split "
+                         "exchange (RCCL code path on a one-GPU box)")
     args = ap.parse_args()
 
     import numpy as np
@@ -123,11 +129,14 @@ def main() -> int:
         local = local % ndev
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if world > 1 or args.exchange_test:
         if shared:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
+    if args.exchange_test:
+        import rtvk.dist as rtvk_dist
+        rtvk_dist._force_collective = True
 
     if args.config is not None:
         args.width, args.height = (3840, 2160) if args.config == 5 else (1920, 1080)
@@ -135,40 +144,54 @@ def main() -> int:
         args.grid = 158 if args.config == 5 else 11
     W, H, spp = args.width, args.height, args.spp
     accel = abi.RT_ACCEL_BRUTE if args.accel == "brute" else abi.RT_ACCEL_LBVH
-    renderer = rtvk.Renderer(local)
     scene = rtvk.generateRandomScene(0.0, args.grid)
-    t_scene = time.perf_counter()
-    renderer.set_scene(scene)
-    t_scene = time.perf_counter() - t_scene
     rci = rtvk.canonical_render_call_info(spp, W, H)
     opts = rtvk.make_options(accel=accel)
     opts.reserved[1] = args.walk
-    stream = torch.cuda.current_stream()
     ev = []
+    split = args.split if (world > 1 or args.exchange_test) else "strips"
 
-    base_render = hip_band_renderer(renderer, rci, opts)
-
-    def timed_render(rows, accum, out):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        base_render(rows, accum, out)
-        e1.record(stream)
-        ev.append((e0, e1))
-
-    split = args.split if world > 1 else "strips"
-    if split == "samples":
-        full_render = hip_full_renderer(renderer, rci, opts)
-
-        def timed_full(number, spp_r, accum, out):
+    def timed(fn):
+        """fn(*a) bracketed by HIP events on the stream it is launched on (the slot's)."""
+        def run(*a):
+            st = torch.cuda.current_stream()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            full_render(number, spp_r, accum, out)
-            e1.record(stream)
+            e0.record(st)
+            fn(*a)
+            e1.record(st)
             ev.append((e0, e1))
+        return run
 
-        dr = SampleSplitRenderer(W, H, spp, rci.number, dev, timed_full, hip_reducer(renderer))
-    else:
-        dr = DistributedRenderer(W, H, dev, timed_render, hip_assembler(renderer))
+    class Slot:
+        """One frame in flight: its own context (scene blob, counters, LPT history), stream and
+        frame buffers; frames go to the slots round robin."""
+        def __init__(self):
+            self.renderer = rtvk.Renderer(local)
+            self.stream = torch.cuda.Stream(device=dev)
+            with torch.cuda.stream(self.stream):
+                if split == "samples":
+                    self.dr = SampleSplitRenderer(W, H, spp, rci.number, dev,
+                                                  timed(hip_full_renderer(self.renderer, rci, opts)),
+                                                  hip_reducer(self.renderer))
+                else:
+                    self.dr = DistributedRenderer(W, H, dev, timed(hip_band_renderer(self.renderer, rci, opts)),
+                                                  hip_assembler(self.renderer))
+
+        def frame(self):
+            # The reference rebuilds its acceleration structure every frame (src/vulkan.h:1020-1059)
+            # and SURVEY.md 8(d) counts the build in the wall clock: rebuild, then render + exchange.
+            # The host build runs while earlier frames render (its upload is queued behind them).
+            with torch.cuda.stream(self.stream):
+                self.renderer.set_scene(scene, stream=self.stream)
+                self.dr.step()
+
+    slots = [Slot() for _ in range(max(1, args.inflight))]
+    renderer, dr = slots[0].renderer, slots[0].dr
+    torch.cuda.synchronize()
+    t_scene = time.perf_counter()
+    renderer.set_scene(scene)
+    torch.cuda.synchronize()
+    t_scene = time.perf_counter() - t_scene
 
     def barrier():
         torch.cuda.synchronize()
@@ -176,15 +199,14 @@ def main() -> int:
             dist.barrier()
         torch.cuda.synchronize()
 
+    n_frames = 0
 
     def frame():
-        # The reference rebuilds its acceleration structure every frame (src/vulkan.h:1020-1059)
-        # and SURVEY.md 8(d) counts the build in the wall clock: rebuild, then render + gather.
-        # The host build of frame k+1 runs while frame k renders (upload queued behind it).
-        renderer.set_scene(scene)
-        dr.step()
+        nonlocal n_frames
+        slots[n_frames % len(slots)].frame()
+        n_frames += 1
 
-    for _ in range(args.warmup):
+    for _ in range(max(args.warmup, len(slots))):   # every slot has rendered once (LPT order)
         frame()
     barrier()
     ev.clear()
@@ -197,6 +219,21 @@ def main() -> int:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if shared else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    kernel_ms_inflight = sum(a.elapsed_time(b) for a, b in ev) / max(1, len(ev))
+    # Kernel duration for the roofline: with frames in flight a launch's events also span the wait
+    # for the CUs the previous frame still holds, so the same launch (this rank's share of the
+    # frame, same slot and LPT order) is timed alone, back to back, right after the timed region.
+    ev.clear()
+    sl0 = slots[0]
+    n_iso = max(2, min(args.steps, 5))
+    for _ in range(n_iso):
+        with torch.cuda.stream(sl0.stream):
+            if split == "samples":
+                if sl0.dr.spp_r:
+                    sl0.dr.render_full(sl0.dr.number, sl0.dr.spp_r, sl0.dr.accum, sl0.dr.out)
+            else:
+                sl0.dr.render_band(sl0.dr.rows, sl0.dr.accum[: sl0.dr.n], sl0.dr.out[: sl0.dr.n])
+        torch.cuda.synchronize()
     kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / max(1, len(ev))
     # the per-frame rebuild alone (host build + upload), outside the timed region
     torch.cuda.synchronize()
@@ -248,6 +285,10 @@ def main() -> int:
                 "unit": "TFLOP/s", "frac": round(achieved / VALU_FP32_PEAK_TFLOPS, 4), "traffic": traffic,
                 "kernel": "rt_trace_lbvh_kernel (octant LDS walk)" if accel == 2 else "rt_trace_brute_kernel",
                 "kernel_ms": round(kernel_ms, 4),
+                "kernel_timing": f"{n_iso} launches of this frame timed alone after the timed region "
+                                 "(HIP events on the launch stream); with frames in flight a launch "
+                                 f"spans {kernel_ms_inflight:.2f} ms including the wait for the previous "
+                                 "frame's CUs",
                 "flop_per_launch": int(flops), "box_tests": int(cs.box_tests * scale),
                 "sphere_tests": int(cs.sphere_tests * scale),
                 "flop_model": "20/box test + 23/sphere test (SURVEY.md 8(d)); counts from the "
@@ -277,7 +318,8 @@ def main() -> int:
                        "width": W, "height": H, "spp": spp, "depth": 50, "spheres": len(scene),
                        "accel": args.accel,
                        "parallelism": (f"sample-split x{world} (number+rank) + rccl all-to-all row reduction "
-                                       "+ gather" if split == "samples" else f"row-strips x{world} + rccl gather")},
+                                       "+ gather" if split == "samples" else f"row-strips x{world} + rccl gather"),
+                       "frames_in_flight": len(slots)},
             "segments_per_sample": round(st.segments / max(1, st.samples), 4),
             "scene_setup_ms": round(t_scene * 1e3, 2),
             "scene_build_ms": round(build_ms, 3),
@@ -296,6 +338,7 @@ def main() -> int:
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         reps = 2
+        stream = torch.cuda.current_stream()
         e0.record(stream)
         for _ in range(reps):
             renderer.render_device(rci, acc, out, options=bopts)
@@ -315,7 +358,8 @@ def main() -> int:
         result["cpu_baseline"] = cpu_baseline(W, H)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    renderer.close()
+    for sl in slots:
+        sl.renderer.close()
     if world > 1:
         dist.destroy_process_group()
     return 0

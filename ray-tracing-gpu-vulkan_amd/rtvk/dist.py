@@ -56,7 +56,8 @@ def max_rows(world: int, height: int, strip: int = STRIP) -> int:
 class DistributedRenderer:
     """One rank's share of a multi-GPU frame.
 
-    render_band(rows_dev, accum_dev, out_dev): renders this rank's rows into [rows, W, 4] buffers.
+    render_band(rows_dev, accum_dev, out_dev): renders this rank's rows into [rows, W, 4] buffers
+    (rows_dev None at one rank: the whole frame, no row map).
     assemble(band_accum, band_out, rows_dev, full_accum, full_out): rank-0 reorder of one rank's
     gathered band into the full image.
     """
@@ -76,7 +77,8 @@ class DistributedRenderer:
         self.nmax = max_rows(self.world, height, strip)
         n = len(self.rows_np)
         # Bands are padded to the largest band so one fixed-size gather moves every rank's rows.
-        self.rows = torch.from_numpy(self.rows_np).to(device)
+        # one rank: the identity map is left out (no per-sample row lookup in the kernel)
+        self.rows = torch.from_numpy(self.rows_np).to(device) if self.world > 1 else None
         self.accum = torch.zeros((self.nmax, width, 4), dtype=torch.float32, device=device)
         self.out = torch.zeros((self.nmax, width, 4), dtype=torch.uint8, device=device)
         self.n = n
@@ -126,7 +128,7 @@ class DistributedRenderer:
 def hip_band_renderer(renderer, rci, options, stream=None):
     """render_band backed by librt_mi355x.so (rt_render_device with a rows map)."""
     def render_band(rows, accum, out):
-        if rows.numel():
+        if rows is None or rows.numel():
             renderer.render_device(rci, accum, out, rows=rows, options=options, stream=stream)
     return render_band
 

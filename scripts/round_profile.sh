@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round profile on the GPU box (outputs under gpurun_out/round/): rocprofv3 kernel-trace stats of
-# the bench command, then one --pmc pass per line of scripts/pmc_quick.txt (kernel-trace only
+# the bench command (one frame in flight, so each launch runs alone and its duration is the
+# kernel's), then one --pmc pass per line of scripts/pmc_quick.txt (kernel-trace only
 # beside --pmc), then the JSON summaries bench.py reads (profiles/pmc_traffic.json,
 # profiles/pmc_valu.json, written in the gpurun_out copy and merged back by the caller).
 # Stops at the first fault-like exit.
@@ -9,8 +10,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/round
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-BARGS=${BENCH_ARGS:-"--steps 20 --warmup 2 --profile"}   # 22 launches: the first (no LPT order yet) barely moves the average
-PARGS=${PMC_BENCH_ARGS:-"--steps 2 --warmup 1 --profile"}
+BARGS=${BENCH_ARGS:-"--steps 20 --warmup 2 --profile --inflight 1"}   # 22 launches: the first (no LPT order yet) barely moves the average
+PARGS=${PMC_BENCH_ARGS:-"--steps 2 --warmup 1 --profile --inflight 1"}
 KEY=${KEY:-lbvh-1920x1080-100spp-grid11-n1}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- \
     python3 bench.py $BARGS > "$OUT/stats.log" 2>&1
