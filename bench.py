@@ -38,31 +38,48 @@ def host_cores() -> int:
     return max(1, min(n, 16))    # the GPU box grants a 16-CPU share
 
 
-def cpu_baseline(width: int, height: int, target_s: float = 15.0) -> dict:
+def cpu_baseline(width: int, height: int, spp: int, gpu_accum=None, gpu_rgba8=None,
+                 target_s: float = 15.0) -> dict:
     """The CPU oracle (C++ restatement of the shaders, brute-force closest hit) on this host's
-    cores. Sample: config 1 (one full 1920x1080 frame at 1 spp); when that takes less than
-    `target_s`, the frame is re-rendered at more spp (same image, same per-pixel streams) so the
-    timed sample is ~10-30 s of CPU work. Msamples/s is spp-independent."""
+    cores, on a bounded sample of the bench workload itself: evenly spaced rows of the bench frame
+    at its full spp, sized to ~`target_s` of CPU work from a timed config-1 frame (1920x1080 at
+    1 spp). Msamples/s is spp-independent. The same rows of the GPU's bench frame
+    (gpu_accum / gpu_rgba8, numpy [H, W, 4]) are compared with the oracle's: exact match and PSNR
+    of the rgba8 image (BASELINE.json's "PSNR vs CPU ref")."""
+    import numpy as np
     from oracle import oracle
     oracle.build()
     sc = oracle.generate_scene(0.0)
     threads = host_cores()
     t0 = time.perf_counter()
-    _, _, st = oracle.render(sc, oracle.render_call_info(1, width, height), width, height, threads=threads)
+    _, _, st1 = oracle.render(sc, oracle.render_call_info(1, width, height), width, height, threads=threads)
     t1 = time.perf_counter() - t0
-    spp, dt, segs = 1, t1, st[0] / st[1]
-    if t1 < target_s / 3:
-        spp = max(2, int(round(target_s / t1)))
-        t0 = time.perf_counter()
-        _, _, st = oracle.render(sc, oracle.render_call_info(spp, width, height), width, height, threads=threads)
-        dt = time.perf_counter() - t0
-        segs = st[0] / st[1]
-    return {"value": round(width * height * spp / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads,
-            "kind": "port",
-            "sample": f"{width}x{height} at {spp} spp (config 1 frame{'' if spp == 1 else ' re-rendered at more spp'}), "
-                      f"depth 50, brute-force closest hit, {threads} threads, {dt:.2f} s "
-                      f"(1-spp frame alone {t1:.2f} s), {segs:.3f} segments/sample",
-            "config1_frame_s": round(t1, 3)}
+    per_row = t1 / height * spp   # seconds per row of the bench frame
+    if per_row * threads > target_s:   # one row per thread would already exceed the budget
+        return {"value": round(width * height / t1 / 1e6, 4), "unit": "Msamples/s", "cores": threads,
+                "kind": "port",
+                "sample": f"config 1 frame ({width}x{height}, 1 spp, depth 50), brute-force closest hit, "
+                          f"{threads} threads, {t1:.2f} s (rows of the {spp}-spp bench frame would exceed "
+                          f"{target_s:.0f} s)", "config1_frame_s": round(t1, 3)}
+    n_rows = int(max(threads, min(height, round(target_s / max(per_row, 1e-9)))))
+    rows = np.unique(np.linspace(0, height - 1, n_rows).round().astype(np.uint32))
+    t0 = time.perf_counter()
+    acc, out, st = oracle.render(sc, oracle.render_call_info(spp, width, height), width, len(rows),
+                                 rows=rows, threads=threads)
+    dt = time.perf_counter() - t0
+    res = {"value": round(width * len(rows) * spp / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads,
+           "kind": "port",
+           "sample": f"{len(rows)} evenly spaced rows of the bench frame ({width} px, {spp} spp, depth 50), "
+                     f"brute-force closest hit, {threads} threads, {dt:.2f} s; config 1 frame "
+                     f"({width}x{height}, 1 spp) alone {t1:.2f} s; {st[0] / max(1, st[1]):.3f} segments/sample",
+           "config1_frame_s": round(t1, 3)}
+    if gpu_accum is not None and gpu_rgba8 is not None:
+        ga, go = gpu_accum[rows.astype(np.int64)], gpu_rgba8[rows.astype(np.int64)]
+        mse = float(np.mean((go[..., :3].astype(np.float64) - out[..., :3].astype(np.float64)) ** 2))
+        res["parity"] = {"rows": int(len(rows)), "accum_bit_exact": bool(np.array_equal(ga, acc)),
+                         "rgba8_equal": bool(np.array_equal(go, out)),
+                         "psnr_db": "inf" if mse == 0.0 else round(float(10.0 * np.log10(255.0 ** 2 / mse)), 2)}
+    return res
 
 
 def _pmc_record(path: Path, key: str):
@@ -355,7 +372,10 @@ def main() -> int:
                          "frac": round(bflops / (bms * 1e-3) / 1e12 / VALU_FP32_PEAK_TFLOPS, 4)}}
         del acc, out
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile:
-        result["cpu_baseline"] = cpu_baseline(W, H)
+        fa, fo = (slots[0].dr.accum[: slots[0].dr.n], slots[0].dr.out[: slots[0].dr.n]) if split == "strips" \
+            else (None, None)   # at one rank the strips frame is the whole frame in row order
+        result["cpu_baseline"] = cpu_baseline(W, H, spp, fa.cpu().numpy() if fa is not None else None,
+                                              fo.cpu().numpy() if fo is not None else None)
     if rank == 0:
         print(json.dumps(result), flush=True)
     for sl in slots:
