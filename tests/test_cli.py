@@ -15,7 +15,7 @@ def run(*args, cwd=None):
 def test_help_lists_reference_flags():
     r = run("--help")
     assert r.returncode == 0
-    for flag in ("--help", "--store", "--samples", "--width", "--height", "--gpus"):
+    for flag in ("--help", "--store", "--samples", "--width", "--height", "--gpus", "--frames", "--animate"):
         assert flag in r.stdout
 
 
@@ -44,4 +44,27 @@ def test_store_matches_oracle(tmp_path, oracle):
     assert data.startswith(hdr)
     img = np.frombuffer(data[len(hdr):], np.uint8).reshape(36, 64, 3)
     _, ref, _ = oracle.render(oracle.generate_scene(), oracle.render_call_info(3, 64, 36), 64, 36)
+    np.testing.assert_array_equal(img, ref[..., :3])
+
+
+def test_frames_no_device_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    r = run("--frames", "3", "--samples", "1", "--width", "8", "--height", "8")
+    assert r.returncode == 1 and "no HIP device" in r.stderr
+
+
+@pytest.mark.gpu
+def test_frame_loop_matches_oracle(tmp_path, oracle):
+    """--frames: the benchmark loop (two frames in flight, per-frame scene rebuild) prints
+    duration_per_frame like the reference and its last frame equals the oracle's."""
+    r = run("--frames", "5", "--store", "--samples", "2", "--width", "72", "--height", "40", cwd=tmp_path)
+    assert r.returncode == 0, r.stderr
+    assert "duration_per_frame" in r.stdout and "Msamples/s" in r.stdout
+    data = (tmp_path / "render.ppm").read_bytes()
+    hdr = b"P6\n72 40\n255\n"
+    assert data.startswith(hdr)
+    img = np.frombuffer(data[len(hdr):], np.uint8).reshape(40, 72, 3)
+    _, ref, _ = oracle.render(oracle.generate_scene(), oracle.render_call_info(2, 72, 40), 72, 40)
     np.testing.assert_array_equal(img, ref[..., :3])
