@@ -950,8 +950,11 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
     bool saw_dry = false;
     WaveChunk ch;
     {   // the first tiles go out by wave id, not through the counter (host starts it past them):
-        // 16 Ki waves asking one address at once would queue for ~0.1 ms
-        const uint32_t wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+        // 16 Ki waves asking one address at once would queue for ~0.1 ms. Tile ranks are dealt
+        // across blocks first (rank = wave-in-block * blocks + block), so the longest chains of
+        // the LPT order start on different CUs (and XCDs) instead of sharing block 0's SIMDs.
+        // (12 spp: -2.3 % against rank = global wave id; 100 spp: equal)
+        const uint32_t wid = (threadIdx.x >> 6) * gridDim.x + blockIdx.x;
         if (wid < P.first_chunks) {
             ch.next = wid * 64u;
             ch.end = ch.next + 64u;
