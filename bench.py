@@ -300,7 +300,9 @@ def main() -> int:
                 traffic = None
         roof = {"bound": "valu-fp32", "achieved": round(achieved, 3), "peak": VALU_FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / VALU_FP32_PEAK_TFLOPS, 4), "traffic": traffic,
-                "kernel": "rt_trace_lbvh_kernel (octant LDS walk)" if accel == 2 else "rt_trace_brute_kernel",
+                "kernel": ("rt_trace_brute_kernel" if accel != 2 else
+                           "rt_trace_top_kernel (LDS treelet + L2 subtrees)" if renderer.scene_array(8)["device_built"]
+                           else "rt_trace_lbvh_kernel (octant LDS walk)"),
                 "kernel_ms": round(kernel_ms, 4),
                 "kernel_timing": f"{n_iso} launches of this frame timed alone after the timed region "
                                  "(HIP events on the launch stream); with frames in flight a launch "

@@ -63,6 +63,7 @@ struct rt_context {
     // host-provided spheres
     float padded_for = 0.0f;   // pad radius the device node copy currently carries
     bool gpu_tree = false;
+    bool treelet_stale = true;        // ACCEL_LBVH_TOP: the treelet predates the current node boxes
     rt::TileSchedule sched;           // pixel hand-out order (LPT from the last launch's costs)
     rt::BuildWorkspace ws;
     Sphere* d_spheres = nullptr;
@@ -583,7 +584,10 @@ int set_scene_gpu(rt_context* ctx, const Sphere* d_sph, uint32_t count, hipStrea
         if (int rc = scene_alloc(ctx, &d.nodes_raw, 2 * size_t(count))) return rc;
         if (int rc = scene_alloc(ctx, &d.leaf_geom, 4 * size_t(count))) return rc;
         if (int rc = scene_alloc(ctx, &d.leaf_ids, 4 * size_t(count))) return rc;
+        if (int rc = scene_alloc(ctx, &d.treelet, 8 * size_t(rt::kTreeletCap))) return rc;
+        if (int rc = scene_alloc(ctx, &d.treelet_count, 1)) return rc;
     }
+    ctx->treelet_stale = true;
     rt::BuildOutputs o{d.geom, d.radius, d.mat, d.big_ids, d.nodes, d.nodes_raw, d.leaf_geom, d.leaf_ids};
     rt::BuildSummary sm;
     const hipError_t e = rt::build_scene_gpu(ctx->ws, d_sph, count, o, refit, st, &sm);
@@ -737,6 +741,11 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     } else if (escape_walk && ctx->lds_scene_bytes && o.reserved[1] != 5u) {
         accel = rt::ACCEL_LBVH_LDS_SCENE;
         lds = ctx->lds_scene_bytes;
+    } else if (escape_walk && !ctx->lds_bytes && ds.treelet && ds.n_nodes && o.reserved[1] != 10u) {
+        // tree too big for LDS (device-built): its top levels in LDS, the rest from L2
+        // (walk form 10 = everything from L2, A/B)
+        accel = rt::ACCEL_LBVH_TOP;
+        lds = size_t(rt::kTreeletCap) * 32u;
     } else if (escape_walk) {
         accel = ctx->lds_bytes ? rt::ACCEL_LBVH_LDS : rt::ACCEL_LBVH;
         lds = ctx->lds_bytes;
@@ -779,6 +788,8 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     P.n_nodes = d.n_nodes;
     P.nodes16 = d.nodes16;
     P.nodes_oct = d.nodes_oct;
+    P.treelet = d.treelet;
+    P.treelet_count = d.treelet_count;
     P.nodes2 = d.nodes2;   // null when the tree is a single leaf (root2 is then a leaf reference)
     P.n_nodes2 = d.n_nodes2;
     P.root2 = d.root2;
@@ -811,6 +822,7 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
         }
         if (ctx->gpu_tree && ctx->pad_radius != ctx->padded_for) {
             RT_HIP(rt::repad_nodes_gpu(d.nodes_raw, d.nodes, d.n_nodes, pad_for(ctx->pad_radius), st));
+            ctx->treelet_stale = true;
             ctx->padded_for = ctx->pad_radius;
         } else if (!ctx->gpu_tree && ctx->pad_radius != ctx->padded_for) {
             std::vector<rt::BvhNode> n1;
@@ -836,7 +848,8 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     // in descending order of their longest pixel chain (RT_SCHEDULE=rowmajor | sum: A/B only);
     // this launch records the next costs.
     if (accel == rt::ACCEL_LBVH || accel == rt::ACCEL_LBVH_LDS || accel == rt::ACCEL_LBVH16_LDS ||
-        accel == rt::ACCEL_LBVH_LDS_SCENE || accel == rt::ACCEL_LBVH_POOL || accel == rt::ACCEL_LBVH_OCT) {   // escape-walk kernels record tile costs
+        accel == rt::ACCEL_LBVH_LDS_SCENE || accel == rt::ACCEL_LBVH_POOL || accel == rt::ACCEL_LBVH_OCT ||
+        accel == rt::ACCEL_LBVH_TOP) {   // escape-walk kernels record tile costs
         rt::TileSchedule& sc = ctx->sched;
         RT_HIP(rt::schedule_reserve(sc, uint32_t(tiles_x * tiles_y), st));
         const char* e = std::getenv("RT_SCHEDULE");
@@ -853,7 +866,7 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     // first-time stamps start at the maximum (atomicMin); 0xff bytes = ~0ull
     RT_HIP(hipMemsetAsync(&ctx->counters->t_first, 0xff, 2 * sizeof(unsigned long long), st));
     const int ci = count ? 1 : 0;
-    static_assert(rt::ACCEL_LBVH_OCT < rt_context::kAccelIds, "occupancy cache too small for the accel ids");
+    static_assert(rt::ACCEL_LBVH_TOP < rt_context::kAccelIds, "occupancy cache too small for the accel ids");
     if (ctx->occ_lds[accel][ci] != lds) {
         int b = 0;
         RT_HIP(rt::trace_occupancy(accel, count, lds, &b));
@@ -881,6 +894,10 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
         P.isolate_tiles = P.tile_order ? uint32_t(std::min<uint64_t>(P.first_chunks, iso)) : 0u;
         if (P.first_chunks) RT_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&ctx->counters->work_head),
                                                      int(P.first_chunks * 64u), 1, st));
+    }
+    if (accel == rt::ACCEL_LBVH_TOP && ctx->treelet_stale) {   // after a build, refit or re-pad
+        RT_HIP(rt::build_treelet(d.nodes, d.n_nodes, d.treelet, d.treelet_count, st));
+        ctx->treelet_stale = false;
     }
     RT_HIP(rt::launch_trace(P, accel, count, grid, lds, st));
     ctx->last_stream = st;

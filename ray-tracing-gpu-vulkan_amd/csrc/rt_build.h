@@ -84,5 +84,8 @@ hipError_t schedule_order(TileSchedule& s, hipStream_t st);
 
 // nodes[i] = nodes_raw[i] grown by `pad` on every side (far-camera re-pad).
 hipError_t repad_nodes_gpu(const BvhNode* raw, BvhNode* nodes, uint32_t n_nodes, float pad, hipStream_t st);
+// Top treelet of the padded tree for ACCEL_LBVH_TOP (layout in rt_internal.h): out holds
+// kTreeletCap x 8 floats, *out_count receives the node count. Asynchronous on `st`.
+hipError_t build_treelet(const BvhNode* nodes, uint32_t n_nodes, float* out, uint32_t* out_count, hipStream_t st);
 
 }  // namespace rt

@@ -356,6 +356,74 @@ __global__ void __launch_bounds__(kBlock) k_repad(const BvhNode* __restrict__ ra
     nodes[i] = nd;
 }
 
+// Top treelet (ACCEL_LBVH_TOP, layout in rt_internal.h) of an escape-link tree in depth-first
+// order: one block gathers the nodes of depth <= kTreeletDepth level by level (children of inner
+// node i: i + 1 and the escape of i + 1), sorts them by node index (bitonic, in LDS) so they keep
+// the tree's depth-first order, and writes each in AB layout with its links as treelet ranks (the
+// escape of a node is never deeper than the node, so it is in the treelet too).
+constexpr uint32_t kTreeletThreads = 1024;
+__global__ void __launch_bounds__(kTreeletThreads) k_treelet(const BvhNode* __restrict__ nodes, uint32_t n_nodes,
+                                                             float4* __restrict__ out, uint32_t* out_count) {
+    constexpr uint32_t kSort = 4096;   // >= kTreeletCap, a power of two
+    static_assert(kSort >= kTreeletCap, "treelet sort capacity");
+    __shared__ unsigned long long key[kSort];   // node index << 8 | depth
+    __shared__ uint32_t count;
+    const uint32_t tid = threadIdx.x;
+    if (tid == 0) {
+        count = n_nodes ? 1u : 0u;
+        key[0] = 0ull;
+    }
+    __syncthreads();
+    uint32_t lb = 0, le = count;
+    for (uint32_t d = 0; d < kTreeletDepth && lb < le; ++d) {
+        for (uint32_t t = lb + tid; t < le; t += kTreeletThreads) {
+            const uint32_t i = uint32_t(key[t] >> 8);
+            if (nodes[i].first_count == 0u) {   // inner: both children, one level deeper
+                const uint32_t s = atomicAdd(&count, 2u);
+                key[s] = (uint64_t(i + 1u) << 8) | (d + 1u);
+                key[s + 1] = (uint64_t(nodes[i + 1].escape) << 8) | (d + 1u);
+            }
+        }
+        __syncthreads();
+        lb = le;
+        le = count;
+        __syncthreads();
+    }
+    const uint32_t n = count;
+    for (uint32_t t = n + tid; t < kSort; t += kTreeletThreads) key[t] = ~0ull;
+    __syncthreads();
+    for (uint32_t k = 2; k <= kSort; k <<= 1) {   // bitonic sort, ascending
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t t = tid; t < kSort; t += kTreeletThreads) {
+                const uint32_t p = t ^ j;
+                if (p > t) {
+                    const unsigned long long a = key[t], b = key[p];
+                    if (((t & k) == 0) == (a > b)) { key[t] = b; key[p] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t t = tid; t < n; t += kTreeletThreads) {
+        const uint32_t i = uint32_t(key[t] >> 8), dep = uint32_t(key[t] & 255u);
+        const BvhNode nd = nodes[i];
+        uint32_t miss = kEnd;
+        if (nd.escape != kEnd) {   // rank of the escape: binary search over the sorted indices
+            uint32_t lo = 0, hi = n;
+            while (lo < hi) {
+                const uint32_t m = (lo + hi) >> 1;
+                if (uint32_t(key[m] >> 8) < nd.escape) lo = m + 1; else hi = m;
+            }
+            if (lo < n && uint32_t(key[lo] >> 8) == nd.escape) miss = lo;
+        }
+        const uint32_t hit = nd.first_count ? (0x80000000u | nd.first_count)
+                                            : (dep == kTreeletDepth ? (0xC0000000u | i) : t + 1u);
+        out[2 * t] = make_float4(nd.lox, nd.loy, nd.hix, nd.hiy);
+        out[2 * t + 1] = make_float4(nd.loz, nd.hiz, __uint_as_float(miss), __uint_as_float(hit));
+    }
+    if (tid == 0) *out_count = n;
+}
+
 __global__ void __launch_bounds__(kBlock) k_iota(uint32_t* v, uint32_t n) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i < n) v[i] = i;
@@ -499,6 +567,11 @@ hipError_t schedule_order(TileSchedule& s, hipStream_t st) {
     size_t tb = s.tmp_bytes;
     return hipcub::DeviceRadixSort::SortPairsDescending(s.tmp, tb, s.cost[s.cur ^ 1], s.keys, s.iota, s.order,
                                                         int(s.n), 0, 32, st);
+}
+
+hipError_t build_treelet(const BvhNode* nodes, uint32_t n_nodes, float* out, uint32_t* out_count, hipStream_t st) {
+    k_treelet<<<1, kTreeletThreads, 0, st>>>(nodes, n_nodes, reinterpret_cast<float4*>(out), out_count);
+    return hipGetLastError();
 }
 
 hipError_t repad_nodes_gpu(const BvhNode* raw, BvhNode* nodes, uint32_t n_nodes, float pad, hipStream_t st) {

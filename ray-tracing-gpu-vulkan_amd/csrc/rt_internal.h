@@ -72,6 +72,8 @@ struct DeviceScene {
     BvhNode16* nodes16 = nullptr;  // compact escape-link nodes (null when the tree is too big)
     BvhNode* nodes_oct = nullptr;  // host-built trees: 8 x n_nodes, one near-child-first order per
                                    // ray octant (null: every octant copy uses `nodes`' order)
+    float* treelet = nullptr;      // device-built trees: kTreeletCap x 8 floats (ACCEL_LBVH_TOP)
+    uint32_t* treelet_count = nullptr;   // device word: nodes in the treelet
     Bvh2Node* nodes2 = nullptr;    // ordered-walk layout (same leaves)
     uint32_t n_nodes2 = 0;
     uint32_t root2 = 0;            // root reference (inner index or leaf reference)
@@ -81,7 +83,16 @@ struct DeviceScene {
 
 enum : uint32_t { ACCEL_BRUTE = 1, ACCEL_LBVH = 2, ACCEL_LBVH_LDS = 3, ACCEL_LBVH2 = 4, ACCEL_LBVH2_LDS = 5, ACCEL_LBVH16_LDS = 6, ACCEL_LBVH_LDS_SCENE = 7,
        ACCEL_LBVH_POOL = 8 /* LBVH_LDS_SCENE + tail-compaction pool, 1024-thread blocks */,
-       ACCEL_LBVH_OCT = 9  /* LBVH_LDS_SCENE with 8 octant-specialised node copies, 1024-thread blocks */ };
+       ACCEL_LBVH_OCT = 9  /* LBVH_LDS_SCENE with 8 octant-specialised node copies, 1024-thread blocks */,
+       ACCEL_LBVH_TOP = 10 /* tree too big for LDS: its top levels (treelet) in LDS, the rest from L2 */ };
+
+// Top treelet of a tree too big for LDS (ACCEL_LBVH_TOP): the nodes of depth <= kTreeletDepth in
+// the tree's depth-first order, 2 float4 each, AB layout: A = (lo.x, lo.y, hi.x, hi.y),
+// B = (lo.z, hi.z, miss, hit). miss = treelet rank of the escape (END = ~0); hit = rank of the
+// next node (inner node above the cut), or a word with bit 31 set: 0x80000000 | first_count
+// (leaf) or 0xC0000000 | global node index (inner node at the cut: walk its subtree from L2).
+constexpr uint32_t kTreeletDepth = 11;
+constexpr uint32_t kTreeletCap = (2u << kTreeletDepth) - 1u;   // 4095 nodes, 128 KiB
 
 // Counters block (device memory, zeroed before each launch by the host).
 struct Counters {
@@ -134,6 +145,8 @@ struct TraceParams {
     uint32_t n_nodes;
     const BvhNode16* nodes16;
     const BvhNode* nodes_oct;      // optional, see DeviceScene
+    const float* treelet;          // ACCEL_LBVH_TOP, see DeviceScene (2 float4 per node)
+    const uint32_t* treelet_count;
     const Bvh2Node* nodes2;
     uint32_t n_nodes2, root2, stack_depth;
     uint32_t n_leaf;               // spheres in the tree (leaf slots)

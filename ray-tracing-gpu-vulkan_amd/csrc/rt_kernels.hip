@@ -683,7 +683,68 @@ __device__ __forceinline__ void walk_escape(const rt::TraceParams& P, const floa
     // found a hit leaf (postponed in `pending`) or finished its walk; then all pending leaves are
     // tested together, so the 4-sphere leaf block runs once per batch instead of in every visit
     // in which any lane of the wave happens to be at a leaf.
-    if (LAYOUT == 0) {   // BvhNode pairs: escape in lo.w, leaf field (first << 4 | count, 0 = inner) in hi.w
+    if (LAYOUT == 3) {
+        // Treelet in LDS (top kTreeletDepth levels, AB layout with LDS-address links), the
+        // subtrees below the cut and all leaf spheres from L2 (ACCEL_LBVH_TOP). A lane leaves
+        // the LDS loop at a hit word — a leaf, or a subtree root at the cut — remembering the
+        // node's miss link, where it continues afterwards (the escape of a leaf or of a whole
+        // subtree). In a balanced 100 k-sphere tree the top 11 levels take ~72 % of the visits
+        // (scripts/visit_depths.py).
+        typedef const __attribute__((address_space(3))) float4* LdsF4;
+        const uint32_t nbase = uint32_t(reinterpret_cast<uintptr_t>((LdsF4)nodes4));
+        const float4* gnodes = reinterpret_cast<const float4*>(P.nodes);
+        uint32_t ni = r.ni == END ? END : nbase;
+        for (;;) {
+            uint32_t cont = END;
+            while (int32_t(ni) >= 0) {
+                const float4 A = lds_f4(ni);
+                const float4 B = lds_f4(ni + 16u);
+                if (COUNT) n_box++;
+                const bool hit = node_hit<1u>(A, B, q, r.limit);
+                cont = __float_as_uint(B.z);
+                ni = __float_as_uint(hit ? B.w : B.z);
+            }
+            const bool at = ni != END;
+            if (!__ballot(at)) break;
+            if (at) {
+                uint32_t pending = 0u;
+                if (ni & 0x40000000u) {   // subtree of global node g (inner, its box was hit): [g + 1, escape(g))
+                    const uint32_t g = ni & 0x3fffffffu;
+                    const uint32_t eg = __float_as_uint(gnodes[2 * g].w);
+                    const uint32_t bound = eg == END ? P.n_nodes : eg;
+                    uint32_t gi = g + 1u;
+                    for (;;) {
+                        while (gi < bound && pending == 0u) {
+                            const float4 n0 = gnodes[2 * gi];
+                            const float4 n1 = gnodes[2 * gi + 1];
+                            if (COUNT) n_box++;
+                            const bool h = node_hit<1>(make_float4(n0.x, n0.y, n1.x, n1.y),
+                                                       make_float4(n0.z, n1.z, 0.0f, 0.0f), q, r.limit);
+                            const uint32_t fc = __float_as_uint(n1.w);
+                            if (h && fc != 0u) pending = fc;
+                            gi = (h && fc == 0u) ? gi + 1u : __float_as_uint(n0.w);
+                        }
+                        if (pending == 0u) break;
+                        const uint32_t first = pending >> 4;
+                        const float4 s0 = leaf4[first], s1 = leaf4[first + 1], s2 = leaf4[first + 2], s3 = leaf4[first + 3];
+                        test4(s0, s1, s2, s3, [&](uint32_t k) { return leaf_ids[first + k]; }, r.o, r.d, r.inv, r.a,
+                              r.best, r.bi, r.limit, P.cull_abs, P.cull_rel);
+                        if (COUNT) n_sph += pending & 15u;
+                        pending = 0u;
+                    }
+                } else {                  // leaf above the cut
+                    pending = ni & 0x3fffffffu;
+                    const uint32_t first = pending >> 4;
+                    const float4 s0 = leaf4[first], s1 = leaf4[first + 1], s2 = leaf4[first + 2], s3 = leaf4[first + 3];
+                    test4(s0, s1, s2, s3, [&](uint32_t k) { return leaf_ids[first + k]; }, r.o, r.d, r.inv, r.a,
+                          r.best, r.bi, r.limit, P.cull_abs, P.cull_rel);
+                    if (COUNT) n_sph += pending & 15u;
+                }
+                ni = cont;
+            }
+        }
+        r.ni = END;
+    } else if (LAYOUT == 0) {   // BvhNode pairs: escape in lo.w, leaf field (first << 4 | count, 0 = inner) in hi.w
         uint32_t pending = 0u;
         for (;;) {
             while (r.ni != END && pending == 0u) {
@@ -1099,6 +1160,7 @@ __device__ __forceinline__ void lbvh_classic(const rt::TraceParams& P, const flo
 #ifndef RT_LBVH_BLOCK
 #define RT_LBVH_BLOCK 512
 #endif
+constexpr uint32_t kTopBlock = 1024;   // one block per CU shares one staged treelet
 
 // LBVH kernel. LDS: stage the tree (nodes, leaf spheres, leaf ids) and, when SCENE_LDS, the
 // per-sphere geometry + material records read by shading, once per persistent block. Blocks of
@@ -1182,6 +1244,30 @@ __global__ __launch_bounds__(BLOCK, RT_TRACE_WAVES_PER_SIMD) void rt_trace_lbvh_
     if (LDS || POOL) __syncthreads();
     lbvh_classic<COUNT, NODE16, POOL, (LDS && !NODE16) ? (NOCT == 8 ? 2 : 1) : 0>(
         P, nodes4, leaf4, leaf_ids, geom4, mat4, &ctl, reinterpret_cast<uint32_t*>(lds + staged4), BLOCK);
+}
+
+// LBVH kernel for trees too big for LDS (ACCEL_LBVH_TOP): the treelet (rt_build.hip
+// build_treelet) is staged in LDS with its rank links turned into LDS addresses; leaves,
+// subtrees below the cut, geometry and materials stay in HBM/L2.
+template <bool COUNT>
+__global__ __launch_bounds__(kTopBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace_top_kernel(const rt::TraceParams P) {
+    extern __shared__ float4 lds[];
+    __shared__ PoolCtl ctl;
+    typedef const __attribute__((address_space(3))) float4* LdsF4;
+    const uint32_t lbase = uint32_t(reinterpret_cast<uintptr_t>((LdsF4)lds));
+    const uint32_t n_top = min(*P.treelet_count, rt::kTreeletCap);
+    for (uint32_t i = threadIdx.x; i < n_top; i += kTopBlock) {
+        const float4* tl = reinterpret_cast<const float4*>(P.treelet);
+        const float4 A = tl[2 * i], B = tl[2 * i + 1];
+        const uint32_t miss = __float_as_uint(B.z), hit = __float_as_uint(B.w);
+        lds[2 * i] = A;
+        lds[2 * i + 1] = make_float4(B.x, B.y, __uint_as_float(miss == END ? END : lbase + miss * 32u),
+                                     __uint_as_float(int32_t(hit) >= 0 ? lbase + hit * 32u : hit));
+    }
+    __syncthreads();
+    lbvh_classic<COUNT, false, false, 3>(P, lds, reinterpret_cast<const float4*>(P.leaf_geom), P.leaf_ids,
+                                         reinterpret_cast<const float4*>(P.geom),
+                                         reinterpret_cast<const float4*>(P.mat), &ctl, nullptr, kTopBlock);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1346,6 +1432,9 @@ static const void* pick(uint32_t accel, bool count) {
             return count ? RT_POOL_FN(true) : RT_POOL_FN(false);
         case ACCEL_LBVH_OCT:
             return count ? RT_OCT_FN(true) : RT_OCT_FN(false);
+        case ACCEL_LBVH_TOP:
+            return count ? reinterpret_cast<const void*>(rt_trace_top_kernel<true>)
+                         : reinterpret_cast<const void*>(rt_trace_top_kernel<false>);
         case ACCEL_LBVH16_LDS:
             return count ? RT_LBVH_FN(true, true, true, false) : RT_LBVH_FN(true, false, true, false);
         case ACCEL_LBVH2:
@@ -1367,6 +1456,7 @@ uint32_t block_size(uint32_t accel) {
         case ACCEL_LBVH2: case ACCEL_LBVH2_LDS: return kLbvh2Block;
         case ACCEL_BRUTE: return 256u;
         case ACCEL_LBVH_POOL: case ACCEL_LBVH_OCT: return kPoolBlock;
+        case ACCEL_LBVH_TOP: return kTopBlock;
         default: return kLbvhBlock;
     }
 }

@@ -482,3 +482,27 @@ def test_isolated_tiles_same_image(rtvk, renderer, torch, oracle, isolate):
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
+
+
+
+@pytest.mark.parametrize("W,H,spp,K,form", [(320, 180, 2, 158, 0), (320, 180, 2, 158, 10), (96, 64, 3, 40, 0)])
+def test_treelet_walk_equals_brute(rtvk, renderer, torch, oracle, W, H, spp, K, form):
+    """Trees too big for LDS (device-built): the top levels staged in LDS as a treelet, subtrees
+    below the cut from L2 (ACCEL_LBVH_TOP, walk form 0) and the all-L2 walk (form 10) equal brute
+    force bit for bit, twice each (the second launch runs with the LPT order)."""
+    sc = oracle.generate_scene(0.0, K)
+    rci = oracle.render_call_info(spp, W, H)
+    ab, ob, sb = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=BRUTE)
+    for _ in range(2):
+        with tree_builder("gpu"):
+            renderer.set_scene(np.ascontiguousarray(sc, np.uint8).reshape(-1, 80))
+        rc = rtvk.RenderCallInfo.from_buffer_copy(np.ascontiguousarray(rci).tobytes())
+        acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+        opt = rtvk.make_options(accel=LBVH)
+        opt.reserved[1] = form
+        renderer.render_device(rc, acc, out, options=opt)
+        torch.cuda.synchronize()
+        assert_same(acc.cpu().numpy(), out.cpu().numpy(), ab, ob)
+        st = renderer.stats()
+        assert (st.segments, st.samples) == (sb.segments, sb.samples)
