@@ -506,3 +506,22 @@ def test_treelet_walk_equals_brute(rtvk, renderer, torch, oracle, W, H, spp, K, 
         assert_same(acc.cpu().numpy(), out.cpu().numpy(), ab, ob)
         st = renderer.stats()
         assert (st.segments, st.samples) == (sb.segments, sb.samples)
+
+
+def test_treelet_after_refit(rtvk, renderer, torch, oracle):
+    """The treelet is rebuilt after a refit of a device-built tree (moving spheres): the treelet
+    walk still equals brute force on the refitted scene."""
+    W, H, spp, K = 128, 72, 2, 40
+    sc0, sc1 = oracle.generate_scene(0.0, K), oracle.generate_scene(0.7, K)
+    rci = oracle.render_call_info(spp, W, H)
+    ab, ob, _ = gpu_render(rtvk, renderer, torch, sc1, rci, W, H, accel=BRUTE)
+    with tree_builder("gpu"):
+        renderer.set_scene(np.ascontiguousarray(sc0, np.uint8).reshape(-1, 80))
+        rc = rtvk.RenderCallInfo.from_buffer_copy(np.ascontiguousarray(rci).tobytes())
+        acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+        renderer.render_device(rc, acc, out, options=rtvk.make_options(accel=LBVH))   # treelet of sc0
+        renderer.refit_scene(np.ascontiguousarray(sc1, np.uint8).reshape(-1, 80))
+        renderer.render_device(rc, acc, out, options=rtvk.make_options(accel=LBVH))
+    torch.cuda.synchronize()
+    assert_same(acc.cpu().numpy(), out.cpu().numpy(), ab, ob)
