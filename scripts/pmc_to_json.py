@@ -10,11 +10,22 @@ Usage: pmc_to_json.py KEY PASS_DIR [OUT_JSON]"""
 import csv
 import glob
 import json
+import re
 import statistics
 import sys
 from pathlib import Path
 
 SIMDS, CLOCK_HZ = 1024, 2.4e9
+
+
+def is_production(kernel_name: str) -> bool:
+    """A trace-kernel launch of the shipped build: rt_trace_lbvh_kernel<LDS, COUNT, ...> or
+    rt_trace_top_kernel<COUNT> with COUNT = false (the instrumented counting pass is excluded)."""
+    m = re.search(r"rt_trace_(lbvh|top)_kernel<([^>]*)>", kernel_name)
+    if not m:
+        return False
+    args = [a.strip() for a in m.group(2).split(",")]
+    return (args[1] if m.group(1) == "lbvh" else args[0]) == "false"
 
 
 def main():
@@ -24,7 +35,7 @@ def main():
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"]
-            if "rt_trace_lbvh_kernel" not in k or "<true, true" in k:   # production launches only
+            if not is_production(k):
                 continue
             e = per.setdefault(r["Dispatch_Id"], {"dur_ns": int(r["End_Timestamp"]) - int(r["Start_Timestamp"])})
             e[r["Counter_Name"]] = float(r["Counter_Value"])

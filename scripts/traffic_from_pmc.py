@@ -8,17 +8,28 @@ wide coalesced streaming reads (MI355X_MICROARCH.md §HBM), so it is doubled. Wr
 import csv
 import glob
 import json
+import re
 import statistics
 import sys
 from pathlib import Path
 
 
-def per_dispatch(d, counter, match="rt_trace_lbvh_kernel", exclude="<true, true"):
-    """Production launches only: the instrumented (COUNT) build is <LDS=true, COUNT=true, ...>."""
+def is_production(kernel_name: str) -> bool:
+    """A trace-kernel launch of the shipped build: rt_trace_lbvh_kernel<LDS, COUNT, ...> or
+    rt_trace_top_kernel<COUNT> with COUNT = false (the instrumented counting pass is excluded)."""
+    m = re.search(r"rt_trace_(lbvh|top)_kernel<([^>]*)>", kernel_name)
+    if not m:
+        return False
+    args = [a.strip() for a in m.group(2).split(",")]
+    return (args[1] if m.group(1) == "lbvh" else args[0]) == "false"
+
+
+def per_dispatch(d, counter):
+    """Production launches only (is_production)."""
     vals = []
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] == counter and match in r["Kernel_Name"] and exclude not in r["Kernel_Name"]:
+            if r["Counter_Name"] == counter and is_production(r["Kernel_Name"]):
                 vals.append(float(r["Counter_Value"]))
     return vals
 
