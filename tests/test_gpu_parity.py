@@ -525,3 +525,18 @@ def test_treelet_after_refit(rtvk, renderer, torch, oracle):
         renderer.render_device(rc, acc, out, options=rtvk.make_options(accel=LBVH))
     torch.cuda.synchronize()
     assert_same(acc.cpu().numpy(), out.cpu().numpy(), ab, ob)
+
+
+@pytest.mark.parametrize("cam", [(500.0, 300.0, -200.0), (13.0, 0.05, -3.0)])
+def test_treelet_far_camera(rtvk, renderer, torch, oracle, cam):
+    """A device-built tree too big for LDS under a far camera (re-pad of the node boxes, so the
+    treelet is rebuilt) and a grazing one: the treelet walk equals brute force."""
+    W, H, K = 64, 40, 40
+    sc = oracle.generate_scene(0.0, K)
+    rci = oracle.render_call_info(2, W, H)
+    f = rci.view(np.float32)
+    f[8:11] = cam
+    f[12:15] = [-cam[0], -cam[1], -cam[2]]
+    ab, ob, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=BRUTE)
+    a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH, builder="gpu")
+    assert_same(a, o, ab, ob)
