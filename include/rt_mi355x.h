@@ -86,7 +86,13 @@ typedef struct rt_options {
     uint32_t accel;       /* rt_accel                                                            */
     uint32_t accumulate;  /* 0: clear the accumulator first (src/vulkan.h:1081-1086); 1: add on top */
     uint32_t sample_base; /* RT_RNG_SAMPLE_COUNTER only: index of this launch's first sample       */
-    uint32_t reserved[2];
+    uint32_t reserved[2]; /* 0 for production. Diagnostics / A/B only: reserved[0] bit 0 = count box
+                             and sphere tests (slower instrumented build, rt_get_stats);
+                             reserved[1] = LBVH walk form: 0 automatic (octant node copies in LDS
+                             when they fit; LDS treelet + L2 subtrees for trees too big for LDS),
+                             2 ordered two-wide walk, 4 compact 16-B nodes, 5 scene records from
+                             global memory, 6 one LDS node copy, 7 + tail-compaction pool,
+                             8 octant copies, 10 whole tree from L2 */
 } rt_options;
 
 /* Statistics of the last rt_render_device() on a context (valid after its stream completes). */
