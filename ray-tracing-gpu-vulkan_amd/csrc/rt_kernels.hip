@@ -59,7 +59,7 @@ struct Stamps { unsigned long long acc[8], t; uint32_t cur; };
 #define STAMP_ARG , stamps
 #else
 #define STAMP(k) do {} while (0)
-#define STAMP_DECL Stamps stamps
+#define STAMP_DECL [[maybe_unused]] Stamps stamps
 #define STAMP_FLUSH do {} while (0)
 #define STAMP_ARG , stamps
 #endif
