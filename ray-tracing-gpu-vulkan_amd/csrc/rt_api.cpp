@@ -274,18 +274,6 @@ class BlobUpload {
     size_t total_ = 0;
 };
 
-template <typename T>
-int upload(rt_context* ctx, const std::vector<T>& v, T** dst, hipStream_t st) {
-    *dst = nullptr;
-    if (v.empty()) return RT_OK;
-    void* p = nullptr;
-    RT_HIP(hipMalloc(&p, v.size() * sizeof(T)));
-    ctx->scene_allocs.push_back(p);
-    RT_HIP(hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st));
-    *dst = static_cast<T*>(p);
-    return RT_OK;
-}
-
 // ---- shader.rgen:29, 48-49, 92-105: camera + viewport, once per launch ------------------
 struct F3 { float x, y, z; };
 inline F3 f3(float x, float y, float z) { return F3{x, y, z}; }
