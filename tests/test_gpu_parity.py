@@ -540,3 +540,19 @@ def test_treelet_far_camera(rtvk, renderer, torch, oracle, cam):
     ab, ob, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=BRUTE)
     a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH, builder="gpu")
     assert_same(a, o, ab, ob)
+
+
+@pytest.mark.parametrize("spp,depth", [(0, 50), (1, 1), (5, 0)])
+def test_degenerate_sample_and_depth_counts(rtvk, renderer, torch, oracle, spp, depth):
+    """spp = 0 (every pixel stored at once: 0/0 tonemaps to 0, alpha 255), depth 1 (one segment
+    per sample: no scattered light) and max_depth 0 (the reference default of 50) match the
+    oracle bit for bit, with the same segment/sample counts, on the production (octant) walk
+    and on brute force."""
+    W, H = 40, 24
+    sc = oracle.generate_scene()
+    rci = oracle.render_call_info(spp, W, H)
+    ra, ro, rs = oracle.render(sc, rci, W, H, opts=oracle.options(max_depth=depth if depth else 50))
+    for accel in (BRUTE, LBVH):
+        a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=accel, max_depth=depth)
+        assert_same(a, o, ra, ro)
+        assert (st.segments, st.samples) == (rs[0], rs[1])
