@@ -145,6 +145,7 @@ int rt_refit_scene_device(rt_context* ctx, const Sphere* d_spheres, uint32_t cou
  *                GPUs); NULL means rows rci->offset.y + [0, band_height).
  *   accum_rgba32f / out_rgba8   DEVICE arrays of band_width * band_height texels, row-major by
  *                band row (the reference's per-band storage images, bindings 3 and 0).
+ *   band_width, band_height < 65536 (RT_ERR_INVALID_ARGUMENT otherwise); 0 renders nothing.
  */
 int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t* rows,
                      uint32_t band_width, uint32_t band_height, float* accum_rgba32f,

@@ -697,6 +697,9 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
         return fail(RT_ERR_INVALID_ARGUMENT, "image_size is zero");
     const uint64_t tiles_x = (band_width + 7u) / 8u, tiles_y = (band_height + 7u) / 8u;
     if (tiles_x * tiles_y * 64u >= (1ull << 32)) return fail(RT_ERR_INVALID_ARGUMENT, "band too large");
+    // the kernel keeps a pixel's band coordinates as 16-bit halves of one word (Path::px)
+    if (band_width > 65535u || band_height > 65535u)
+        return fail(RT_ERR_INVALID_ARGUMENT, "band width and height must be below 65536");
     rt_options o;
     std::memset(&o, 0, sizeof(o));
     if (opt) o = *opt;

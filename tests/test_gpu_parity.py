@@ -556,3 +556,14 @@ def test_degenerate_sample_and_depth_counts(rtvk, renderer, torch, oracle, spp, 
         a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=accel, max_depth=depth)
         assert_same(a, o, ra, ro)
         assert (st.segments, st.samples) == (rs[0], rs[1])
+
+
+def test_band_dimension_limits(rtvk, renderer, torch, oracle):
+    """Bands wider or taller than 65535 pixels are refused (the kernel packs band coordinates into
+    16-bit halves); an empty band is a no-op."""
+    renderer.set_scene(oracle.generate_scene())
+    rci = rtvk.RenderCallInfo.from_buffer_copy(oracle.render_call_info(1, 70000, 8).tobytes())
+    acc = torch.zeros((1, 70000, 4), dtype=torch.float32, device="cuda")
+    out = torch.zeros((1, 70000, 4), dtype=torch.uint8, device="cuda")
+    with pytest.raises(rtvk.RtError):
+        renderer.render_device(rci, acc, out, options=rtvk.make_options())
