@@ -732,7 +732,8 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     } else if (escape_walk && ctx->lds_scene_bytes && o.reserved[1] != 5u) {
         accel = rt::ACCEL_LBVH_LDS_SCENE;
         lds = ctx->lds_scene_bytes;
-    } else if (escape_walk && !ctx->lds_bytes && ds.treelet && ds.n_nodes && o.reserved[1] != 10u) {
+    } else if (escape_walk && !ctx->lds_bytes && ds.treelet && ds.n_nodes && ds.n_leaf < (1u << 26) &&
+               o.reserved[1] != 10u) {   // (treelet leaf words carry first_count in 30 bits)
         // tree too big for LDS (device-built): its top levels in LDS, the rest from L2
         // (walk form 10 = everything from L2, A/B)
         accel = rt::ACCEL_LBVH_TOP;
