@@ -147,7 +147,7 @@ def _split_worker(rank, world, port, out_path, force_collective=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,force_collective", [(2, False), (3, False), (2, True), (3, True)])
+@pytest.mark.parametrize("world,force_collective", [(2, False), (3, False), (2, True), (3, True), (4, True)])
 def test_sample_split_world(tmp_path, oracle, world, force_collective):
     """Rank r renders split_samples(spp)[r] samples with number = 7 + r; the reduced frame equals
     the rank-ordered float sum of those sub-frames, tonemapped with the full spp."""
