@@ -28,6 +28,9 @@ VALU_FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, vector FP32 (256 CU x 2.4
 HBM_PEAK_GBPS = 8000.0
 FLOP_PER_SPHERE_TEST = 23
 FLOP_PER_BOX_TEST = 20
+BYTES_PER_BOX_TEST = 32         # bytes/sample = S·(B·32 + T·16), read from LDS
+BYTES_PER_SPHERE_TEST = 16
+LDS_PEAK_TBPS = 256 * 256 * 2.4e9 / 1e12   # ds_read_b128: 256 B/clk/CU (MI355X_MICROARCH.md §LDS) x 256 CU x 2.4 GHz
 
 
 def host_cores() -> int:
@@ -313,6 +316,13 @@ def main() -> int:
                 "flop_model": "20/box test + 23/sphere test (SURVEY.md 8(d)); counts from the "
                               f"instrumented build of the same kernel at {cnt_spp} spp"
                               + (f", x{scale:g}" if scale != 1 else "")}
+        if accel == 2:   # the other fraction SURVEY.md 8(d) asks for: the LBVH's own bytes, from LDS
+            lds_bytes = (cs.box_tests * BYTES_PER_BOX_TEST + cs.sphere_tests * BYTES_PER_SPHERE_TEST) * scale
+            lds_tbps = lds_bytes / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
+            roof["lds"] = {"achieved": round(lds_tbps, 3), "peak": round(LDS_PEAK_TBPS, 1), "unit": "TB/s",
+                           "frac": round(lds_tbps / LDS_PEAK_TBPS, 4), "bytes_per_launch": int(lds_bytes),
+                           "model": "32 B per box test + 16 B per sphere test (node and leaf records; "
+                                    "from L2 instead of LDS below the treelet of trees too big for LDS)"}
         valu = _pmc_record(ROOT / "profiles" / "pmc_valu.json", f"{args.accel}-{W}x{H}-{spp}spp-grid{args.grid}-n{world}")
         if valu:
             roof["valu_issue_busy"] = valu.get("valu_issue_busy")
