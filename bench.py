@@ -1,19 +1,27 @@
 #!/usr/bin/env python3
 """bench.py — Msamples/s of the MI355X path tracer on the canonical RTIOW scene (BASELINE.json).
 
-One step = one frame of the hot path: every pixel of the 1920x1080 image traced at `--spp`
-samples, depth 50, on the canonical scene (generateRandomScene(t=0): 488 spheres, camera
-(13,11,-3) -> origin), i.e. BASELINE.json config 2's input. For N > 1 the step also includes the
-RCCL gather of every rank's row strips to rank 0 and the on-device reassembly (strong scaling:
-the image is fixed, each GPU renders 1/N of its rows).
+One step = one frame of the hot path: every pixel of the image traced at `spp` samples, depth 50,
+on the canonical scene (generateRandomScene(t=0): 488 spheres, camera (13,11,-3) -> origin),
+rebuilding the acceleration structure as the reference does every frame. Default workload:
+BASELINE config 3 (1920x1080, 10 000 spp, LBVH + persistent threads); on N GPUs the same frame is
+tiled into 8-row strips over the ranks and gathered to rank 0 over RCCL (config 4 at N = 8):
+strong scaling. `--config 2` (100 spp, brute force) and `--config 5` (3840x2160, 99 860 spheres,
+1 000 spp) select the other BASELINE configs.
 
-Launch: python bench.py [--gpus 1 --steps 5 --warmup 2]
+Random stream (`--rng`): "hash" (default; RT_RNG_SAMPLE_HASH, the north star's counter-based RNG:
+per-sample LCG starts, fixed-point sums, samples of a pixel split into chunks over the lanes) or
+"stream" (the reference's per-pixel LCG stream). Both are bit-exact against the CPU oracle; the
+N = 1 line also times the other stream on the same frame (`reference_stream`).
+
+Launch: python bench.py [--gpus 1 --steps 3 --warmup 1]
         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 Rank 0 prints one JSON line (DESIGN.md §6 explains every field).
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -24,107 +32,155 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "ray-tracing-gpu-vulkan_amd"))
 
-VALU_FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, vector FP32 (256 CU x 2.4 GHz)
-HBM_PEAK_GBPS = 8000.0
+VALU_FP32_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, vector FP32 (256 CU x 4 SIMD x 64 FLOP/clk x 2.4 GHz)
 FLOP_PER_SPHERE_TEST = 23
 FLOP_PER_BOX_TEST = 20
 BYTES_PER_BOX_TEST = 32         # bytes/sample = S·(B·32 + T·16), read from LDS
 BYTES_PER_SPHERE_TEST = 16
-LDS_PEAK_TBPS = 256 * 256 * 2.4e9 / 1e12   # ds_read_b128: 256 B/clk/CU (MI355X_MICROARCH.md §LDS) x 256 CU x 2.4 GHz
+LDS_PEAK_TBPS = 256 * 256 * 2.4e9 / 1e12   # ds_read_b128: 256 B/clk/CU x 256 CU x 2.4 GHz
+
+CONFIGS = {   # BASELINE.json configs: width, height, spp, grid half extent, accel
+    2: (1920, 1080, 100, 11, "brute"),
+    3: (1920, 1080, 10000, 11, "lbvh"),
+    4: (1920, 1080, 10000, 11, "lbvh"),
+    5: (3840, 2160, 1000, 158, "lbvh"),
+}
 
 
-def host_cores() -> int:
+def host_cpus() -> dict:
+    """CPUs this process may use (affinity, capped by a cgroup CPU quota) and the machine's."""
     try:
-        n = len(os.sched_getaffinity(0))
+        aff = len(os.sched_getaffinity(0))
     except AttributeError:
-        n = os.cpu_count() or 1
-    return max(1, min(n, 16))    # the GPU box grants a 16-CPU share
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for ln in Path("/proc/cpuinfo").read_text().splitlines():
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"threads": max(1, min(aff, quota) if quota else aff), "affinity": aff, "cgroup_quota": quota,
+            "nproc": os.cpu_count(), "model": model}
 
 
-def cpu_baseline(width: int, height: int, spp: int, gpu_accum=None, gpu_rgba8=None,
+def cpu_baseline(width: int, height: int, spp: int, grid: int, rng_mode: int, gpu_accum=None, gpu_rgba8=None,
                  target_s: float = 15.0) -> dict:
     """The CPU oracle (C++ restatement of the shaders, brute-force closest hit) on this host's
-    cores, on a bounded sample of the bench workload itself: evenly spaced rows of the bench frame
-    at its full spp, sized to ~`target_s` of CPU work from a timed config-1 frame (1920x1080 at
-    1 spp). Msamples/s is spp-independent. The same rows of the GPU's bench frame
-    (gpu_accum / gpu_rgba8, numpy [H, W, 4]) are compared with the oracle's: exact match and PSNR
-    of the rgba8 image (BASELINE.json's "PSNR vs CPU ref")."""
+    cores, on a bounded sample of the bench frame itself: 8 blocks (one row per thread, a few
+    pixels wide) of the frame at its full spp, spread over the image, sized to ~`target_s` of CPU work from a timed config-1 frame
+    (1920x1080 at 1 spp). The same pixels of the GPU's bench frame (numpy [H, W, 4]) are compared
+    with the oracle's: exact match and PSNR of the rgba8 pixels (BASELINE.json's "PSNR vs CPU ref")."""
     import numpy as np
     from oracle import oracle
     oracle.build()
-    sc = oracle.generate_scene(0.0)
-    threads = host_cores()
+    sc = oracle.generate_scene(0.0, grid)
+    cpus = host_cpus()
+    threads = cpus["threads"]
+    opts = oracle.options(rng_mode=rng_mode)
     t0 = time.perf_counter()
-    _, _, st1 = oracle.render(sc, oracle.render_call_info(1, width, height), width, height, threads=threads)
+    _, _, st1 = oracle.render(oracle.generate_scene(0.0), oracle.render_call_info(1, 1920, 1080), 1920, 1080,
+                              threads=threads)
     t1 = time.perf_counter() - t0
-    per_row = t1 / height * spp   # seconds per row of the bench frame
-    if per_row * threads > target_s:   # one row per thread would already exceed the budget
-        return {"value": round(width * height / t1 / 1e6, 4), "unit": "Msamples/s", "cores": threads,
-                "kind": "port",
-                "sample": f"config 1 frame ({width}x{height}, 1 spp, depth 50), brute-force closest hit, "
-                          f"{threads} threads, {t1:.2f} s (rows of the {spp}-spp bench frame would exceed "
-                          f"{target_s:.0f} s)", "config1_frame_s": round(t1, 3)}
-    n_rows = int(max(threads, min(height, round(target_s / max(per_row, 1e-9)))))
-    rows = np.unique(np.linspace(0, height - 1, n_rows).round().astype(np.uint32))
-    t0 = time.perf_counter()
-    acc, out, st = oracle.render(sc, oracle.render_call_info(spp, width, height), width, len(rows),
-                                 rows=rows, threads=threads)
-    dt = time.perf_counter() - t0
-    res = {"value": round(width * len(rows) * spp / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads,
-           "kind": "port",
-           "sample": f"{len(rows)} evenly spaced rows of the bench frame ({width} px, {spp} spp, depth 50), "
-                     f"brute-force closest hit, {threads} threads, {dt:.2f} s; config 1 frame "
-                     f"({width}x{height}, 1 spp) alone {t1:.2f} s; {st[0] / max(1, st[1]):.3f} segments/sample",
-           "config1_frame_s": round(t1, 3)}
-    if gpu_accum is not None and gpu_rgba8 is not None:
-        ga, go = gpu_accum[rows.astype(np.int64)], gpu_rgba8[rows.astype(np.int64)]
-        mse = float(np.mean((go[..., :3].astype(np.float64) - out[..., :3].astype(np.float64)) ** 2))
-        res["parity"] = {"rows": int(len(rows)), "accum_bit_exact": bool(np.array_equal(ga, acc)),
-                         "rgba8_equal": bool(np.array_equal(go, out)),
+    rate = 1920 * 1080 / t1   # samples/s on the canonical scene at 1 spp (spp-independent, SURVEY.md 8(d))
+    # blocks of `nr` rows x bw pixels (one oracle thread per row), evenly spread
+    nr = min(threads, height)
+    cost_scale = max(1.0, len(sc) / 488.0)   # brute force: cost per sample ~ sphere count
+    pixels = max(nr, int(rate * target_s / cost_scale / max(1, spp)))
+    n_blocks = 8
+    bw = max(1, min(width, pixels // (n_blocks * nr)))
+    ys = np.linspace(0, height - nr, n_blocks).round().astype(int)
+    xs = np.linspace(0, width - bw, n_blocks).round().astype(int)[::-1]
+    samples, dt, same_acc, same_px, sq = 0, 0.0, True, True, []
+    st = [0, 0, 0]
+    for y, x in zip(ys, xs):
+        rows = np.arange(y, y + nr, dtype=np.uint32)
+        t0 = time.perf_counter()
+        acc, out, s = oracle.render(sc, oracle.render_call_info(spp, width, height, (int(x), 0)), bw, len(rows),
+                                    rows=rows, opts=opts, threads=threads)
+        dt += time.perf_counter() - t0
+        samples += bw * len(rows) * spp
+        st = [a + b for a, b in zip(st, s)]
+        if gpu_accum is not None:
+            ga = gpu_accum[y:y + nr, x:x + bw]
+            go = gpu_rgba8[y:y + nr, x:x + bw]
+            same_acc &= bool(np.array_equal(ga, acc))
+            same_px &= bool(np.array_equal(go, out))
+            sq.append(((go[..., :3].astype(np.float64) - out[..., :3]) ** 2).ravel())
+    res = {"value": round(samples / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+           "nproc": cpus["nproc"], "cpu_model": cpus["model"], "affinity": cpus["affinity"],
+           "cgroup_quota": cpus["cgroup_quota"],
+           "sample": f"{n_blocks} blocks of {nr} rows x {bw} px of the bench frame ({width}x{height}, {spp} spp, "
+                     f"depth 50, {len(sc)} spheres, {'hash' if rng_mode == 2 else 'reference'} stream), brute-force "
+                     f"closest hit, {threads} threads, {dt:.2f} s; config 1 frame (1920x1080, 1 spp) alone "
+                     f"{t1:.2f} s = {rate / 1e6:.3f} Msamples/s; {st[0] / max(1, st[1]):.3f} segments/sample",
+           "config1_frame_s": round(t1, 3), "config1_msamples_per_s": round(rate / 1e6, 4)}
+    if gpu_accum is not None:
+        mse = float(np.mean(np.concatenate(sq))) if sq else 0.0
+        res["parity"] = {"pixels": int(n_blocks * nr * bw), "accum_bit_exact": same_acc,
+                         "rgba8_equal": same_px,
                          "psnr_db": "inf" if mse == 0.0 else round(float(10.0 * np.log10(255.0 ** 2 / mse)), 2)}
     return res
 
 
-def _pmc_record(path: Path, key: str):
-    """A committed rocprofv3 --pmc summary (scripts/pmc_to_json.py) for this workload, or None."""
+def lib_sha256() -> str:
+    from rtvk import abi
+    return hashlib.sha256(Path(abi.LIB_PATH).read_bytes()).hexdigest()[:16]
+
+
+def pmc_record(key: str, sha: str) -> dict:
+    """rocprofv3 --pmc summary of this workload (scripts/pmc_to_json.py), used only when it was
+    measured on this exact library build (its sha256 prefix)."""
+    path = ROOT / "profiles" / "pmc.json"
     try:
-        return json.loads(path.read_text()).get(key)
+        rec = json.loads(path.read_text()).get(key)
     except (OSError, ValueError):
-        return None
+        rec = None
+    if not rec:
+        return {"pmc": f"no PMC record for {key} in profiles/pmc.json"}
+    if rec.get("lib_sha256") != sha:
+        return {"pmc": f"stale: profiles/pmc.json {key} measured on build {rec.get('lib_sha256')}, this build is {sha}"}
+    return {k: rec[k] for k in ("valu_issue_busy", "lane_util", "hbm_bytes_per_launch", "kernel_ms") if k in rec}
 
 
 def main() -> int:
-    ap = argparse.ArgumentParser(description=__doc__)
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--spp", type=int, default=100)
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--accel", choices=["lbvh", "brute"], default="lbvh")
-    ap.add_argument("--grid", type=int, default=11, help="scene grid half extent (11: 488 spheres)")
-    ap.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=None,
-                    help="BASELINE.json config preset: 2/3/4 = 1920x1080 at 100/10000/10000 spp, "
-                         "5 = 3840x2160, 99 860 spheres, 1000 spp (overrides --width/--height/--spp/--grid)")
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", type=int, choices=sorted(CONFIGS), default=3)
+    ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--grid", type=int, default=None, help="scene grid half extent (11: 488 spheres)")
+    ap.add_argument("--accel", choices=["lbvh", "brute"], default=None)
+    ap.add_argument("--rng", choices=["hash", "stream"], default="hash")
     ap.add_argument("--count-spp", type=int, default=100,
-                    help="spp of the instrumented (test-counting) launch; its counts are scaled to --spp "
-                         "(per-sample statistics are stationary: same scene, same per-pixel streams)")
+                    help="spp of the instrumented (test-counting) launch; its counts are scaled to the frame's "
+                         "spp (per-sample statistics are stationary: same scene, same streams)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-brute-line", action="store_true", help="skip the brute-force side measurement")
-    ap.add_argument("--profile", action="store_true", help="short run for rocprofv3 (no side legs)")
-    ap.add_argument("--walk", type=int, default=0,
-                    help="LBVH walk form (A/B only): 0 default escape-link, 2 ordered, 4 compact nodes")
-    ap.add_argument("--split", choices=["samples", "strips"], default="samples",
-                    help="N>1 work split: samples (each rank renders the frame with spp/N samples and "
-                         "stream salt number+rank, row-slice reduction) or strips (8-row strips of the "
-                         "one-GPU frame); identical at N=1")
+    ap.add_argument("--no-side-lines", action="store_true", help="skip the other-stream and brute-force lines")
+    ap.add_argument("--profile", action="store_true", help="short run for rocprofv3 (no side legs, one frame in flight)")
+    ap.add_argument("--walk", type=int, default=0, help="LBVH walk form (A/B only): 0 auto, 6 one LDS copy, 10 L2")
     ap.add_argument("--inflight", type=int, default=2,
-                    help="frames in flight: contexts + streams used round robin, so frame k+1's blocks "
-                         "start on the CUs frame k's tail leaves idle (1 = one frame at a time)")
-    ap.add_argument("--exchange-test", action="store_true",
-                    help="test only: one rank on a one-rank NCCL group still runs the sample-split "
-                         "exchange (RCCL code path on a one-GPU box)")
+                    help="frames in flight: contexts + streams used round robin, so frame k+1's blocks start on "
+                         "the CUs frame k's tail leaves idle (1 = one frame at a time)")
     args = ap.parse_args()
+    W0, H0, spp0, grid0, accel0 = CONFIGS[args.config]
+    W, H = args.width or W0, args.height or H0
+    spp = args.spp if args.spp is not None else spp0
+    grid = args.grid if args.grid is not None else grid0
+    accel_name = args.accel or accel0
+    if args.profile:
+        args.inflight = 1
 
     import numpy as np
     import torch
@@ -132,44 +188,25 @@ def main() -> int:
 
     import rtvk
     from rtvk import abi
-    from rtvk.dist import (DistributedRenderer, SampleSplitRenderer, hip_assembler, hip_band_renderer,
-                           hip_full_renderer, hip_reducer)
+    from rtvk.dist import DistributedRenderer, hip_assembler, hip_band_renderer
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    # RT_SHARE_DEVICE=1 (rehearsal only): map ranks onto the visible devices round robin, so the
-    # multi-rank code path can be exercised on a one-GPU box.
-    ndev = torch.cuda.device_count()
-    # RCCL refuses two ranks on one device, so the rehearsal runs over gloo with host staging.
-    shared = os.environ.get("RT_SHARE_DEVICE") == "1" and ndev > 0
-    if shared:
-        local = local % ndev
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1 or args.exchange_test:
-        if shared:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=dev)
-    if args.exchange_test:
-        import rtvk.dist as rtvk_dist
-        rtvk_dist._force_collective = True
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
 
-    if args.config is not None:
-        args.width, args.height = (3840, 2160) if args.config == 5 else (1920, 1080)
-        args.spp = {2: 100, 3: 10000, 4: 10000, 5: 1000}[args.config]
-        args.grid = 158 if args.config == 5 else 11
-    W, H, spp = args.width, args.height, args.spp
-    accel = abi.RT_ACCEL_BRUTE if args.accel == "brute" else abi.RT_ACCEL_LBVH
-    scene = rtvk.generateRandomScene(0.0, args.grid)
+    accel = abi.RT_ACCEL_BRUTE if accel_name == "brute" else abi.RT_ACCEL_LBVH
+    rng_mode = abi.RT_RNG_SAMPLE_HASH if args.rng == "hash" else abi.RT_RNG_PIXEL_STREAM
+    scene = rtvk.generateRandomScene(0.0, grid)
     rci = rtvk.canonical_render_call_info(spp, W, H)
-    opts = rtvk.make_options(accel=accel)
+    opts = rtvk.make_options(accel=accel, rng_mode=rng_mode)
     opts.reserved[1] = args.walk
     ev = []
-    split = args.split if (world > 1 or args.exchange_test) else "strips"
 
     def timed(fn):
         """fn(*a) bracketed by HIP events on the stream it is launched on (the slot's)."""
@@ -189,21 +226,16 @@ def main() -> int:
             self.renderer = rtvk.Renderer(local)
             self.stream = torch.cuda.Stream(device=dev)
             with torch.cuda.stream(self.stream):
-                if split == "samples":
-                    self.dr = SampleSplitRenderer(W, H, spp, rci.number, dev,
-                                                  timed(hip_full_renderer(self.renderer, rci, opts)),
-                                                  hip_reducer(self.renderer))
-                else:
-                    self.dr = DistributedRenderer(W, H, dev, timed(hip_band_renderer(self.renderer, rci, opts)),
-                                                  hip_assembler(self.renderer))
+                self.dr = DistributedRenderer(W, H, dev, timed(hip_band_renderer(self.renderer, rci, opts)),
+                                              hip_assembler(self.renderer))
 
         def frame(self):
             # The reference rebuilds its acceleration structure every frame (src/vulkan.h:1020-1059)
-            # and SURVEY.md 8(d) counts the build in the wall clock: rebuild, then render + exchange.
+            # and SURVEY.md 8(d) counts the build in the wall clock: rebuild, then render + gather.
             # The host build runs while earlier frames render (its upload is queued behind them).
             with torch.cuda.stream(self.stream):
                 self.renderer.set_scene(scene, stream=self.stream)
-                self.dr.step()
+                return self.dr.step()
 
     slots = [Slot() for _ in range(max(1, args.inflight))]
     renderer, dr = slots[0].renderer, slots[0].dr
@@ -223,36 +255,34 @@ def main() -> int:
 
     def frame():
         nonlocal n_frames
-        slots[n_frames % len(slots)].frame()
+        r = slots[n_frames % len(slots)].frame()
         n_frames += 1
+        return r
 
     for _ in range(max(args.warmup, len(slots))):   # every slot has rendered once (LPT order)
         frame()
     barrier()
     ev.clear()
     t0 = time.perf_counter()
+    last = None
     for _ in range(args.steps):
-        frame()
+        last = frame()
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if shared else dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kernel_ms_inflight = sum(a.elapsed_time(b) for a, b in ev) / max(1, len(ev))
     # Kernel duration for the roofline: with frames in flight a launch's events also span the wait
-    # for the CUs the previous frame still holds, so the same launch (this rank's share of the
-    # frame, same slot and LPT order) is timed alone, back to back, right after the timed region.
+    # for the CUs the previous frame still holds, so this rank's band is timed alone, back to
+    # back, right after the timed region (same slot, same LPT order).
     ev.clear()
     sl0 = slots[0]
-    n_iso = max(2, min(args.steps, 5))
+    n_iso = max(2, min(args.steps, 3))
     for _ in range(n_iso):
         with torch.cuda.stream(sl0.stream):
-            if split == "samples":
-                if sl0.dr.spp_r:
-                    sl0.dr.render_full(sl0.dr.number, sl0.dr.spp_r, sl0.dr.accum, sl0.dr.out)
-            else:
-                sl0.dr.render_band(sl0.dr.rows, sl0.dr.accum[: sl0.dr.n], sl0.dr.out[: sl0.dr.n])
+            sl0.dr.render_band(sl0.dr.rows, sl0.dr.accum[: sl0.dr.n], sl0.dr.out[: sl0.dr.n])
         torch.cuda.synchronize()
     kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / max(1, len(ev))
     # the per-frame rebuild alone (host build + upload), outside the timed region
@@ -261,74 +291,70 @@ def main() -> int:
     renderer.set_scene(scene)
     torch.cuda.synchronize()
     build_ms = (time.perf_counter() - tb) * 1e3
-    st = renderer.stats()   # last frame's counters on this rank
+    st = renderer.stats()   # this rank's last band
+    info = renderer.launch_info()
 
     samples_per_step = W * H * spp
     value = samples_per_step * args.steps / elapsed / 1e6
 
     # Algorithmic work of one launch on this rank, counted by the instrumented build of the same
     # kernel (identical image, same traversal; outside the timed region).
-    local_rows = len(dr.rows_np) if split == "strips" else (H if dr.spp_r else 0)
-    local_spp = spp if split == "strips" else dr.spp_r
-    cnt_opts = rtvk.make_options(accel=accel, count_tests=True)
+    local_rows = dr.n
+    cnt_opts = rtvk.make_options(accel=accel, rng_mode=rng_mode, count_tests=True)
     cnt_opts.reserved[1] = args.walk
-    cnt_spp = max(1, min(local_spp, args.count_spp))
+    cnt_spp = max(1, min(spp, args.count_spp))
     if local_rows:
         acc = torch.zeros((local_rows, W, 4), dtype=torch.float32, device=dev)
         out = torch.zeros((local_rows, W, 4), dtype=torch.uint8, device=dev)
-        crci = rtvk.canonical_render_call_info(cnt_spp, W, H)
-        if split == "samples":
-            crci.number = dr.number
-        renderer.render_device(crci, acc, out, rows=dr.rows if split == "strips" else None,
+        renderer.render_device(rtvk.canonical_render_call_info(cnt_spp, W, H), acc, out, rows=dr.rows,
                                options=cnt_opts)
         torch.cuda.synchronize()
         cs = renderer.stats()
         del acc, out
     else:
         cs = rtvk.Stats()
-    scale = local_spp / cnt_spp
+    scale = spp / cnt_spp
     flops = (cs.box_tests * FLOP_PER_BOX_TEST + cs.sphere_tests * FLOP_PER_SPHERE_TEST) * scale
     achieved = flops / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
 
     result = None
     if rank == 0:
-        traffic = None
-        tf = ROOT / "profiles" / "pmc_traffic.json"
-        if tf.exists():
-            try:
-                tj = json.loads(tf.read_text())
-                key = f"{args.accel}-{W}x{H}-{spp}spp-grid{args.grid}-n{world}"
-                traffic = tj.get(key, {}).get("hbm_bytes_per_launch")
-            except (ValueError, OSError):
-                traffic = None
+        sha = lib_sha256()
+        kname = {"lbvh-octant-lds": "rt_trace_lds_kernel<8 octant copies>", "lbvh-lds": "rt_trace_lds_kernel<1 copy>",
+                 "lbvh-treelet": "rt_trace_top_kernel (LDS treelet + L2 subtrees)",
+                 "lbvh-global": "rt_trace_global_kernel"}.get(info["form"], info["form"])
+        if accel == abi.RT_ACCEL_BRUTE:
+            kname = "rt_trace_brute_kernel"
+        key = f"{accel_name}-{args.rng}-{W}x{H}-{spp}spp-grid{grid}-n{world}"
+        pmc = pmc_record(key, sha)
         roof = {"bound": "valu-fp32", "achieved": round(achieved, 3), "peak": VALU_FP32_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / VALU_FP32_PEAK_TFLOPS, 4), "traffic": traffic,
-                "kernel": ("rt_trace_brute_kernel" if accel != 2 else
-                           "rt_trace_top_kernel (LDS treelet + L2 subtrees)" if renderer.scene_array(8)["device_built"]
-                           else "rt_trace_lbvh_kernel (octant LDS walk)"),
-                "kernel_ms": round(kernel_ms, 4),
-                "kernel_timing": f"{n_iso} launches of this frame timed alone after the timed region "
-                                 "(HIP events on the launch stream); with frames in flight a launch "
-                                 f"spans {kernel_ms_inflight:.2f} ms including the wait for the previous "
-                                 "frame's CUs",
+                "unit": "TFLOP/s", "frac": round(achieved / VALU_FP32_PEAK_TFLOPS, 4),
+                "traffic": pmc.get("hbm_bytes_per_launch"),
+                "kernel": kname, "kernel_ms": round(kernel_ms, 4),
+                "frac_basis": f"per isolated launch: algorithmic FLOP of this rank's band / its launch time, "
+                              f"{n_iso} launches timed alone after the timed region (HIP events on the launch "
+                              f"stream); with frames in flight a launch spans {kernel_ms_inflight:.2f} ms "
+                              "including the wait for the previous frame's CUs",
+                "frac_per_step": round(flops / (elapsed / args.steps) / 1e12 / VALU_FP32_PEAK_TFLOPS, 4),
                 "flop_per_launch": int(flops), "box_tests": int(cs.box_tests * scale),
                 "sphere_tests": int(cs.sphere_tests * scale),
-                "flop_model": "20/box test + 23/sphere test (SURVEY.md 8(d)); counts from the "
-                              f"instrumented build of the same kernel at {cnt_spp} spp"
-                              + (f", x{scale:g}" if scale != 1 else "")}
-        if accel == 2:   # the other fraction SURVEY.md 8(d) asks for: the LBVH's own bytes, from LDS
+                "flop_model": "20/box test + 23/sphere test (SURVEY.md 8(d)); counts from the instrumented "
+                              f"build of the same kernel at {cnt_spp} spp" + (f", x{scale:g}" if scale != 1 else ""),
+                "lib_sha256": sha}
+        roof.update({k: v for k, v in pmc.items() if k in ("valu_issue_busy", "lane_util", "pmc")})
+        if accel != abi.RT_ACCEL_BRUTE:   # the other fraction SURVEY.md 8(d) asks for: the LBVH's own bytes
             lds_bytes = (cs.box_tests * BYTES_PER_BOX_TEST + cs.sphere_tests * BYTES_PER_SPHERE_TEST) * scale
             lds_tbps = lds_bytes / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
             roof["lds"] = {"achieved": round(lds_tbps, 3), "peak": round(LDS_PEAK_TBPS, 1), "unit": "TB/s",
                            "frac": round(lds_tbps / LDS_PEAK_TBPS, 4), "bytes_per_launch": int(lds_bytes),
-                           "model": "32 B per box test + 16 B per sphere test (node and leaf records; "
-                                    "from L2 instead of LDS below the treelet of trees too big for LDS)"}
-        valu = _pmc_record(ROOT / "profiles" / "pmc_valu.json", f"{args.accel}-{W}x{H}-{spp}spp-grid{args.grid}-n{world}")
-        if valu:
-            roof["valu_issue_busy"] = valu.get("valu_issue_busy")
-            roof["lane_util"] = valu.get("lane_util")
+                           "model": "32 B per box test + 16 B per sphere test (node and leaf records; from L2 "
+                                    "instead of LDS below the treelet of trees too big for LDS)"}
+        cfg_name = (f"BASELINE config {args.config}" if world == 1 or args.config not in (3, 4)
+                    else f"BASELINE config {4 if world == 8 else 3} frame on {world} GPUs")
+        default_shape = (W, H, spp, grid, accel_name) == CONFIGS[args.config]
         result = {
-            "metric": "Msamples/s (1920x1080 RTIOW scene, depth 50)",
+            "metric": "Msamples/s (1920x1080 RTIOW scene, depth 50)" if (W, H) == (1920, 1080)
+                      else f"Msamples/s ({W}x{H} RTIOW scene, depth 50)",
             "value": round(value, 2),
             "unit": "Msamples/s",
             "n_gpus": world,
@@ -339,15 +365,14 @@ def main() -> int:
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": f"synthetic: canonical scene generateRandomScene(t=0), {len(scene)} spheres, "
-                    "camera (13,11,-3) -> origin, global per-pixel seeds TEA(TEA(x,y),0)",
-            "config": {"workload": f"rtiow-{W}x{H}-{spp}spp-depth50"
-                                   + (f" (BASELINE config {args.config})" if args.config else
-                                      " (BASELINE config 2 input)" if (W, H, spp, args.grid) == (1920, 1080, 100, 11) else ""),
+            "data": f"synthetic: canonical scene generateRandomScene(t=0), grid {2 * grid}x{2 * grid} "
+                    f"({len(scene)} spheres), camera (13,11,-3) -> origin, global per-pixel seeds "
+                    f"TEA(TEA(x,y),0), {'counter-based per-sample streams (RT_RNG_SAMPLE_HASH)' if args.rng == 'hash' else 'the reference per-pixel LCG stream'}",
+            "config": {"workload": f"rtiow-{W}x{H}-{spp}spp-depth50-{accel_name}"
+                                   + (f" ({cfg_name})" if default_shape else " (custom)"),
                        "width": W, "height": H, "spp": spp, "depth": 50, "spheres": len(scene),
-                       "accel": args.accel,
-                       "parallelism": (f"sample-split x{world} (number+rank) + rccl all-to-all row reduction "
-                                       "+ gather" if split == "samples" else f"row-strips x{world} + rccl gather"),
+                       "accel": accel_name, "rng": args.rng, "sample_chunks": info["chunks"],
+                       "parallelism": f"8-row strips x{world} + rccl gather to rank 0",
                        "frames_in_flight": len(slots)},
             "segments_per_sample": round(st.segments / max(1, st.samples), 4),
             "scene_setup_ms": round(t_scene * 1e3, 2),
@@ -358,36 +383,50 @@ def main() -> int:
             "context": {"reference_rx6800xt_vulkan_rt_msamples": 1658.9,
                         "source": "README.md:57,61 via BASELINE.md (different GPU, HW RT cores)"},
         }
-    # Side measurement: brute force (BASELINE config 2 as specified: no BVH), N = 1 only.
-    if world == 1 and not args.no_brute_line and not args.profile and accel != abi.RT_ACCEL_BRUTE:
-        bopts = rtvk.make_options(accel=abi.RT_ACCEL_BRUTE)
-        acc = torch.zeros((H, W, 4), dtype=torch.float32, device=dev)
-        out = torch.zeros((H, W, 4), dtype=torch.uint8, device=dev)
-        renderer.render_device(rci, acc, out, options=bopts)
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        reps = 2
-        stream = torch.cuda.current_stream()
-        e0.record(stream)
-        for _ in range(reps):
-            renderer.render_device(rci, acc, out, options=bopts)
-        e1.record(stream)
-        torch.cuda.synchronize()
-        bms = e0.elapsed_time(e1) / reps
-        bst = renderer.stats()
-        bflops = bst.segments * len(scene) * FLOP_PER_SPHERE_TEST
-        result["brute_force"] = {
-            "value": round(samples_per_step / (bms * 1e-3) / 1e6, 2), "unit": "Msamples/s",
-            "kernel_ms": round(bms, 3),
-            "roofline": {"bound": "valu-fp32", "achieved": round(bflops / (bms * 1e-3) / 1e12, 3),
-                         "peak": VALU_FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(bflops / (bms * 1e-3) / 1e12 / VALU_FP32_PEAK_TFLOPS, 4)}}
-        del acc, out
+    frame_np = None
+    if rank == 0 and world == 1:
+        fa, fo = last
+        frame_np = (fa.cpu().numpy(), fo.cpu().numpy())
+    # Side lines (N = 1): the same frame with the other random stream, and BASELINE config 2 as
+    # specified (100 spp, brute force).
+    if world == 1 and not args.no_side_lines and not args.profile:
+        def time_frames(o, w, h, s, n):
+            a = torch.zeros((h, w, 4), dtype=torch.float32, device=dev)
+            b = torch.zeros((h, w, 4), dtype=torch.uint8, device=dev)
+            r = rtvk.canonical_render_call_info(s, w, h)
+            renderer.render_device(r, a, b, options=o)   # warm: LPT order, occupancy
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(n):
+                renderer.render_device(r, a, b, options=o)
+            e1.record()
+            torch.cuda.synchronize()
+            return e0.elapsed_time(e1) / n, a, b
+        if accel != abi.RT_ACCEL_BRUTE:
+            other = abi.RT_RNG_PIXEL_STREAM if rng_mode == abi.RT_RNG_SAMPLE_HASH else abi.RT_RNG_SAMPLE_HASH
+            oms, _, ob = time_frames(rtvk.make_options(accel=accel, rng_mode=other), W, H, spp, 1)
+            o_np = ob.cpu().numpy()
+            mse = float(np.mean((o_np[..., :3].astype(np.float64) - frame_np[1][..., :3]) ** 2))
+            result["reference_stream" if other == abi.RT_RNG_PIXEL_STREAM else "hash_stream"] = {
+                "value": round(samples_per_step / (oms * 1e-3) / 1e6, 2), "unit": "Msamples/s",
+                "kernel_ms": round(oms, 3), "rng": "stream" if other == abi.RT_RNG_PIXEL_STREAM else "hash",
+                "psnr_vs_headline_frame_db": "inf" if mse == 0 else round(10 * np.log10(255 ** 2 / mse), 2),
+                "note": "same frame, other random stream (two independent Monte-Carlo estimates of one picture)"}
+        if grid == 11:
+            bw_, bh_, bspp = CONFIGS[2][:3]
+            bms, _, _ = time_frames(rtvk.make_options(accel=abi.RT_ACCEL_BRUTE, rng_mode=rng_mode), bw_, bh_, bspp, 2)
+            bst = renderer.stats()
+            bflops = bst.segments * len(scene) * FLOP_PER_SPHERE_TEST
+            result["brute_force"] = {
+                "workload": "BASELINE config 2: 1920x1080, 100 spp, brute-force sphere list",
+                "value": round(bw_ * bh_ * bspp / (bms * 1e-3) / 1e6, 2), "unit": "Msamples/s",
+                "kernel_ms": round(bms, 3),
+                "roofline": {"bound": "valu-fp32", "achieved": round(bflops / (bms * 1e-3) / 1e12, 3),
+                             "peak": VALU_FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                             "frac": round(bflops / (bms * 1e-3) / 1e12 / VALU_FP32_PEAK_TFLOPS, 4)}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile:
-        fa, fo = (slots[0].dr.accum[: slots[0].dr.n], slots[0].dr.out[: slots[0].dr.n]) if split == "strips" \
-            else (None, None)   # at one rank the strips frame is the whole frame in row order
-        result["cpu_baseline"] = cpu_baseline(W, H, spp, fa.cpu().numpy() if fa is not None else None,
-                                              fo.cpu().numpy() if fo is not None else None)
+        result["cpu_baseline"] = cpu_baseline(W, H, spp, grid, rng_mode, frame_np[0], frame_np[1])
     if rank == 0:
         print(json.dumps(result), flush=True)
     for sl in slots:

@@ -25,8 +25,13 @@
  *                            (src/vulkan.h:1061-1106) + vkCmdTraceRaysKHR(W, band_h, 1)
  *                            (src/vulkan.h:994-995) executing shaders/shader.{rgen,rint,rchit,rmiss}.
  *                            Device pointers, caller's stream, asynchronous.
+ *   rt_multi_*()             one process driving N devices (src/ray_trace.cpp:42-105 creates one
+ *                            Vulkan device per GPU, :74-93 splits the image into bands): one RCCL
+ *                            communicator over the devices (ncclCommInitAll), the image tiled into
+ *                            8-row strips dealt round robin, every device's strips gathered to
+ *                            device 0 over xGMI (grouped ncclSend/ncclRecv) and reordered there.
  *   rt_render()              host-pointer convenience wrapper (one call = one frame); rci_count > 1
- *                            renders one band per GPU like src/ray_trace.cpp:74-93.
+ *                            renders one band per GPU like src/ray_trace.cpp:74-93, gathered by RCCL.
  *
  * Error model: every rt_* call returns RT_OK (0) or a negative rt_status; the message of the
  * calling thread's last failure is rt_last_error(). Exceptions never cross this boundary (the
@@ -47,7 +52,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1u
+#define RT_ABI_VERSION 2u
 
 typedef enum rt_status {
     RT_OK = 0,
@@ -68,8 +73,13 @@ typedef enum rt_seed_mode {
 /* Random stream layout. */
 typedef enum rt_rng_mode {
     RT_RNG_PIXEL_STREAM = 0,   /* reference: one LCG stream per pixel runs through every sample (random.glsl)   */
-    RT_RNG_SAMPLE_COUNTER = 1  /* counter-based: sample s of a pixel starts at TEA(pixel_seed, s): samples of a
-                                  pixel are independent and may be split across launches / devices             */
+    RT_RNG_SAMPLE_COUNTER = 1, /* counter-based: sample s of a pixel starts at TEA(pixel_seed, s): samples of a
+                                  pixel are independent and may be split across launches                        */
+    RT_RNG_SAMPLE_HASH = 2     /* counter-based (the north star's RNG): sample s starts its LCG at
+                                  lowbias32(pixel_seed + 0x9E3779B9 * s) and per-sample colours are summed in
+                                  20.44 fixed point, so the library splits a pixel's samples into chunks run
+                                  by any lanes in any order with bit-identical results;
+                                  samplesPerRenderCall <= 2^19                                                */
 } rt_rng_mode;
 
 /* Closest-hit search structure (the reference uses the driver's BVH, src/vulkan.h:395-554). */
@@ -85,14 +95,13 @@ typedef struct rt_options {
     uint32_t rng_mode;    /* rt_rng_mode                                                         */
     uint32_t accel;       /* rt_accel                                                            */
     uint32_t accumulate;  /* 0: clear the accumulator first (src/vulkan.h:1081-1086); 1: add on top */
-    uint32_t sample_base; /* RT_RNG_SAMPLE_COUNTER only: index of this launch's first sample       */
+    uint32_t sample_base; /* counter modes only: index of this launch's first sample               */
     uint32_t reserved[2]; /* 0 for production. Diagnostics / A/B only: reserved[0] bit 0 = count box
                              and sphere tests (slower instrumented build, rt_get_stats);
                              reserved[1] = LBVH walk form: 0 automatic (octant node copies in LDS
-                             when they fit; LDS treelet + L2 subtrees for trees too big for LDS),
-                             2 ordered two-wide walk, 4 compact 16-B nodes, 5 scene records from
-                             global memory, 6 one LDS node copy, 7 + tail-compaction pool,
-                             8 octant copies, 10 whole tree from L2 */
+                             when they fit, else one copy in LDS, else an LDS treelet over L2
+                             subtrees), 6 one LDS node copy, 8 octant copies, 10 every node from
+                             L2 */
 } rt_options;
 
 /* Statistics of the last rt_render_device() on a context (valid after its stream completes). */
@@ -154,36 +163,50 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
 int rt_get_stats(rt_context* ctx, rt_stats* out);
 /*
  * Scatter band rows into a full image on the device: dst_row[rows[i]] = src_row[i]
- * (the host-side reorder after the multi-GPU gather).
+ * (the reorder after the multi-GPU gather). dst has dst_rows rows of `width`
+ * texels; map entries >= dst_rows are skipped.
  */
 int rt_scatter_rows(rt_context* ctx, const float* src_accum, const uint8_t* src_rgba8,
-                    const uint32_t* rows, uint32_t n_rows, uint32_t width, float* dst_accum,
-                    uint8_t* dst_rgba8, void* stream);
+                    const uint32_t* rows, uint32_t n_rows, uint32_t width, uint32_t dst_rows,
+                    float* dst_accum, uint8_t* dst_rgba8, void* stream);
 
 /*
  * Tonemap a summed accumulator to rgba8 on the device, exactly as the trace kernel's store
  * (shader.rgen:65-66): rgba8 = round(clamp(sqrt(sum / spp), 0, 1) * 255) per channel, alpha 255.
- * For a frame assembled from several launches (the sample-split multi-GPU frame: rank r renders
- * spp_r samples with RenderCallInfo.number = r, the float sums are added in rank order).
  * accum_rgba32f: n_texels float4 (DEVICE); out_rgba8: n_texels x 4 bytes (DEVICE).
  */
 int rt_resolve_rgba8(rt_context* ctx, const float* accum_rgba32f, uint64_t n_texels, uint32_t spp,
                      uint8_t* out_rgba8, void* stream);
 
+/* ---- multi-device (one process, N GPUs, RCCL over xGMI) ----------------------------- */
+typedef struct rt_multi rt_multi;
+/* Devices 0 .. n-1, n = min(gpu_count, visible devices) (>= 1): one context and one stream per
+ * device and one RCCL communicator over them (ncclCommInitAll). */
+int rt_multi_create(uint32_t gpu_count, rt_multi** out);
+int rt_multi_destroy(rt_multi* m);
+int rt_multi_device_count(const rt_multi* m, uint32_t* n);
+/* rt_set_scene on every device (host spheres). */
+int rt_multi_set_scene(rt_multi* m, const Sphere* spheres, uint32_t count);
 /*
- * The sample-split reduction in one pass: slices = n_slices consecutive accumulators of n_texels
- * float4 each (rank order); accum_out (optional, may alias slice 0) = their float sum added in
- * slice order, alpha 1.0 (shader.rgen:63); out_rgba8 = the tonemap of that sum as
- * rt_resolve_rgba8. All pointers DEVICE.
+ * One frame of the whole image rci->image_size (rci->offset ignored). The rows are cut into
+ * 8-row strips, strip k rendered by device k % n (rt_render_device with a rows map, global
+ * seeds); every device's strips travel to device 0 in one RCCL group (ncclSend / ncclRecv, device
+ * 0 included) and are reordered into accum_rgba32f / out_rgba8: DEVICE pointers on device 0,
+ * W*H texels. Asynchronous on `stream` (a hipStream_t of device 0; NULL = the legacy stream): the
+ * call returns once everything is queued. The image equals the one-device image bit for bit.
+ * With opt->accumulate each device adds to its own strips of the previous frame of the same size.
  */
-int rt_reduce_resolve(rt_context* ctx, const float* slices, uint32_t n_slices, uint64_t n_texels,
-                      uint32_t spp, float* accum_out, uint8_t* out_rgba8, void* stream);
+int rt_multi_render(rt_multi* m, const RenderCallInfo* rci, const rt_options* opt,
+                    float* accum_rgba32f, uint8_t* out_rgba8, void* stream);
+/* Sum over the devices of the last frame's statistics (synchronises). */
+int rt_multi_stats(rt_multi* m, rt_stats* out);
 
 /* ---- host-pointer convenience ------------------------------------------------------ */
 /*
  * One frame over the full image rci[0].image_size with host buffers. rci_count bands, band i
  * spanning rows [rci[i].offset.y, rci[i+1].offset.y) (last band to image height), band i on
- * device i % device_count. accum_rgba32f: W*H*4 floats, out_rgba8: W*H*4 bytes (full image).
+ * device i % device_count, gathered to device 0 by RCCL (rt_multi), then copied to the host.
+ * accum_rgba32f: W*H*4 floats (read first when opt->accumulate), out_rgba8: W*H*4 bytes.
  */
 int rt_render(const Sphere* spheres, uint32_t sphere_count, const RenderCallInfo* rci,
               uint32_t rci_count, float* accum_rgba32f, uint8_t* out_rgba8,
@@ -193,8 +216,13 @@ int rt_render(const Sphere* spheres, uint32_t sphere_count, const RenderCallInfo
 int rt_store_ppm(const char* path, const uint8_t* rgba8, uint32_t width, uint32_t height);
 
 /* Diagnostic (tests only): evaluates one arithmetic-contract primitive on `device` for n
- * (x, y) pairs: op 0 sqrt(x), 1 x/y, 2 sin(x), 3 fma(x,y,1), 4 normalize(x,y,0.5).x, 5 pow(x,5). */
+ * (x, y) pairs: op 0 sqrt(x), 1 x/y, 2 sin(x), 3 fma(x,y,1), 4 normalize(x,y,0.5).x, 5 pow(x,5),
+ * 6 sample_seed_hash(bits(x), bits(y)) as bits, 7 / 8 low / high word of the 20.44 fixed-point
+ * value of colour x, as bits. */
 int rt_debug_math(int device, int op, const float* in_pairs, float* out, uint32_t n);
+/* Diagnostic: of ctx's last launch, {sample chunks per pixel, staged kernel form of the scene
+ * (rt_internal.h ACCEL_*), its LDS bytes, CU count}. */
+int rt_debug_launch_info(rt_context* ctx, uint32_t* out4);
 /* Diagnostic: per-phase cycle sums of ctx's last launch, filled only by -DRT_STAMPS builds. */
 int rt_debug_stamps(rt_context* ctx, uint64_t* out8);
 /* Diagnostic: histogram of LBVH box tests per segment of the last instrumented launch
@@ -217,7 +245,9 @@ int rt_debug_tile_cost(rt_context* ctx, uint32_t* out, uint64_t capacity, uint64
 int rt_debug_scene(rt_context* ctx, uint32_t what, void* out, uint64_t capacity, uint64_t* bytes);
 
 /* src/ray_trace.h:9-15 — identical symbol and parameter list. Renders the canonical scene once
- * (t = 0), prints the frame time, stores `render.ppm` when storeRenderResult, and returns. */
+ * (t = 0) on min(gpu_count, visible) GPUs through rt_multi (8-row strips, RCCL gather; the
+ * reference's per-pixel LCG stream with global seeds, so the image does not depend on gpu_count),
+ * prints the frame time, stores `render.ppm` when storeRenderResult, and returns. */
 void ray_trace(uint32_t samples, bool storeRenderResult, uint32_t width, uint32_t height,
                uint32_t gpu_count);
 

@@ -38,6 +38,10 @@ def lib() -> ctypes.CDLL:
         l.orc_random_float.argtypes = [ctypes.POINTER(_U)]
         l.orc_sinf.restype = ctypes.c_float
         l.orc_sinf.argtypes = [ctypes.c_float]
+        l.orc_sample_seed_hash.restype = _U
+        l.orc_sample_seed_hash.argtypes = [_U, _U]
+        l.orc_sample_fixed.restype = ctypes.c_uint64
+        l.orc_sample_fixed.argtypes = [ctypes.c_float]
         l.orc_viewport.restype = None
         l.orc_viewport.argtypes = [_P, _P]
         l.orc_generate_scene.restype = _I
@@ -65,6 +69,16 @@ def random_floats(seed: int, n: int) -> list[float]:
 
 def sinf(x: float) -> float:
     return lib().orc_sinf(x)
+
+
+def sample_seed_hash(pixel_seed: int, s: int) -> int:
+    """RT_RNG_SAMPLE_HASH: LCG start of sample s of a pixel."""
+    return lib().orc_sample_seed_hash(pixel_seed, s)
+
+
+def sample_fixed(c: float) -> int:
+    """RT_RNG_SAMPLE_HASH: 20.44 fixed-point value of a sample colour channel."""
+    return lib().orc_sample_fixed(c)
 
 
 def generate_scene(t: float = 0.0, grid_half_extent: int = 11) -> np.ndarray:

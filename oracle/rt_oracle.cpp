@@ -161,6 +161,23 @@ float rt_sinf(float x) {
     }
 }
 
+// RT_RNG_SAMPLE_HASH: LCG start of sample s (golden-ratio spread + "lowbias32" finaliser).
+inline uint32_t sample_seed_hash(uint32_t pixel_seed, uint32_t s) {
+    uint32_t x = pixel_seed + 0x9E3779B9u * s;
+    x ^= x >> 16;
+    x *= 0x21F0AAADu;
+    x ^= x >> 15;
+    x *= 0x735A2D97u;
+    x ^= x >> 15;
+    return x;
+}
+
+// RT_RNG_SAMPLE_HASH: a colour channel as 20.44 fixed point, truncated (NaN -> 0).
+inline uint64_t sample_fixed(float c) {
+    float v = std::fmin(std::fmax(c, 0.0f), 1.0f) * 0x1p44f;
+    return uint64_t(v);
+}
+
 inline float pow5_glsl(float x) {
     if (x < 0.0f) return std::numeric_limits<float>::quiet_NaN();
     float x2 = x * x;
@@ -378,11 +395,14 @@ void render_pixel(const RenderJob& job, uint32_t lx, uint32_t ly, Counters& cnt)
 
     size_t texel = (size_t(ly) * job.band_w + lx) * 4;
     float* acc = job.accum + texel;
+    const bool hash = job.opt.rng_mode == RT_RNG_SAMPLE_HASH;
     double sum[3] = {0.0, 0.0, 0.0};
+    uint64_t q[3] = {0, 0, 0};
     if (job.opt.accumulate) { sum[0] = acc[0]; sum[1] = acc[1]; sum[2] = acc[2]; }
 
     for (uint32_t i = 0; i < rci.samplesPerRenderCall; i++) {
         if (job.opt.rng_mode == RT_RNG_SAMPLE_COUNTER) seed = tea(pixel_seed, job.opt.sample_base + i);
+        if (hash) seed = sample_seed_hash(pixel_seed, job.opt.sample_base + i);
         // shader.rgen:57 uv (x then y)
         float ux = rox + random_float(seed);
         float uy = roy + random_float(seed);
@@ -401,9 +421,19 @@ void render_pixel(const RenderJob& job, uint32_t lx, uint32_t ly, Counters& cnt)
         V3 dir = normalize(sub(to, from));
         cnt.samples++;
         V3 c = ray_color(job.sph, job.n, from, dir, seed, max_depth, cnt);
-        sum[0] += double(c.x);
-        sum[1] += double(c.y);
-        sum[2] += double(c.z);
+        if (hash) {
+            q[0] += sample_fixed(c.x);
+            q[1] += sample_fixed(c.y);
+            q[2] += sample_fixed(c.z);
+        } else {
+            sum[0] += double(c.x);
+            sum[1] += double(c.y);
+            sum[2] += double(c.z);
+        }
+    }
+    if (hash) {   // float accumulator in + fixed-point sum, rounded once to float
+        for (int k = 0; k < 3; k++)
+            sum[k] = double(job.opt.accumulate ? acc[k] : 0.0f) + double(q[k]) * 0x1p-44;
     }
     float s0 = float(sum[0]), s1 = float(sum[1]), s2 = float(sum[2]);
     acc[0] = s0; acc[1] = s1; acc[2] = s2; acc[3] = 1.0f;          // shader.rgen:63
@@ -459,6 +489,10 @@ uint32_t orc_lcg(uint32_t seed) { return random_int(seed); }
 float orc_random_float(uint32_t* seed) { return random_float(*seed); }
 
 float orc_sinf(float x) { return rt_sinf(x); }
+
+uint32_t orc_sample_seed_hash(uint32_t pixel_seed, uint32_t s) { return sample_seed_hash(pixel_seed, s); }
+
+uint64_t orc_sample_fixed(float c) { return sample_fixed(c); }
 
 void orc_viewport(const RenderCallInfo* rci, float* out18) {
     Viewport vp = make_viewport(*rci);

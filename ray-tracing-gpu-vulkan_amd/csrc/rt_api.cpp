@@ -1,13 +1,12 @@
-// rt_api.cpp — host runtime behind the C-ABI (include/rt_mi355x.h).
+// rt_api.cpp — host runtime behind the C-ABI (include/rt_mi355x.h), one device context at a time.
 //
 // Replaces the reference's host orchestration for the hot path (src/ray_trace.cpp:42-972,
 // src/vulkan.h): device contexts instead of Vulkan devices, one HBM-resident scene + LBVH per
 // context instead of UBO + BLAS/TLAS, one fused persistent kernel launch per band instead of
-// clear + vkCmdTraceRaysKHR, and a headless ray_trace() that renders once and returns.
+// clear + vkCmdTraceRaysKHR. The multi-device frame (RCCL) and ray_trace() are in rt_multi.cpp.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -16,25 +15,25 @@
 #include <memory>
 #include <random>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "../../include/rt_abi.h"
 #include "../../include/rt_mi355x.h"
 #include "rt_build.h"
 #include "rt_bvh.h"
+#include "rt_host.h"
 #include "rt_internal.h"
 
 namespace rt {
-hipError_t launch_trace(const TraceParams& P, uint32_t accel, bool count, int grid, size_t lds_bytes,
+hipError_t launch_trace(const TraceParams& P, uint32_t accel, bool count, int mode, int grid, size_t lds_bytes,
                         hipStream_t st);
-hipError_t trace_occupancy(uint32_t accel, bool count, size_t lds_bytes, int* blocks_per_cu);
-hipError_t launch_reduce_resolve(const float* slices, uint32_t n_slices, uint64_t n_texels, uint32_t spp,
-                                 float* accum_out, uint8_t* out, hipStream_t st);
+hipError_t trace_occupancy(uint32_t accel, bool count, int mode, size_t lds_bytes, int* blocks_per_cu);
+hipError_t launch_resolve_fixed(unsigned long long* fixed, uint64_t n_texels, uint32_t accumulate, uint32_t spp,
+                                float* accum, uint8_t* out, hipStream_t st);
+hipError_t launch_tonemap(const float* accum, uint64_t n_texels, uint32_t spp, uint8_t* out, hipStream_t st);
 uint32_t block_size(uint32_t accel);
-size_t pool_bytes(uint32_t accel);
 hipError_t launch_scatter_rows(const float* src_acc, const uint8_t* src_px, const uint32_t* rows,
-                               uint32_t n_rows, uint32_t width, float* dst_acc, uint8_t* dst_px,
+                               uint32_t n_rows, uint32_t width, uint32_t dst_rows, float* dst_acc, uint8_t* dst_px,
                                hipStream_t st);
 hipError_t launch_debug_math(int op, const float* in, float* out, uint32_t n, hipStream_t st);
 }  // namespace rt
@@ -43,30 +42,30 @@ struct rt_context {
     int device = 0;
     int cu_count = 0;
     rt::DeviceScene scene;
+    bool scene_set = false;                      // a set/refit call has succeeded (RT_ERR_NO_SCENE)
     std::vector<void*> scene_allocs;
-    rt::Counters* counters = nullptr;   // device
+    rt::Counters* counters = nullptr;            // device
+    // Every device operation of a context (scene upload / build, render) is ordered after the
+    // previous one, whatever streams they are issued on: an op on a stream other than the last
+    // one first waits for `ev_last`, and every op records it when issued.
     hipStream_t last_stream = nullptr;
-    // occupancy cache per kernel (accel id < kAccelIds) and count flag, valid for occ_lds bytes
-    static constexpr uint32_t kAccelIds = 16;
-    int occ[kAccelIds][2] = {};
-    size_t occ_lds[kAccelIds][2] = {};
-    size_t lds_bytes = 0;                        // LBVH_LDS staging size of the current scene
-    size_t lds2_bytes = 0;                       // LBVH2_LDS staging size (0: does not fit)
-    size_t lds16_bytes = 0;                      // compact-node LBVH staging size (0: not used)
-    size_t lds_scene_bytes = 0;                  // LBVH + geometry + materials staging (0: no fit)
+    hipEvent_t ev_last = nullptr;
+    bool ev_valid = false;
+    // occupancy cache per kernel form, count flag and rng mode, valid for occ_lds bytes
+    int occ[rt::ACCEL_COUNT][2][2] = {};
+    size_t occ_lds[rt::ACCEL_COUNT][2][2] = {};
+    size_t lds1_bytes = 0;                       // one node copy + leaves + scene records (0: no fit)
+    size_t oct_bytes = 0;                        // 8 octant node copies + leaves + scene records (0: no fit)
     // unpadded LBVH node boxes (host) and the radius the device copy is padded for
     std::vector<rt::BvhNode> nodes_host;
-    std::vector<rt::Bvh2Node> nodes2_host;
     float scene_radius = 0.0f;
     float pad_radius = 0.0f;
-    // device-side build (rt_build.hip): scratch kept for refits, and a staging copy of
-    // host-provided spheres
-    float padded_for = 0.0f;   // pad radius the device node copy currently carries
+    float padded_for = 0.0f;                     // pad radius the device node copy currently carries
     bool gpu_tree = false;
-    bool treelet_stale = true;        // ACCEL_LBVH_TOP: the treelet predates the current node boxes
-    rt::TileSchedule sched;           // pixel hand-out order (LPT from the last launch's costs)
-    rt::BuildWorkspace ws;
-    Sphere* d_spheres = nullptr;
+    bool treelet_stale = true;                   // ACCEL_LBVH_TOP: the treelet predates the node boxes
+    rt::TileSchedule sched;                      // unit hand-out order (LPT from the last launch's costs)
+    rt::BuildWorkspace ws;                       // device build scratch, kept for refits
+    Sphere* d_spheres = nullptr;                 // staging copy of host-provided spheres (device build)
     uint32_t d_spheres_cap = 0;
     // Host-built scenes: every device array lives in one device blob, rewritten in stream order
     // by one copy from a pinned staging buffer (two, alternating, each guarded by the event of
@@ -79,6 +78,11 @@ struct rt_context {
     hipEvent_t stage_ev[2] = {nullptr, nullptr};
     bool stage_used[2] = {false, false};
     int stage_cur = 0;
+    // RT_RNG_SAMPLE_HASH: 3 planes of fixed-point sums, zero between launches (the resolve
+    // kernel clears what it reads)
+    unsigned long long* fixed = nullptr;
+    uint64_t fixed_cap = 0;                      // texels
+    uint32_t last_chunks = 1;
 };
 
 namespace {
@@ -87,53 +91,11 @@ namespace {
 // for |o|, |bound| <= R; 1.5x margin.
 float pad_for(float R) { return 18.0f * 5.9604645e-8f * R; }
 
-// float -> binary16 rounded toward -inf (down) or +inf (up), so a box only ever grows.
-uint16_t half_bits(float x, bool up) {
-    const _Float16 h0 = (_Float16)x;   // round to nearest
-    uint16_t b = __builtin_bit_cast(uint16_t, h0);
-    const float back = (float)h0;
-    if ((up && back < x) || (!up && back > x)) {
-        // one binary16 step outward
-        if (up) b = (b == 0x8000u) ? 0x0001u : ((b & 0x8000u) ? uint16_t(b - 1) : uint16_t(b + 1));
-        else b = (b == 0x0000u) ? 0x8001u : ((b & 0x8000u) ? uint16_t(b + 1) : uint16_t(b - 1));
-    }
-    return b;
-}
-
-// Compact nodes from (padded) escape-link nodes; false when the tree does not fit the format.
-bool make_nodes16(const std::vector<rt::BvhNode>& in, std::vector<rt::BvhNode16>& out) {
-    out.clear();
-    if (in.empty() || in.size() >= 0xffffu) return false;
-    out.reserve(in.size());
-    for (const rt::BvhNode& n : in) {
-        uint32_t leaf = 0;
-        if (n.first_count) {
-            const uint32_t first = n.first_count >> 4, cnt = n.first_count & 15u;
-            if ((first & 3u) || (first >> 2) >= 8192u || cnt < 1u || cnt > 4u) return false;
-            leaf = 0x8000u | ((first >> 2) << 2) | (cnt - 1u);
-        }
-        const uint32_t esc = (n.escape == 0xffffffffu) ? 0xffffu : n.escape;
-        rt::BvhNode16 m;
-        m.x = half_bits(n.lox, false) | (uint32_t(half_bits(n.loy, false)) << 16);
-        m.y = half_bits(n.loz, false) | (uint32_t(half_bits(n.hix, true)) << 16);
-        m.z = half_bits(n.hiy, true) | (uint32_t(half_bits(n.hiz, true)) << 16);
-        m.w = esc | (leaf << 16);
-        out.push_back(m);
-    }
-    return true;
-}
-
-void pad_nodes(const std::vector<rt::BvhNode>& in, std::vector<rt::BvhNode>& out,
-               const std::vector<rt::Bvh2Node>& in2, std::vector<rt::Bvh2Node>& out2, float pad) {
+void pad_nodes(const std::vector<rt::BvhNode>& in, std::vector<rt::BvhNode>& out, float pad) {
     out = in;
     for (auto& n : out) {
         n.lox -= pad; n.loy -= pad; n.loz -= pad;
         n.hix += pad; n.hiy += pad; n.hiz += pad;
-    }
-    out2 = in2;
-    for (auto& n : out2) {
-        n.l0x -= pad; n.l0y -= pad; n.l0z -= pad; n.h0x += pad; n.h0y += pad; n.h0z += pad;
-        n.l1x -= pad; n.l1y -= pad; n.l1z -= pad; n.h1x += pad; n.h1y += pad; n.h1z += pad;
     }
 }
 
@@ -177,51 +139,41 @@ void make_octant_orders(const std::vector<rt::BvhNode>& n, std::vector<rt::BvhNo
         }
     }
 }
-}  // namespace
 
-// LBVH staged in LDS when its image is at most this large.
-static constexpr size_t kMaxLdsBvhBytes = 24 * 1024;
-// LBVH + per-sphere geometry/material records staged together up to this size (512-thread
-// blocks: 3 blocks = 24 waves per CU fit in the 160 KiB LDS).
-static constexpr size_t kMaxLdsSceneBytes = 52 * 1024;
-// LDS-scene staging + the tail-compaction pool of a 1024-thread block (one block per CU).
-static constexpr size_t kMaxLdsPoolBytes = 156 * 1024;
-// Ordered-walk LBVH staged in LDS up to this size (plus the per-lane stacks).
-static constexpr size_t kMaxLdsBvh2Bytes = 40 * 1024;
+// LDS budget of the staged forms: 160 KiB per CU, one 1024-thread block per CU; 4 KiB kept free.
+constexpr size_t kMaxLdsBytes = 156 * 1024;
+// The LDS walk's leaf words hold a leaf index in 10 bits (<= 4096 slots of 4) and an escape node
+// of the 8 copies in 19 bits.
+constexpr uint32_t kMaxLdsLeafSlots = 4096;
+constexpr uint32_t kMaxLdsNodes = 0x7fffeu / 8u;
 
-namespace {
-
-thread_local std::string g_last_error;
-
-int fail(int code, const std::string& msg) {
-    g_last_error = msg;
-    return code;
+void size_lds_forms(rt_context* ctx, uint32_t count) {
+    const rt::DeviceScene& d = ctx->scene;
+    const size_t tree = size_t(2 * d.n_nodes + d.n_leaf + (d.n_leaf + 3) / 4) * 16;
+    const size_t lds1 = tree + size_t(count) * 48u;
+    const bool ok = d.n_nodes && d.n_leaf <= kMaxLdsLeafSlots && d.n_nodes <= kMaxLdsNodes;
+    ctx->lds1_bytes = (ok && lds1 <= kMaxLdsBytes) ? lds1 : 0;
+    const size_t oct = lds1 + size_t(14u) * d.n_nodes * 16u;
+    ctx->oct_bytes = (ok && oct <= kMaxLdsBytes) ? oct : 0;
 }
-
-#define RT_HIP(call)                                                                        \
-    do {                                                                                    \
-        hipError_t e_ = (call);                                                             \
-        if (e_ != hipSuccess)                                                               \
-            return fail(e_ == hipErrorOutOfMemory ? RT_ERR_OUT_OF_MEMORY : RT_ERR_DEVICE,   \
-                        std::string(#call) + ": " + hipGetErrorString(e_));                  \
-    } while (0)
-
-// RAII device selection: restores the caller's current device.
-struct DeviceGuard {
-    int prev = -1;
-    explicit DeviceGuard(int dev) {
-        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
-        (void)hipSetDevice(dev);
-    }
-    ~DeviceGuard() {
-        if (prev >= 0) (void)hipSetDevice(prev);
-    }
-};
 
 void free_scene(rt_context* ctx) {
     for (void* p : ctx->scene_allocs) (void)hipFree(p);
     ctx->scene_allocs.clear();
     ctx->scene = rt::DeviceScene{};
+}
+
+// Stream chaining of a context's device operations (rt_context::ev_last).
+int order_on(rt_context* ctx, hipStream_t st) {
+    if (ctx->ev_valid && ctx->last_stream != st) RT_HIP(hipStreamWaitEvent(st, ctx->ev_last, 0));
+    return RT_OK;
+}
+int mark_issued(rt_context* ctx, hipStream_t st) {
+    if (!ctx->ev_last) RT_HIP(hipEventCreateWithFlags(&ctx->ev_last, hipEventDisableTiming));
+    RT_HIP(hipEventRecord(ctx->ev_last, st));
+    ctx->ev_valid = true;
+    ctx->last_stream = st;
+    return RT_OK;
 }
 
 // One device blob for a host-built scene (rt_context::blob): add() the arrays, then commit()
@@ -345,6 +297,16 @@ Sphere make_sphere(rt_vec4 g, uint32_t mat, uint32_t tex, rt_vec4 c0, rt_vec4 c1
     return s;
 }
 
+}  // namespace
+
+namespace rt {
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
 int current_device_count(int* n) {
     hipError_t e = hipGetDeviceCount(n);
     if (e != hipSuccess || *n <= 0) {
@@ -353,18 +315,20 @@ int current_device_count(int* n) {
     }
     return RT_OK;
 }
+}  // namespace rt
 
-}  // namespace
+using rt::fail;
+using rt::DeviceGuard;
 
 extern "C" {
 
 uint32_t rt_abi_version(void) { return RT_ABI_VERSION; }
 
-const char* rt_last_error(void) { return g_last_error.c_str(); }
+const char* rt_last_error(void) { return rt::g_last_error.c_str(); }
 
 int rt_device_count(int* count) {
     if (!count) return fail(RT_ERR_INVALID_ARGUMENT, "count is NULL");
-    return current_device_count(count);
+    return rt::current_device_count(count);
 }
 
 int rt_generate_scene(float t, uint32_t K, Sphere* out, uint32_t capacity, uint32_t* count) {
@@ -426,7 +390,7 @@ int rt_context_create(int device, rt_context** out) {
     if (!out) return fail(RT_ERR_INVALID_ARGUMENT, "out is NULL");
     *out = nullptr;
     int n = 0;
-    if (int rc = current_device_count(&n)) return rc;
+    if (int rc = rt::current_device_count(&n)) return rc;
     if (device < 0 || device >= n) return fail(RT_ERR_INVALID_ARGUMENT, "device index out of range");
     DeviceGuard g(device);
     std::unique_ptr<rt_context> ctx(new rt_context());
@@ -436,8 +400,9 @@ int rt_context_create(int device, rt_context** out) {
     RT_HIP(hipMalloc(&c, sizeof(rt::Counters)));
     RT_HIP(hipMemset(c, 0, sizeof(rt::Counters)));
     ctx->counters = static_cast<rt::Counters*>(c);
-    for (uint32_t a = 0; a < rt_context::kAccelIds; a++)
-        for (int cnt = 0; cnt < 2; cnt++) ctx->occ_lds[a][cnt] = ~size_t(0);
+    for (auto& a : ctx->occ_lds)
+        for (auto& b : a)
+            for (auto& v : b) v = ~size_t(0);
     *out = ctx.release();
     return RT_OK;
 }
@@ -454,7 +419,9 @@ int rt_context_destroy(rt_context* ctx) {
         if (ctx->stage[k]) (void)hipHostFree(ctx->stage[k]);
         if (ctx->stage_ev[k]) (void)hipEventDestroy(ctx->stage_ev[k]);
     }
+    if (ctx->ev_last) (void)hipEventDestroy(ctx->ev_last);
     if (ctx->d_spheres) (void)hipFree(ctx->d_spheres);
+    if (ctx->fixed) (void)hipFree(ctx->fixed);
     if (ctx->counters) (void)hipFree(ctx->counters);
     delete ctx;
     return RT_OK;
@@ -464,8 +431,8 @@ int rt_context_destroy(rt_context* ctx) {
 
 namespace {
 
-// Host-built tree (rt_bvh.cpp): the A/B reference for the device builder and the only source of
-// the alternative walk layouts (ordered two-wide, compact binary16 nodes).
+// Host-built tree (rt_bvh.cpp, binned SAH or Morton split): the default for scenes whose tree and
+// records fit LDS, and the A/B reference of the device builder.
 int set_scene_host(rt_context* ctx, const Sphere* spheres, uint32_t count, hipStream_t st, bool sah) {
     try {
         if (ctx->gpu_tree || !ctx->scene_allocs.empty()) {   // leaving a device-built scene
@@ -517,28 +484,11 @@ int set_scene_host(rt_context* ctx, const Sphere* spheres, uint32_t count, hipSt
         ctx->pad_radius = R * 1.01f + 100.0f;
         ctx->padded_for = ctx->pad_radius;
         ctx->nodes_host = bvh.nodes;
-        ctx->nodes2_host = bvh.nodes2;
-        pad_nodes(ctx->nodes_host, bvh.nodes, ctx->nodes2_host, bvh.nodes2, pad_for(ctx->pad_radius));
+        pad_nodes(ctx->nodes_host, bvh.nodes, pad_for(ctx->pad_radius));
         std::vector<rt::BvhNode> oct;
         make_octant_orders(bvh.nodes, oct);
         up.add(oct, &d.nodes_oct);
-        const size_t lds = size_t(2 * d.n_nodes + d.n_leaf + (d.n_leaf + 3) / 4) * 16;
-        ctx->lds_bytes = (d.n_nodes && lds <= kMaxLdsBvhBytes) ? lds : 0;
-        const size_t lds_scene = lds + size_t(count) * 48u;
-        ctx->lds_scene_bytes = (d.n_nodes && lds_scene <= kMaxLdsSceneBytes) ? lds_scene : 0;
-        std::vector<rt::BvhNode16> n16;
-        const size_t lds16 = size_t(d.n_nodes + d.n_leaf + (d.n_leaf + 3) / 4) * 16;
-        ctx->lds16_bytes = 0;
-        if (make_nodes16(bvh.nodes, n16) && lds16 <= kMaxLdsBvhBytes) {
-            up.add(n16, &d.nodes16);
-            ctx->lds16_bytes = lds16;
-        }
-        d.n_nodes2 = uint32_t(bvh.nodes2.size());
-        d.root2 = bvh.root2;
-        d.depth2 = bvh.depth2;
-        up.add(bvh.nodes2, &d.nodes2);
-        const size_t lds2 = size_t(4 * d.n_nodes2 + d.n_leaf + (d.n_leaf + 3) / 4) * 16;
-        ctx->lds2_bytes = (d.n_leaf && lds2 <= kMaxLdsBvh2Bytes) ? lds2 : 0;
+        size_lds_forms(ctx, count);
         up.add(bvh.nodes, &d.nodes);
         up.add(bvh.leaf_geom, &d.leaf_geom);
         up.add(bvh.leaf_ids, &d.leaf_ids);
@@ -589,26 +539,18 @@ int set_scene_gpu(rt_context* ctx, const Sphere* d_sph, uint32_t count, hipStrea
     d.n_nodes = sm.n_nodes;
     d.n_leaf = sm.n_leaf_slots;
     d.small_rmax = rt::summary_float(sm.rmax_o);
-    d.nodes16 = nullptr;
-    d.nodes2 = nullptr;
-    d.n_nodes2 = d.root2 = d.depth2 = 0;
     ctx->scene_radius = rt::summary_float(sm.R_o);
     ctx->pad_radius = ctx->scene_radius * 1.01f + 100.0f;   // the build padded for this radius
     ctx->padded_for = ctx->pad_radius;
     ctx->nodes_host.clear();
-    ctx->nodes2_host.clear();
-    const size_t lds = size_t(2 * d.n_nodes + d.n_leaf + (d.n_leaf + 3) / 4) * 16;
-    ctx->lds_bytes = (d.n_nodes && lds <= kMaxLdsBvhBytes) ? lds : 0;
-    const size_t lds_scene = lds + size_t(count) * 48u;
-    ctx->lds_scene_bytes = (d.n_nodes && lds_scene <= kMaxLdsSceneBytes) ? lds_scene : 0;
-    ctx->lds16_bytes = 0;
-    ctx->lds2_bytes = 0;
+    size_lds_forms(ctx, count);
     return RT_OK;
 }
 
-// Tree builder (RT_BVH_BUILD): "auto" (default) = host SAH up to kHostSahMaxSpheres (best walk
-// cost, build <= ~2 ms) else the device LBVH; "gpu", "sah", "morton" force one (A/B, tests).
-constexpr uint32_t kHostSahMaxSpheres = 4096;
+// Tree builder (RT_BVH_BUILD): "auto" (default) = host binned SAH for scenes whose tree and
+// records fit LDS (best walk cost, build <= ~1 ms), else the device LBVH (LDS treelet over L2);
+// "gpu", "sah", "morton" force one (A/B, tests).
+constexpr uint32_t kHostSahMaxSpheres = 1024;
 enum class Builder { GPU, HOST_SAH, HOST_MORTON };
 Builder pick_builder(uint32_t count) {
     const char* b = std::getenv("RT_BVH_BUILD");
@@ -620,7 +562,10 @@ Builder pick_builder(uint32_t count) {
 
 int stage_spheres(rt_context* ctx, const Sphere* spheres, uint32_t count, hipStream_t st) {
     if (count > ctx->d_spheres_cap) {
-        if (ctx->d_spheres) (void)hipFree(ctx->d_spheres);
+        if (ctx->d_spheres) {
+            RT_HIP(hipDeviceSynchronize());
+            (void)hipFree(ctx->d_spheres);
+        }
         ctx->d_spheres = nullptr;
         ctx->d_spheres_cap = 0;
         void* p = nullptr;
@@ -639,124 +584,124 @@ int check_scene_args(rt_context* ctx, const Sphere* spheres, uint32_t count) {
     return RT_OK;
 }
 
+// Scene calls: ordered after the context's previous operation, and before its next one.
+template <typename F>
+int scene_op(rt_context* ctx, hipStream_t st, F&& body) {
+    DeviceGuard g(ctx->device);
+    if (int rc = order_on(ctx, st)) return rc;
+    const int rc = body();
+    if (rc != RT_OK) {
+        ctx->scene_set = false;
+        return rc;
+    }
+    ctx->scene_set = true;
+    return mark_issued(ctx, st);
+}
+
 }  // namespace
 
 extern "C" {
 
 int rt_set_scene(rt_context* ctx, const Sphere* spheres, uint32_t count, void* stream) {
     if (int rc = check_scene_args(ctx, spheres, count)) return rc;
-    DeviceGuard g(ctx->device);
     hipStream_t st = static_cast<hipStream_t>(stream);
-    // Launches on another stream may still read the old scene: wait for them. Launches on `st`
-    // are ordered before the new scene's upload (the host build overlaps them).
-    if (ctx->last_stream != st) RT_HIP(hipStreamSynchronize(ctx->last_stream));
-    const Builder b = pick_builder(count);
-    if (b != Builder::GPU) return set_scene_host(ctx, spheres, count, st, b == Builder::HOST_SAH);
-    RT_HIP(hipStreamSynchronize(st));  // the device builder frees and rebuilds in place
-    if (int rc = stage_spheres(ctx, spheres, count, st)) return rc;
-    return set_scene_gpu(ctx, ctx->d_spheres, count, st, false);
+    return scene_op(ctx, st, [&]() -> int {
+        const Builder b = pick_builder(count);
+        if (b != Builder::GPU) return set_scene_host(ctx, spheres, count, st, b == Builder::HOST_SAH);
+        RT_HIP(hipStreamSynchronize(st));  // the device builder frees and rebuilds in place
+        if (int rc = stage_spheres(ctx, spheres, count, st)) return rc;
+        return set_scene_gpu(ctx, ctx->d_spheres, count, st, false);
+    });
 }
 
 int rt_set_scene_device(rt_context* ctx, const Sphere* d_spheres, uint32_t count, void* stream) {
     if (int rc = check_scene_args(ctx, d_spheres, count)) return rc;
-    DeviceGuard g(ctx->device);
     hipStream_t st = static_cast<hipStream_t>(stream);
-    RT_HIP(hipStreamSynchronize(st));
-    return set_scene_gpu(ctx, d_spheres, count, st, false);
+    return scene_op(ctx, st, [&]() -> int {
+        RT_HIP(hipStreamSynchronize(st));
+        return set_scene_gpu(ctx, d_spheres, count, st, false);
+    });
 }
 
 int rt_refit_scene(rt_context* ctx, const Sphere* spheres, uint32_t count, void* stream) {
     if (int rc = check_scene_args(ctx, spheres, count)) return rc;
     if (!ctx->gpu_tree || count != ctx->scene.n_spheres || ctx->ws.topo_n != count)
         return rt_set_scene(ctx, spheres, count, stream);   // no topology to reuse: full build
-    DeviceGuard g(ctx->device);
     hipStream_t st = static_cast<hipStream_t>(stream);
-    RT_HIP(hipStreamSynchronize(st));
-    if (int rc = stage_spheres(ctx, spheres, count, st)) return rc;
-    return set_scene_gpu(ctx, ctx->d_spheres, count, st, true);
+    return scene_op(ctx, st, [&]() -> int {
+        RT_HIP(hipStreamSynchronize(st));
+        if (int rc = stage_spheres(ctx, spheres, count, st)) return rc;
+        return set_scene_gpu(ctx, ctx->d_spheres, count, st, true);
+    });
 }
 
 int rt_refit_scene_device(rt_context* ctx, const Sphere* d_spheres, uint32_t count, void* stream) {
     if (int rc = check_scene_args(ctx, d_spheres, count)) return rc;
     if (!ctx->gpu_tree || count != ctx->scene.n_spheres || ctx->ws.topo_n != count)
         return rt_set_scene_device(ctx, d_spheres, count, stream);
-    DeviceGuard g(ctx->device);
     hipStream_t st = static_cast<hipStream_t>(stream);
-    RT_HIP(hipStreamSynchronize(st));
-    return set_scene_gpu(ctx, d_spheres, count, st, true);
+    return scene_op(ctx, st, [&]() -> int {
+        RT_HIP(hipStreamSynchronize(st));
+        return set_scene_gpu(ctx, d_spheres, count, st, true);
+    });
 }
 
 int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t* rows,
                      uint32_t band_width, uint32_t band_height, float* accum, uint8_t* out,
                      const rt_options* opt, void* stream) {
     if (!ctx || !rci) return fail(RT_ERR_INVALID_ARGUMENT, "ctx or rci is NULL");
-    if (!ctx->scene.geom && ctx->scene.n_spheres) return fail(RT_ERR_NO_SCENE, "no scene set");
+    if (!ctx->scene_set) return fail(RT_ERR_NO_SCENE, "rt_render_device before rt_set_scene");
     if (band_width == 0 || band_height == 0) return RT_OK;
     if (!accum || !out) return fail(RT_ERR_INVALID_ARGUMENT, "accum or out is NULL");
     if (rci->image_size.x == 0 || rci->image_size.y == 0)
         return fail(RT_ERR_INVALID_ARGUMENT, "image_size is zero");
-    const uint64_t tiles_x = (band_width + 7u) / 8u, tiles_y = (band_height + 7u) / 8u;
-    if (tiles_x * tiles_y * 64u >= (1ull << 32)) return fail(RT_ERR_INVALID_ARGUMENT, "band too large");
     // the kernel keeps a pixel's band coordinates as 16-bit halves of one word (Path::px)
     if (band_width > 65535u || band_height > 65535u)
         return fail(RT_ERR_INVALID_ARGUMENT, "band width and height must be below 65536");
     rt_options o;
     std::memset(&o, 0, sizeof(o));
     if (opt) o = *opt;
-    // reserved[1] (internal, A/B only): LBVH walk form, 0 = default (stackless escape-link walk
-    // over 32-B nodes), 2 = ordered two-wide walk with an LDS stack, 4 = escape-link walk over
-    // compact 16-B binary16 nodes (both slower on the canonical scene), 5 = scene
-    // records from global memory, 6 = LDS scene with one node copy, 7 = that + the tail-compaction
-    // pool (at 4 waves per SIMD the tail is already short: the pool measured 1 ms slower), 8 =
-    // octant-specialised node copies (the default whenever they fit in LDS)
-    const bool escape_walk = o.reserved[1] != 2u;
-    if (!escape_walk && ctx->gpu_tree && ctx->scene.n_nodes)
-        return fail(RT_ERR_INVALID_ARGUMENT, "the ordered walk needs a host-built tree (RT_BVH_BUILD=sah or morton)");
-    const bool allow16 = o.reserved[1] == 4u;
-    uint32_t accel;
-    size_t lds = 0;
-    const rt::DeviceScene& ds = ctx->scene;
-    if (o.accel == RT_ACCEL_BRUTE) {
-        accel = rt::ACCEL_BRUTE;
-    } else if (escape_walk && allow16 && ctx->lds16_bytes) {
-        accel = rt::ACCEL_LBVH16_LDS;
-        lds = ctx->lds16_bytes;
-    } else if (escape_walk && ctx->lds_scene_bytes && (o.reserved[1] == 0u || o.reserved[1] == 8u) &&
-               ctx->lds_scene_bytes + size_t(14u) * ds.n_nodes * 16u <= kMaxLdsPoolBytes) {
-        accel = rt::ACCEL_LBVH_OCT;   // default when it fits: octant-specialised node copies in LDS
-        lds = ctx->lds_scene_bytes + size_t(14u) * ds.n_nodes * 16u;
-    } else if (escape_walk && ctx->lds_scene_bytes && o.reserved[1] == 7u &&
-               ctx->lds_scene_bytes + rt::pool_bytes(rt::ACCEL_LBVH_POOL) <= kMaxLdsPoolBytes) {
-        accel = rt::ACCEL_LBVH_POOL;   // A/B: tail compaction through the block's LDS pool
-        lds = ctx->lds_scene_bytes + rt::pool_bytes(rt::ACCEL_LBVH_POOL);
-    } else if (escape_walk && ctx->lds_scene_bytes && o.reserved[1] != 5u) {
-        accel = rt::ACCEL_LBVH_LDS_SCENE;
-        lds = ctx->lds_scene_bytes;
-    } else if (escape_walk && !ctx->lds_bytes && ds.treelet && ds.n_nodes && ds.n_leaf < (1u << 26) &&
-               o.reserved[1] != 10u) {   // (treelet leaf words carry first_count in 30 bits)
-        // tree too big for LDS (device-built): its top levels in LDS, the rest from L2
-        // (walk form 10 = everything from L2, A/B)
-        accel = rt::ACCEL_LBVH_TOP;
-        lds = size_t(rt::kTreeletCap) * 32u;
-    } else if (escape_walk) {
-        accel = ctx->lds_bytes ? rt::ACCEL_LBVH_LDS : rt::ACCEL_LBVH;
-        lds = ctx->lds_bytes;
-    } else {
-        const uint32_t blk = rt::block_size(rt::ACCEL_LBVH2);
-        const size_t stack = size_t(blk) * std::max(1u, ds.depth2) * 4u;
-        accel = ctx->lds2_bytes ? rt::ACCEL_LBVH2_LDS : rt::ACCEL_LBVH2;
-        lds = (ctx->lds2_bytes ? ctx->lds2_bytes : 0) + stack;
-        if (lds > 160u * 1024u) return fail(RT_ERR_INVALID_ARGUMENT, "LBVH too deep for the LDS stack");
-    }
     if (o.accel > RT_ACCEL_LBVH) return fail(RT_ERR_INVALID_ARGUMENT, "unknown accel");
     if (o.seed_mode > RT_SEED_LAUNCH_LOCAL) return fail(RT_ERR_INVALID_ARGUMENT, "unknown seed_mode");
-    if (o.rng_mode > RT_RNG_SAMPLE_COUNTER) return fail(RT_ERR_INVALID_ARGUMENT, "unknown rng_mode");
+    if (o.rng_mode > RT_RNG_SAMPLE_HASH) return fail(RT_ERR_INVALID_ARGUMENT, "unknown rng_mode");
+    const int mode = o.rng_mode == RT_RNG_SAMPLE_HASH ? rt::MODE_HASH : rt::MODE_STREAM;
+    const uint32_t spp = rci->samplesPerRenderCall;
+    if (mode == rt::MODE_HASH && spp > rt::kHashMaxSpp)
+        return fail(RT_ERR_INVALID_ARGUMENT, "RT_RNG_SAMPLE_HASH: samplesPerRenderCall above 2^19");
+    const uint64_t tiles_x = (band_width + 7u) / 8u, tiles_y = (band_height + 7u) / 8u;
+    const uint64_t n_tiles = tiles_x * tiles_y;
+    // reserved[1] (internal, A/B only): LBVH walk form, 0 = automatic (octant node copies in LDS
+    // when they fit, else one copy in LDS, else an LDS treelet over L2), 6 = one LDS node copy,
+    // 8 = octant copies, 10 = every node from L2.
+    const uint32_t form = o.reserved[1];
+    const rt::DeviceScene& d = ctx->scene;
+    uint32_t accel;
+    size_t lds = 0;
+    if (o.accel == RT_ACCEL_BRUTE) {
+        accel = rt::ACCEL_BRUTE;
+    } else if (ctx->oct_bytes && (form == 0u || form == 8u)) {
+        accel = rt::ACCEL_LBVH_OCT;
+        lds = ctx->oct_bytes;
+    } else if (ctx->lds1_bytes && (form == 0u || form == 6u || form == 8u)) {
+        accel = rt::ACCEL_LBVH_LDS;
+        lds = ctx->lds1_bytes;
+    } else if (ctx->gpu_tree && d.treelet && d.n_nodes && d.n_leaf < (1u << 26) && form != 10u) {
+        // (treelet leaf words carry first_count in 30 bits)
+        accel = rt::ACCEL_LBVH_TOP;
+        lds = size_t(rt::kTreeletCap) * 32u;
+    } else {
+        accel = rt::ACCEL_LBVH_GLOBAL;
+    }
     const bool count = (o.reserved[0] & 1u) != 0;  // internal: count box / sphere tests
+    DeviceGuard g(ctx->device);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (int rc = order_on(ctx, st)) return rc;
+
     rt::TraceParams P;
     std::memset(&P, 0, sizeof(P));
     fill_camera(*rci, P);
     P.number = rci->number;
-    P.spp = rci->samplesPerRenderCall;
+    P.spp = spp;
     P.max_depth = o.max_depth ? o.max_depth : 50u;
     P.seed_local = o.seed_mode == RT_SEED_LAUNCH_LOCAL;
     P.rng_counter = o.rng_mode == RT_RNG_SAMPLE_COUNTER;
@@ -767,9 +712,7 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     P.band_w = band_width;
     P.band_h = band_height;
     P.tiles_x = uint32_t(tiles_x);
-    P.n_units = uint32_t(tiles_x * tiles_y * 64u);
     P.rows = rows;
-    const rt::DeviceScene& d = ctx->scene;
     P.n_spheres = d.n_spheres;
     P.geom = d.geom;
     P.radius = d.radius;
@@ -778,37 +721,24 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     P.big_ids = d.big_ids;
     P.nodes = d.n_nodes ? d.nodes : nullptr;
     P.n_nodes = d.n_nodes;
-    P.nodes16 = d.nodes16;
     P.nodes_oct = d.nodes_oct;
     P.treelet = d.treelet;
     P.treelet_count = d.treelet_count;
-    P.nodes2 = d.nodes2;   // null when the tree is a single leaf (root2 is then a leaf reference)
-    P.n_nodes2 = d.n_nodes2;
-    P.root2 = d.root2;
-    P.stack_depth = d.depth2;
     P.n_leaf = d.n_leaf;
     P.leaf_geom = d.leaf_geom;
     P.leaf_ids = d.leaf_ids;
     // Node-cull slack: a candidate's AABB entry lies at most
     // 2.75 r + 1.15e-3 t beyond its reported t.
-#ifdef RT_CULL_ABS_AB   // A/B experiments only (scripts/perf_variants.py --inexact)
-    P.cull_abs = RT_CULL_ABS_AB;
-    P.cull_rel = RT_CULL_REL_AB;
-#else
     P.cull_abs = 3.0f * d.small_rmax + 1e-3f;
     P.cull_rel = 2e-3f;
-#endif
-
     P.accum = accum;
     P.out = reinterpret_cast<uint32_t*>(out);
     P.counters = ctx->counters;
 
-    DeviceGuard g(ctx->device);
-    hipStream_t st = static_cast<hipStream_t>(stream);
     {   // a camera outside the padded radius: re-pad the node boxes for it (rare, synchronous)
         const float cx = rci->camera_pos.x, cy = rci->camera_pos.y, cz = rci->camera_pos.z;
         const float cam_r = std::sqrt(cx * cx + cy * cy + cz * cz);
-        if (!(cam_r <= ctx->pad_radius) && (d.n_nodes || d.n_nodes2)) {
+        if (!(cam_r <= ctx->pad_radius) && d.n_nodes) {
             if (!std::isfinite(cam_r)) return fail(RT_ERR_INVALID_ARGUMENT, "camera position is not finite");
             ctx->pad_radius = std::max(ctx->scene_radius, cam_r) * 1.01f + 100.0f;
         }
@@ -818,8 +748,7 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
             ctx->padded_for = ctx->pad_radius;
         } else if (!ctx->gpu_tree && ctx->pad_radius != ctx->padded_for) {
             std::vector<rt::BvhNode> n1;
-            std::vector<rt::Bvh2Node> n2;
-            pad_nodes(ctx->nodes_host, n1, ctx->nodes2_host, n2, pad_for(ctx->pad_radius));
+            pad_nodes(ctx->nodes_host, n1, pad_for(ctx->pad_radius));
             RT_HIP(hipStreamSynchronize(st));
             if (!n1.empty()) RT_HIP(hipMemcpy(d.nodes, n1.data(), n1.size() * sizeof(n1[0]), hipMemcpyHostToDevice));
             if (d.nodes_oct) {
@@ -827,23 +756,59 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
                 make_octant_orders(n1, oct);
                 RT_HIP(hipMemcpy(d.nodes_oct, oct.data(), oct.size() * sizeof(oct[0]), hipMemcpyHostToDevice));
             }
-            if (!n2.empty()) RT_HIP(hipMemcpy(d.nodes2, n2.data(), n2.size() * sizeof(n2[0]), hipMemcpyHostToDevice));
-            std::vector<rt::BvhNode16> n16;
-            if (d.nodes16) {
-                if (!make_nodes16(n1, n16)) return fail(RT_ERR_DEVICE, "compact LBVH re-pad failed");
-                RT_HIP(hipMemcpy(d.nodes16, n16.data(), n16.size() * sizeof(n16[0]), hipMemcpyHostToDevice));
-            }
             ctx->padded_for = ctx->pad_radius;
         }
     }
+    // Grid: one persistent block per CU slot the occupancy allows.
+    const int ci = count ? 1 : 0;
+    if (ctx->occ_lds[accel][ci][mode] != lds) {
+        int b = 0;
+        RT_HIP(rt::trace_occupancy(accel, count, mode, lds, &b));
+        ctx->occ[accel][ci][mode] = std::max(1, b);
+        ctx->occ_lds[accel][ci][mode] = lds;
+    }
+    const uint64_t blk = rt::block_size(accel);
+    const uint64_t lanes = uint64_t(ctx->cu_count) * ctx->occ[accel][ci][mode] * blk;
+    // Sample chunks per pixel (HASH only: the image does not depend on them):
+    // enough units for ~16 per lane, so the frame is throughput-bound rather than bound by the
+    // longest unit (RT_SAMPLE_CHUNKS forces a count, RT_UNITS_PER_LANE the target; tests, A/B).
+    uint64_t chunks = 1;
+    if (mode == rt::MODE_HASH && spp > 1) {
+        uint64_t per_lane = 16;
+        if (const char* e = std::getenv("RT_UNITS_PER_LANE")) per_lane = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
+        const uint64_t pixels = uint64_t(band_width) * band_height;
+        chunks = (lanes * per_lane + pixels - 1) / pixels;
+        if (const char* e = std::getenv("RT_SAMPLE_CHUNKS")) chunks = std::strtoull(e, nullptr, 10);
+        chunks = std::max<uint64_t>(1, std::min<uint64_t>({chunks, spp, 4096}));
+        while (chunks > 1 && n_tiles * chunks * 64u >= (1ull << 31)) chunks /= 2;   // unit ids in 32 bits
+    }
+    if (n_tiles * chunks * 64u >= (1ull << 32)) return fail(RT_ERR_INVALID_ARGUMENT, "band too large");
+    P.chunks = uint32_t(chunks);
+    ctx->last_chunks = P.chunks;
+    P.n_units = uint32_t(n_tiles * chunks * 64u);
+    const uint64_t texels = uint64_t(band_width) * band_height;
+    if (mode == rt::MODE_HASH) {
+        if (ctx->fixed_cap < texels) {
+            if (ctx->fixed) {
+                RT_HIP(hipStreamSynchronize(st));   // ordered after every earlier op of ctx
+                RT_HIP(hipFree(ctx->fixed));
+            }
+            ctx->fixed = nullptr;
+            ctx->fixed_cap = 0;
+            void* p = nullptr;
+            RT_HIP(hipMalloc(&p, texels * 3 * sizeof(unsigned long long)));
+            RT_HIP(hipMemsetAsync(p, 0, texels * 3 * sizeof(unsigned long long), st));
+            ctx->fixed = static_cast<unsigned long long*>(p);
+            ctx->fixed_cap = texels;
+        }
+        P.fixed = ctx->fixed;
+    }
     // Longest-processing-time-first hand-out from the last launch of this band geometry: tiles
-    // in descending order of their longest pixel chain (RT_SCHEDULE=rowmajor | sum: A/B only);
+    // in descending order of their longest unit chain (RT_SCHEDULE=rowmajor | sum: A/B only);
     // this launch records the next costs.
-    if (accel == rt::ACCEL_LBVH || accel == rt::ACCEL_LBVH_LDS || accel == rt::ACCEL_LBVH16_LDS ||
-        accel == rt::ACCEL_LBVH_LDS_SCENE || accel == rt::ACCEL_LBVH_POOL || accel == rt::ACCEL_LBVH_OCT ||
-        accel == rt::ACCEL_LBVH_TOP) {   // escape-walk kernels record tile costs
+    if (accel != rt::ACCEL_BRUTE) {
         rt::TileSchedule& sc = ctx->sched;
-        RT_HIP(rt::schedule_reserve(sc, uint32_t(tiles_x * tiles_y), st));
+        RT_HIP(rt::schedule_reserve(sc, uint32_t(n_tiles), st));
         const char* e = std::getenv("RT_SCHEDULE");
         const bool lpt = !(e && std::strcmp(e, "rowmajor") == 0);
         if (lpt && sc.valid) {
@@ -857,53 +822,45 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     RT_HIP(hipMemsetAsync(ctx->counters, 0, sizeof(rt::Counters), st));
     // first-time stamps start at the maximum (atomicMin); 0xff bytes = ~0ull
     RT_HIP(hipMemsetAsync(&ctx->counters->t_first, 0xff, 2 * sizeof(unsigned long long), st));
-    const int ci = count ? 1 : 0;
-    static_assert(rt::ACCEL_LBVH_TOP < rt_context::kAccelIds, "occupancy cache too small for the accel ids");
-    if (ctx->occ_lds[accel][ci] != lds) {
-        int b = 0;
-        RT_HIP(rt::trace_occupancy(accel, count, lds, &b));
-        ctx->occ[accel][ci] = std::max(1, b);
-        ctx->occ_lds[accel][ci] = lds;
-    }
-    const uint64_t blk = rt::block_size(accel);
-    const uint64_t full = uint64_t(ctx->cu_count) * ctx->occ[accel][ci];
+    const uint64_t full = uint64_t(ctx->cu_count) * ctx->occ[accel][ci][mode];
     const uint64_t by_work = (uint64_t(P.n_units) + blk - 1) / blk;
     const int grid = int(std::max<uint64_t>(1, std::min(full, by_work)));
-    {   // chunked refill (escape-walk kernels): the last `reserve` units go out
-        // pixel by pixel. Measured (scripts/refill_ab.py, 1080p): 0 to 32 Ki are within 1 %, one
-        // pixel per lane of the grid (262 Ki) is 10-15 % slower at 13-50 spp.
+    {   // Block hand-out: the last `reserve` units go out one by one. Measured
+        // (scripts/refill_ab.py, 1080p): 0 to 32 Ki are within 1 %, one pixel per lane of the
+        // grid (262 Ki) is 10-15 % slower at 13-50 spp.
         uint64_t reserve = 8192;
         if (const char* e = std::getenv("RT_REFILL_RESERVE")) reserve = std::strtoull(e, nullptr, 10);
-        P.n_chunk_units = 0;
-        if (P.tile_cost && P.n_units > reserve) P.n_chunk_units = uint32_t((P.n_units - reserve) & ~uint64_t(63));
-        P.first_chunks = uint32_t(std::min<uint64_t>(uint64_t(grid) * blk / 64u, P.n_chunk_units / 64u));
-        // The frame is as long as its longest pixel chain; the waves that start
-        // on the longest-chain tiles of the LPT order take no further pixels, so no refill of
+        P.n_block_units = P.n_units > reserve ? uint32_t((P.n_units - reserve) & ~uint64_t(63)) : 0u;
+        P.first_blocks = uint32_t(std::min<uint64_t>(uint64_t(grid) * blk / 64u, P.n_block_units / 64u));
+        // A STREAM frame is as long as its longest pixel chain; the waves that
+        // start on the longest-chain tiles of the LPT order take no further work, so no refill of
         // their other lanes slows the chain down. 1/512 of the waves (32 on a full MI355X):
-        // 12 spp -3.4 %, 50 spp -3 %, 100 spp +-0 (scripts/env_ab.py RT_ISOLATE_TILES).
+        // 12 spp -3.4 %, 50 spp -3 %, 100 spp +-0 (scripts/env_ab.py RT_ISOLATE_TILES). HASH
+        // units are short: no isolation.
         uint64_t iso = uint64_t(grid) * blk / 64u / 512u;
         if (const char* e = std::getenv("RT_ISOLATE_TILES")) iso = std::strtoull(e, nullptr, 10);
-        P.isolate_tiles = P.tile_order ? uint32_t(std::min<uint64_t>(P.first_chunks, iso)) : 0u;
-        if (P.first_chunks) RT_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&ctx->counters->work_head),
-                                                     int(P.first_chunks * 64u), 1, st));
+        P.isolate_blocks = (P.tile_order && mode == rt::MODE_STREAM) ? uint32_t(std::min<uint64_t>(P.first_blocks, iso)) : 0u;
+        if (P.first_blocks) RT_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&ctx->counters->work_head),
+                                                     int(P.first_blocks * 64u), 1, st));
     }
     if (accel == rt::ACCEL_LBVH_TOP && ctx->treelet_stale) {   // after a build, refit or re-pad
         RT_HIP(rt::build_treelet(d.nodes, d.n_nodes, d.treelet, d.treelet_count, st));
         ctx->treelet_stale = false;
     }
-    RT_HIP(rt::launch_trace(P, accel, count, grid, lds, st));
-    ctx->last_stream = st;
+    RT_HIP(rt::launch_trace(P, accel, count, mode, grid, lds, st));
+    if (mode == rt::MODE_HASH)
+        RT_HIP(rt::launch_resolve_fixed(ctx->fixed, texels, P.accumulate, spp, accum, out, st));
     if (P.tile_cost) {
         ctx->sched.cur ^= 1;
         ctx->sched.valid = true;
     }
-    return RT_OK;
+    return mark_issued(ctx, st);
 }
 
 int rt_get_stats(rt_context* ctx, rt_stats* out) {
     if (!ctx || !out) return fail(RT_ERR_INVALID_ARGUMENT, "ctx or out is NULL");
     DeviceGuard g(ctx->device);
-    RT_HIP(hipStreamSynchronize(ctx->last_stream));
+    if (ctx->ev_valid) RT_HIP(hipEventSynchronize(ctx->ev_last));
     rt::Counters c;
     RT_HIP(hipMemcpy(&c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
     out->segments = c.segments;
@@ -920,30 +877,18 @@ int rt_resolve_rgba8(rt_context* ctx, const float* accum, uint64_t n_texels, uin
     if (!accum || !out) return fail(RT_ERR_INVALID_ARGUMENT, "accum or out is NULL");
     if (spp == 0) return fail(RT_ERR_INVALID_ARGUMENT, "spp is zero");
     DeviceGuard g(ctx->device);
-    RT_HIP(rt::launch_reduce_resolve(accum, 1, n_texels, spp, nullptr, out, static_cast<hipStream_t>(stream)));
-    return RT_OK;
-}
-
-int rt_reduce_resolve(rt_context* ctx, const float* slices, uint32_t n_slices, uint64_t n_texels,
-                      uint32_t spp, float* accum_out, uint8_t* out_rgba8, void* stream) {
-    if (!ctx) return fail(RT_ERR_INVALID_ARGUMENT, "ctx is NULL");
-    if (n_texels == 0) return RT_OK;
-    if (!slices || !out_rgba8) return fail(RT_ERR_INVALID_ARGUMENT, "slices or out_rgba8 is NULL");
-    if (n_slices == 0 || spp == 0) return fail(RT_ERR_INVALID_ARGUMENT, "n_slices or spp is zero");
-    DeviceGuard g(ctx->device);
-    RT_HIP(rt::launch_reduce_resolve(slices, n_slices, n_texels, spp, accum_out, out_rgba8,
-                                     static_cast<hipStream_t>(stream)));
+    RT_HIP(rt::launch_tonemap(accum, n_texels, spp, out, static_cast<hipStream_t>(stream)));
     return RT_OK;
 }
 
 int rt_scatter_rows(rt_context* ctx, const float* src_accum, const uint8_t* src_rgba8,
-                    const uint32_t* rows, uint32_t n_rows, uint32_t width, float* dst_accum,
+                    const uint32_t* rows, uint32_t n_rows, uint32_t width, uint32_t dst_rows, float* dst_accum,
                     uint8_t* dst_rgba8, void* stream) {
     if (!ctx || !rows) return fail(RT_ERR_INVALID_ARGUMENT, "ctx or rows is NULL");
     if ((dst_accum && !src_accum) || (dst_rgba8 && !src_rgba8))
         return fail(RT_ERR_INVALID_ARGUMENT, "source missing for a destination");
     DeviceGuard g(ctx->device);
-    RT_HIP(rt::launch_scatter_rows(src_accum, src_rgba8, rows, n_rows, width, dst_accum, dst_rgba8,
+    RT_HIP(rt::launch_scatter_rows(src_accum, src_rgba8, rows, n_rows, width, dst_rows, dst_accum, dst_rgba8,
                                    static_cast<hipStream_t>(stream)));
     return RT_OK;
 }
@@ -952,7 +897,7 @@ int rt_scatter_rows(rt_context* ctx, const float* src_accum, const uint8_t* src_
 int rt_debug_stamps(rt_context* ctx, uint64_t* out8) {
     if (!ctx || !out8) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     DeviceGuard g(ctx->device);
-    RT_HIP(hipStreamSynchronize(ctx->last_stream));
+    if (ctx->ev_valid) RT_HIP(hipEventSynchronize(ctx->ev_last));
     rt::Counters c;
     RT_HIP(hipMemcpy(&c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
     for (int k = 0; k < 8; k++) out8[k] = c.stamp[k];
@@ -967,7 +912,7 @@ int rt_debug_tile_cost(rt_context* ctx, uint32_t* out, uint64_t capacity, uint64
     if (!sc.valid || !out) return RT_OK;   // size query
     if (capacity < sc.n) return fail(RT_ERR_INVALID_ARGUMENT, "capacity");
     DeviceGuard g(ctx->device);
-    RT_HIP(hipStreamSynchronize(ctx->last_stream));
+    if (ctx->ev_valid) RT_HIP(hipEventSynchronize(ctx->ev_last));
     RT_HIP(hipMemcpy(out, sc.cost[sc.cur ^ 1], size_t(sc.n) * 4, hipMemcpyDeviceToHost));
     return RT_OK;
 }
@@ -975,7 +920,7 @@ int rt_debug_tile_cost(rt_context* ctx, uint32_t* out, uint64_t capacity, uint64
 int rt_debug_lane_hist(rt_context* ctx, uint64_t* out68) {
     if (!ctx || !out68) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     DeviceGuard g(ctx->device);
-    RT_HIP(hipStreamSynchronize(ctx->last_stream));
+    if (ctx->ev_valid) RT_HIP(hipEventSynchronize(ctx->ev_last));
     rt::Counters c;
     RT_HIP(hipMemcpy(&c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
     std::memcpy(out68, c.lane_hist, sizeof(c.lane_hist));
@@ -989,10 +934,20 @@ int rt_debug_lane_hist(rt_context* ctx, uint64_t* out68) {
 int rt_debug_walk_hist(rt_context* ctx, uint64_t* out128) {
     if (!ctx || !out128) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     DeviceGuard g(ctx->device);
-    RT_HIP(hipStreamSynchronize(ctx->last_stream));
+    if (ctx->ev_valid) RT_HIP(hipEventSynchronize(ctx->ev_last));
     rt::Counters c;
     RT_HIP(hipMemcpy(&c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
     std::memcpy(out128, c.walk_hist, sizeof(c.walk_hist));
+    return RT_OK;
+}
+
+int rt_debug_launch_info(rt_context* ctx, uint32_t* out4) {
+    if (!ctx || !out4) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    out4[0] = ctx->last_chunks;
+    out4[1] = ctx->oct_bytes ? rt::ACCEL_LBVH_OCT : ctx->lds1_bytes ? rt::ACCEL_LBVH_LDS
+              : ctx->gpu_tree ? rt::ACCEL_LBVH_TOP : rt::ACCEL_LBVH_GLOBAL;
+    out4[2] = uint32_t(ctx->oct_bytes ? ctx->oct_bytes : ctx->lds1_bytes);
+    out4[3] = uint32_t(ctx->cu_count);
     return RT_OK;
 }
 
@@ -1011,7 +966,6 @@ int rt_debug_scene(rt_context* ctx, uint32_t what, void* out, uint64_t capacity,
     }
     const void* src = nullptr;
     size_t n = 0;
-    std::vector<rt::BvhNode> raw;
     switch (what) {
         case 0: src = d.geom; n = size_t(d.n_spheres) * sizeof(rt::GeomRec); break;
         case 1: src = d.radius; n = size_t(d.n_spheres) * 4; break;
@@ -1038,7 +992,8 @@ int rt_debug_scene(rt_context* ctx, uint32_t what, void* out, uint64_t capacity,
 int rt_debug_math(int device, int op, const float* in_pairs, float* out, uint32_t n) {
     if (!in_pairs || !out) return fail(RT_ERR_INVALID_ARGUMENT, "NULL buffer");
     int nd = 0;
-    if (int rc = current_device_count(&nd)) return rc;
+    if (int rc = rt::current_device_count(&nd)) return rc;
+    if (device < 0 || device >= nd) return fail(RT_ERR_INVALID_ARGUMENT, "device index out of range");
     DeviceGuard g(device);
     float *din = nullptr, *dout = nullptr;
     RT_HIP(hipMalloc(&din, size_t(n) * 2 * sizeof(float) + 16));
@@ -1048,76 +1003,6 @@ int rt_debug_math(int device, int op, const float* in_pairs, float* out, uint32_
     RT_HIP(hipMemcpy(out, dout, size_t(n) * sizeof(float), hipMemcpyDeviceToHost));
     (void)hipFree(din);
     (void)hipFree(dout);
-    return RT_OK;
-}
-
-int rt_render(const Sphere* spheres, uint32_t sphere_count, const RenderCallInfo* rci,
-              uint32_t rci_count, float* accum, uint8_t* out, const rt_options* opt,
-              rt_stats* stats) {
-    if (!rci || rci_count == 0) return fail(RT_ERR_INVALID_ARGUMENT, "no RenderCallInfo");
-    if (!accum || !out) return fail(RT_ERR_INVALID_ARGUMENT, "accum or out is NULL");
-    const uint32_t W = rci[0].image_size.x, H = rci[0].image_size.y;
-    if (W == 0 || H == 0) return fail(RT_ERR_INVALID_ARGUMENT, "image_size is zero");
-    for (uint32_t i = 0; i < rci_count; i++) {
-        const uint32_t y0 = rci[i].offset.y;
-        const uint32_t y1 = (i + 1 < rci_count) ? rci[i + 1].offset.y : H;
-        if (rci[i].image_size.x != W || rci[i].image_size.y != H || rci[i].offset.x != 0 || y1 < y0 || y1 > H)
-            return fail(RT_ERR_INVALID_ARGUMENT, "bands must tile the image top to bottom");
-    }
-    int nd = 0;
-    if (int rc = current_device_count(&nd)) return rc;
-    std::vector<int> rcs(rci_count, RT_OK);
-    std::vector<std::string> errs(rci_count);
-    std::vector<rt_stats> st(rci_count);
-    // One host thread per band, as the reference fans out per device (src/ray_trace.cpp:687).
-    auto band = [&](uint32_t i) {
-        const uint32_t y0 = rci[i].offset.y;
-        const uint32_t y1 = (i + 1 < rci_count) ? rci[i + 1].offset.y : H;
-        const uint32_t bh = y1 - y0;
-        std::memset(&st[i], 0, sizeof(rt_stats));
-        if (bh == 0) return;
-        rt_context* ctx = nullptr;
-        int rc = rt_context_create(int(i % uint32_t(nd)), &ctx);
-        float* dacc = nullptr;
-        uint8_t* dout = nullptr;
-        const size_t texels = size_t(W) * bh;
-        auto run = [&]() -> int {
-            if (rc) return rc;
-            DeviceGuard g(ctx->device);
-            if (int r = rt_set_scene(ctx, spheres, sphere_count, nullptr)) return r;
-            RT_HIP(hipMalloc(&dacc, texels * 16));
-            RT_HIP(hipMalloc(&dout, texels * 4));
-            float* hacc = accum + size_t(y0) * W * 4;
-            uint8_t* hout = out + size_t(y0) * W * 4;
-            if (opt && opt->accumulate) RT_HIP(hipMemcpy(dacc, hacc, texels * 16, hipMemcpyHostToDevice));
-            if (int r = rt_render_device(ctx, &rci[i], nullptr, W, bh, dacc, dout, opt, nullptr)) return r;
-            RT_HIP(hipMemcpy(hacc, dacc, texels * 16, hipMemcpyDeviceToHost));
-            RT_HIP(hipMemcpy(hout, dout, texels * 4, hipMemcpyDeviceToHost));
-            return rt_get_stats(ctx, &st[i]);
-        };
-        rcs[i] = run();
-        if (rcs[i]) errs[i] = g_last_error;
-        if (ctx) {
-            DeviceGuard g(ctx->device);
-            if (dacc) (void)hipFree(dacc);
-            if (dout) (void)hipFree(dout);
-        }
-        rt_context_destroy(ctx);
-    };
-    std::vector<std::thread> pool;
-    for (uint32_t i = 1; i < rci_count; i++) pool.emplace_back(band, i);
-    band(0);
-    for (auto& t : pool) t.join();
-    rt_stats total;
-    std::memset(&total, 0, sizeof(total));
-    for (uint32_t i = 0; i < rci_count; i++) {
-        if (rcs[i]) return fail(rcs[i], errs[i]);
-        total.segments += st[i].segments;
-        total.samples += st[i].samples;
-        total.box_tests += st[i].box_tests;
-        total.sphere_tests += st[i].sphere_tests;
-    }
-    if (stats) *stats = total;
     return RT_OK;
 }
 
@@ -1135,51 +1020,6 @@ int rt_store_ppm(const char* path, const uint8_t* rgba8, uint32_t width, uint32_
     }
     ok = (std::fclose(f) == 0) && ok;
     return ok ? RT_OK : fail(RT_ERR_IO, std::string("write failed: ") + path);
-}
-
-// src/ray_trace.h:9-15. Headless: one frame of the canonical scene (t = 0), split into
-// gpu_count row bands like src/ray_trace.cpp:74-93 (the first band takes the remainder).
-void ray_trace(uint32_t samples, bool storeRenderResult, uint32_t width, uint32_t height,
-               uint32_t gpu_count) {
-    try {
-        int nd = 0;
-        if (current_device_count(&nd)) {
-            std::fprintf(stderr, "ray_trace: %s\n", g_last_error.c_str());
-            return;
-        }
-        uint32_t n = std::max(1u, std::min(gpu_count, uint32_t(nd)));
-        n = std::min(n, std::max(1u, height));
-        std::vector<Sphere> scene(488);
-        uint32_t cnt = 0;
-        rt_generate_scene(0.0f, 11, scene.data(), uint32_t(scene.size()), &cnt);
-        std::vector<RenderCallInfo> rci(n);
-        const uint32_t base = height / n, rem = height % n;
-        uint32_t y = 0;
-        for (uint32_t i = 0; i < n; i++) {
-            rt_canonical_render_call_info(samples, width, height, &rci[i]);
-            rci[i].offset = rt_uvec2{0, y};
-            y += base + (i == 0 ? rem : 0);
-        }
-        std::vector<float> acc(size_t(width) * height * 4);
-        std::vector<uint8_t> img(size_t(width) * height * 4);
-        rt_stats st;
-        const auto t0 = std::chrono::steady_clock::now();
-        int rc = rt_render(scene.data(), cnt, rci.data(), n, acc.data(), img.data(), nullptr, &st);
-        const auto t1 = std::chrono::steady_clock::now();
-        if (rc) {
-            std::fprintf(stderr, "ray_trace: %s\n", g_last_error.c_str());
-            return;
-        }
-        const double sec = std::chrono::duration<double>(t1 - t0).count();
-        std::printf("duration_per_frame: %.3f ms (%u GPU, %llu samples, %.1f Msamples/s incl. setup)\n",
-                    sec * 1e3, n, (unsigned long long)st.samples, double(st.samples) / sec / 1e6);
-        if (storeRenderResult) {
-            if (rt_store_ppm("render.ppm", img.data(), width, height))
-                std::fprintf(stderr, "ray_trace: %s\n", g_last_error.c_str());
-        }
-    } catch (const std::exception& e) {
-        std::fprintf(stderr, "ray_trace: %s\n", e.what());
-    }
 }
 
 }  // extern "C"

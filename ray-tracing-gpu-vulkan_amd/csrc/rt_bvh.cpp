@@ -217,9 +217,8 @@ struct Builder {
         return uint32_t(mid - prims.begin());
     }
 
-    // Returns the reference of the subtree [lo, hi) in the two-wide layout (inner nodes emitted
-    // depth first) and its height in inner nodes; also emits the escape-link node list.
-    uint32_t build(uint32_t lo, uint32_t hi, float* bmin_out, float* bmax_out, uint32_t* height) {
+    // Emits the subtree [lo, hi) as escape-link nodes in depth-first order.
+    void build(uint32_t lo, uint32_t hi) {
         const uint32_t me = uint32_t(out.nodes.size());
         out.nodes.push_back(BvhNode{});
         float bmin[3], bmax[3];
@@ -227,8 +226,6 @@ struct Builder {
         BvhNode n;
         n.lox = bmin[0]; n.loy = bmin[1]; n.loz = bmin[2];
         n.hix = bmax[0]; n.hiy = bmax[1]; n.hiz = bmax[2];
-        for (int k = 0; k < 3; k++) { bmin_out[k] = bmin[k]; bmax_out[k] = bmax[k]; }
-        uint32_t ref;
         if (hi - lo <= kLeafMax) {
             const uint32_t first = uint32_t(out.leaf_geom.size());
             for (uint32_t i = lo; i < lo + kLeafMax; i++) {
@@ -242,8 +239,6 @@ struct Builder {
                 }
             }
             n.first_count = (first << 4) | (hi - lo);
-            ref = kLeafFlag | (first << 3) | (hi - lo);
-            *height = 0;
         } else {
             uint32_t s = sah ? split_sah(lo, hi) : split(lo, hi);
             if (knobs.order) {   // put the larger (order 1) / smaller (order 2) child first
@@ -260,25 +255,12 @@ struct Builder {
                     s = lo + (hi - s);
                 }
             }
-            const uint32_t me2 = uint32_t(out.nodes2.size());
-            out.nodes2.push_back(Bvh2Node{});
-            float l0[3], h0[3], l1[3], h1[3];
-            uint32_t ht0 = 0, ht1 = 0;
-            const uint32_t c0 = build(lo, s, l0, h0, &ht0);
-            const uint32_t c1 = build(s, hi, l1, h1, &ht1);
+            build(lo, s);
+            build(s, hi);
             n.first_count = 0;
-            Bvh2Node m;
-            m.l0x = l0[0]; m.l0y = l0[1]; m.l0z = l0[2]; m.c0 = c0;
-            m.h0x = h0[0]; m.h0y = h0[1]; m.h0z = h0[2]; m.pad0 = 0;
-            m.l1x = l1[0]; m.l1y = l1[1]; m.l1z = l1[2]; m.c1 = c1;
-            m.h1x = h1[0]; m.h1y = h1[1]; m.h1z = h1[2]; m.pad1 = 0;
-            out.nodes2[me2] = m;
-            ref = me2;
-            *height = 1 + std::max(ht0, ht1);
         }
         n.escape = uint32_t(out.nodes.size());  // first node after this subtree
         out.nodes[me] = n;
-        return ref;
     }
 };
 
@@ -338,8 +320,7 @@ void build_lbvh_host(const Sphere* sph, uint32_t n, HostBvh& out, bool sah) {
         knobs.order = std::strstr(k, "order1") ? 1 : std::strstr(k, "order2") ? 2 : 0;
     }
     Builder b{sph, prims, out, sah, knobs};
-    float bmin[3], bmax[3];
-    out.root2 = b.build(0, uint32_t(prims.size()), bmin, bmax, &out.depth2);
+    b.build(0, uint32_t(prims.size()));
     for (BvhNode& nd : out.nodes)
         if (nd.escape >= out.nodes.size()) nd.escape = 0xffffffffu;
 }

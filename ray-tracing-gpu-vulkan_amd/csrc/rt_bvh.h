@@ -15,9 +15,6 @@ struct HostBvh {
     std::vector<GeomRec> leaf_geom;   // small spheres in leaf order: center, RADIUS (4 per leaf)
     std::vector<uint32_t> leaf_ids;   // original index per leaf slot
     float small_rmax = 0.0f;          // largest radius inside the tree (traversal slack)
-    std::vector<Bvh2Node> nodes2;     // ordered-walk layout over the same leaves
-    uint32_t root2 = 0;               // root reference for nodes2
-    uint32_t depth2 = 0;              // max inner nodes on a root-to-leaf path
 };
 
 // sah: binned surface-area splits (the default tree for small scenes); else the Morton radix

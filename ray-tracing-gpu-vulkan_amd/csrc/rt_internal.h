@@ -31,28 +31,6 @@ struct alignas(16) BvhNode {
     uint32_t first_count;        // leaf: first << 4 | count (count 1..15); inner: 0
 };
 
-// Two-wide LBVH node for the ordered (stack) walk, 64 B: both children's boxes, so one visit
-// tests two boxes and descends into the nearer hit child first (the farther one is pushed).
-// Child reference: bit 31 set = leaf, (first slot << 3) | count in the low bits; else the index
-// of an inner node.
-struct alignas(16) Bvh2Node {
-    float l0x, l0y, l0z; uint32_t c0;   // child 0: box lo, reference
-    float h0x, h0y, h0z; uint32_t pad0; // child 0: box hi
-    float l1x, l1y, l1z; uint32_t c1;   // child 1: box lo, reference
-    float h1x, h1y, h1z; uint32_t pad1; // child 1: box hi
-};
-constexpr uint32_t kLeafFlag = 0x80000000u;
-
-// Compact escape-link node, 16 B (one ds_read_b128 per visit): the padded box rounded OUTWARD to
-// binary16 (so it still contains every member sphere's AABB: the walk stays conservative and
-// exact), the escape index and the leaf field in 16 bits each. Used when the tree has fewer than
-// 65535 nodes and 8192 leaves (the LDS-staged case).
-//   x = lo.x | lo.y << 16, y = lo.z | hi.x << 16, z = hi.y | hi.z << 16  (binary16 bit patterns)
-//   w = escape | leaf << 16, escape 0xffff = end, leaf 0 = inner else 0x8000 | index << 2 | (count - 1)
-struct alignas(16) BvhNode16 {
-    uint32_t x, y, z, w;
-};
-
 // Scene as resident in HBM (one allocation per context, rebuilt by rt_set_scene).
 struct DeviceScene {
     uint32_t n_spheres = 0;
@@ -69,22 +47,28 @@ struct DeviceScene {
     GeomRec* leaf_geom = nullptr;  // spheres permuted into leaf order (contiguous per leaf)
     uint32_t* leaf_ids = nullptr;  // original index of each leaf slot
     uint32_t n_leaf = 0;
-    BvhNode16* nodes16 = nullptr;  // compact escape-link nodes (null when the tree is too big)
     BvhNode* nodes_oct = nullptr;  // host-built trees: 8 x n_nodes, one near-child-first order per
                                    // ray octant (null: every octant copy uses `nodes`' order)
     float* treelet = nullptr;      // device-built trees: kTreeletCap x 8 floats (ACCEL_LBVH_TOP)
     uint32_t* treelet_count = nullptr;   // device word: nodes in the treelet
-    Bvh2Node* nodes2 = nullptr;    // ordered-walk layout (same leaves)
-    uint32_t n_nodes2 = 0;
-    uint32_t root2 = 0;            // root reference (inner index or leaf reference)
-    uint32_t depth2 = 0;           // inner nodes on the longest root-to-leaf path (stack bound)
     float small_rmax = 0.0f;       // largest radius in the tree
 };
 
-enum : uint32_t { ACCEL_BRUTE = 1, ACCEL_LBVH = 2, ACCEL_LBVH_LDS = 3, ACCEL_LBVH2 = 4, ACCEL_LBVH2_LDS = 5, ACCEL_LBVH16_LDS = 6, ACCEL_LBVH_LDS_SCENE = 7,
-       ACCEL_LBVH_POOL = 8 /* LBVH_LDS_SCENE + tail-compaction pool, 1024-thread blocks */,
-       ACCEL_LBVH_OCT = 9  /* LBVH_LDS_SCENE with 8 octant-specialised node copies, 1024-thread blocks */,
-       ACCEL_LBVH_TOP = 10 /* tree too big for LDS: its top levels (treelet) in LDS, the rest from L2 */ };
+// Trace kernel forms (rt_kernels.hip pick()). Production: BRUTE (BASELINE config 2), OCT (trees
+// whose 8 octant node copies + scene records fit LDS: the canonical scene), LDS (one node copy +
+// scene records in LDS), TOP (bigger trees: LDS treelet + L2 subtrees). GLOBAL (every node from
+// L2) is the A/B reference of TOP (options.reserved[1] = 10).
+enum : uint32_t { ACCEL_BRUTE = 1, ACCEL_LBVH_GLOBAL = 2, ACCEL_LBVH_LDS = 3, ACCEL_LBVH_OCT = 4,
+                  ACCEL_LBVH_TOP = 5, ACCEL_COUNT = 6 };
+
+// Random stream layout of a launch (template parameter of the trace kernels).
+//   STREAM: the reference's per-pixel LCG stream (random.glsl), or with rng_counter the TEA
+//           counter restart per sample (RT_RNG_SAMPLE_COUNTER); dvec3 sum per pixel
+//           (shader.rgen:55), one lane runs all samples of a pixel.
+//   HASH:   RT_RNG_SAMPLE_HASH: sample s restarts the LCG at sample_seed(pixel_seed, s); per-sample
+//           colours summed as 20.44 fixed point with integer atomics, so a pixel's samples may be
+//           split into chunks on any lanes / GPUs in any order and the sum is the same bits.
+enum : int { MODE_STREAM = 0, MODE_HASH = 1 };
 
 // Top treelet of a tree too big for LDS (ACCEL_LBVH_TOP): the nodes of depth <= kTreeletDepth in
 // the tree's depth-first order, 2 float4 each, AB layout: A = (lo.x, lo.y, hi.x, hi.y),
@@ -96,8 +80,8 @@ constexpr uint32_t kTreeletCap = (2u << kTreeletDepth) - 1u;   // 4095 nodes, 12
 
 // Counters block (device memory, zeroed before each launch by the host).
 struct Counters {
-    uint32_t work_head;            // next unit (pixel) to hand out; chunked refill: next 64-unit chunk
-    uint32_t work_tail;            // chunked refill: next unit past n_chunk_units (per-lane hand-out)
+    uint32_t work_head;            // next unit to hand out; block refill: next 64-unit block
+    uint32_t work_tail;            // block refill: next unit past n_block_units (per-lane hand-out)
     unsigned long long segments;
     unsigned long long samples;
     unsigned long long box_tests;
@@ -111,6 +95,11 @@ struct Counters {
 };
 
 // Kernel launch parameters (passed by value as the kernel argument).
+//
+// Work units: unit u = (8x8 tile, sample chunk, pixel of the tile). Block b = u / 64 covers one
+// chunk of one tile's 64 pixels; tile rank = b / chunks, chunk = b % chunks; the tile is
+// tile_order[rank] (LPT hand-out) or the rank itself. Chunk c of a pixel runs samples
+// [c * spp / chunks, (c + 1) * spp / chunks). STREAM launches have chunks = 1.
 struct TraceParams {
     // Camera / viewport (shader.rgen:92-115), computed once per launch on the host.
     float lf[3], hor[3], ver[3], ulc[3], cup[3], crt[3];
@@ -118,21 +107,22 @@ struct TraceParams {
     float size_x, size_y;          // full image size as float (shader.rgen:42)
     uint32_t number, spp, max_depth;
     uint32_t seed_local;           // 1: seed from launch-local ids (shader.rgen:40 verbatim)
-    uint32_t rng_counter;          // 1: RT_RNG_SAMPLE_COUNTER
+    uint32_t rng_counter;          // STREAM only, 1: RT_RNG_SAMPLE_COUNTER
     uint32_t sample_base;
-    uint32_t accumulate;
+    uint32_t accumulate;           // STREAM: the pixel sum starts from accum (HASH: the resolve adds it)
     uint32_t off_x, off_y;         // band offset (rows == nullptr)
     uint32_t band_w, band_h;
     uint32_t tiles_x;              // ceil(band_w / 8)
-    uint32_t n_units;              // tiles_x * ceil(band_h / 8) * 64
-    uint32_t n_chunk_units;        // LBVH kernels: units [0, n_chunk_units) go out as whole 8x8 tiles
-                                   // (one atomic per 64 pixels per wave), the rest pixel by pixel
-    uint32_t first_chunks;         // tiles [0, first_chunks) start on wave id = tile rank (no atomic)
-    uint32_t isolate_tiles;        // waves of the first LPT tiles take no further work
+    uint32_t chunks;               // sample chunks per pixel (>= 1)
+    uint32_t n_units;              // tiles * chunks * 64
+    uint32_t n_block_units;        // units [0, n_block_units) go out as whole 64-unit blocks (one
+                                   // atomic per block per wave), the rest unit by unit
+    uint32_t first_blocks;         // blocks [0, first_blocks) start on wave id = block (no atomic)
+    uint32_t isolate_blocks;       // waves of the first LPT blocks take no further work
     const uint32_t* rows;          // optional global row per band row
     const uint32_t* tile_order;    // optional: hand-out rank -> 8x8 tile index (null: row-major)
-    uint32_t* tile_cost;           // optional: per 8x8 tile, traced segments of its most expensive
-                                   // pixel (zeroed by the host)
+    uint32_t* tile_cost;           // optional: per 8x8 tile, traced segments of its longest unit
+                                   // (zeroed by the host)
     uint32_t tile_cost_sum;        // A/B only: record the tile's total instead
     // scene
     uint32_t n_spheres;
@@ -143,21 +133,25 @@ struct TraceParams {
     const uint32_t* big_ids;
     const BvhNode* nodes;
     uint32_t n_nodes;
-    const BvhNode16* nodes16;
     const BvhNode* nodes_oct;      // optional, see DeviceScene
     const float* treelet;          // ACCEL_LBVH_TOP, see DeviceScene (2 float4 per node)
     const uint32_t* treelet_count;
-    const Bvh2Node* nodes2;
-    uint32_t n_nodes2, root2, stack_depth;
     uint32_t n_leaf;               // spheres in the tree (leaf slots)
     const GeomRec* leaf_geom;
     const uint32_t* leaf_ids;
     float cull_abs;                // LBVH node-cull slack: best + cull_abs + cull_rel * best
     float cull_rel;
     // outputs
-    float* accum;                  // band_w * band_h * 4 floats
-    uint32_t* out;                 // band_w * band_h packed rgba8
+    float* accum;                  // STREAM: band_w * band_h * 4 floats
+    uint32_t* out;                 // STREAM: band_w * band_h packed rgba8
+    unsigned long long* fixed;     // HASH: 3 planes of band_w * band_h u64 (r, g, b), zero on entry
     Counters* counters;
 };
+
+// HASH mode fixed point: a sample colour channel c in [0, 1] (every colour and the sky are <= 1,
+// so is every product of them) adds trunc(c * 2^44) (rt_kernels.hip sample_fixed); a launch may sum
+// up to 2^19 samples per pixel without overflow.
+constexpr int kFixedFracBits = 44;
+constexpr uint32_t kHashMaxSpp = 1u << 19;
 
 }  // namespace rt

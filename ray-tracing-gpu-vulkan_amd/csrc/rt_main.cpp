@@ -4,11 +4,12 @@
 // but a flag missing its value is an error here (the reference reads past argv, :33-46).
 //
 //   --help  --store  --samples <spp>  --width <w>  --height <h>  --gpus <n>
-//   --frames <n> [--animate]: the reference's benchmark frame loop (src/ray_trace.cpp:567-748):
-//   n frames back to back, each rebuilding the scene (generateRandomScene(t), t = seconds since
-//   start with --animate, else 0) and rendering one contiguous row band per GPU (the reference's
-//   split, :74-93), two frames in flight per GPU (the reference keeps one per swapchain image);
-//   prints duration_per_frame like the reference (:740-744).
+//   --frames <n> [--animate] [--rng stream|hash]: the reference's benchmark frame loop
+//   (src/ray_trace.cpp:567-748): n frames back to back, each rebuilding the scene
+//   (generateRandomScene(t), t = seconds since start with --animate, else 0) and rendering the
+//   image tiled over the GPUs with an RCCL gather to GPU 0 (rt_multi), two frames in flight (the
+//   reference keeps one per swapchain image); prints duration_per_frame like the reference
+//   (:740-744). --rng hash selects the counter-based stream (RT_RNG_SAMPLE_HASH).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -46,51 +47,40 @@ static bool parse_u32(const char* s, uint32_t& out) {
 
 namespace {
 
-struct Slot {   // one frame in flight on one GPU
-    rt_context* ctx = nullptr;
-    hipStream_t stream = nullptr;
+struct Slot {   // one frame in flight: a multi-device renderer and its device-0 frame buffers
+    rt_multi* m = nullptr;
+    hipStream_t stream = nullptr;   // device 0
     float* accum = nullptr;
     uint8_t* rgba8 = nullptr;
 };
 
 int run_frames(uint32_t samples, uint32_t width, uint32_t height, uint32_t gpu_count, uint32_t frames,
-               bool animate, bool store) {
-    int nd = 0;
-    CLI_RT(rt_device_count(&nd));
-    const uint32_t n = std::max(1u, std::min({gpu_count, uint32_t(nd), std::max(1u, height)}));
-    std::vector<uint32_t> y0(n), bh(n);   // contiguous bands, the first takes the remainder
-    for (uint32_t i = 0, y = 0; i < n; i++) {
-        bh[i] = height / n + (i == 0 ? height % n : 0);
-        y0[i] = y;
-        y += bh[i];
-    }
+               bool animate, bool store, uint32_t rng_mode) {
     constexpr int kInFlight = 2;
-    std::vector<Slot> slots(size_t(n) * kInFlight);
-    for (uint32_t g = 0; g < n; g++) {
-        CLI_HIP(hipSetDevice(int(g)));
-        for (int k = 0; k < kInFlight; k++) {
-            Slot& s = slots[g * kInFlight + k];
-            CLI_RT(rt_context_create(int(g), &s.ctx));
-            CLI_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-            CLI_HIP(hipMalloc(&s.accum, size_t(width) * bh[g] * 16));
-            CLI_HIP(hipMalloc(&s.rgba8, size_t(width) * bh[g] * 4));
-        }
+    std::vector<Slot> slots(kInFlight);
+    uint32_t n = 1;
+    CLI_HIP(hipSetDevice(0));
+    for (Slot& s : slots) {
+        CLI_RT(rt_multi_create(gpu_count, &s.m));
+        CLI_RT(rt_multi_device_count(s.m, &n));
+        CLI_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+        CLI_HIP(hipMalloc(&s.accum, size_t(width) * height * 16));
+        CLI_HIP(hipMalloc(&s.rgba8, size_t(width) * height * 4));
     }
+    rt_options opt;
+    std::memset(&opt, 0, sizeof(opt));
+    opt.rng_mode = rng_mode;
     std::vector<Sphere> scene(488);
     uint32_t cnt = 0;
     const auto t_start = std::chrono::steady_clock::now();
     auto frame = [&](uint32_t f) -> int {
         const float t = animate ? std::chrono::duration<float>(std::chrono::steady_clock::now() - t_start).count() : 0.0f;
         CLI_RT(rt_generate_scene(t, 11, scene.data(), uint32_t(scene.size()), &cnt));   // scene.h:79
-        for (uint32_t g = 0; g < n; g++) {
-            Slot& s = slots[g * kInFlight + f % kInFlight];
-            CLI_HIP(hipSetDevice(int(g)));
-            RenderCallInfo rci;
-            CLI_RT(rt_canonical_render_call_info(samples, width, height, &rci));
-            rci.offset = rt_uvec2{0, y0[g]};
-            CLI_RT(rt_set_scene(s.ctx, scene.data(), cnt, s.stream));
-            CLI_RT(rt_render_device(s.ctx, &rci, nullptr, width, bh[g], s.accum, s.rgba8, nullptr, s.stream));
-        }
+        Slot& s = slots[f % kInFlight];
+        RenderCallInfo rci;
+        CLI_RT(rt_canonical_render_call_info(samples, width, height, &rci));
+        CLI_RT(rt_multi_set_scene(s.m, scene.data(), cnt));
+        CLI_RT(rt_multi_render(s.m, &rci, &opt, s.accum, s.rgba8, s.stream));
         return 0;
     };
     auto sync_all = [&]() -> int {
@@ -98,6 +88,7 @@ int run_frames(uint32_t samples, uint32_t width, uint32_t height, uint32_t gpu_c
             CLI_HIP(hipSetDevice(int(g)));
             CLI_HIP(hipDeviceSynchronize());
         }
+        CLI_HIP(hipSetDevice(0));
         return 0;
     };
     for (uint32_t f = 0; f < kInFlight; f++)   // warm-up: every context has its LPT order
@@ -120,25 +111,17 @@ int run_frames(uint32_t samples, uint32_t width, uint32_t height, uint32_t gpu_c
         std::printf("duration_per_frame: %.3f ms (%u frames, %u GPU, %.1f Msamples/s)\n", sec / k * 1e3, k, n,
                     double(width) * height * samples * k / sec / 1e6);
     }
-    if (store) {   // the last frame: the slot it went to on every GPU
+    if (store) {   // the last frame
         std::vector<uint8_t> img(size_t(width) * height * 4);
         const uint32_t last = kInFlight + frames - 1;
-        for (uint32_t g = 0; g < n; g++) {
-            CLI_HIP(hipSetDevice(int(g)));
-            CLI_HIP(hipMemcpy(img.data() + size_t(y0[g]) * width * 4, slots[g * kInFlight + last % kInFlight].rgba8,
-                              size_t(width) * bh[g] * 4, hipMemcpyDeviceToHost));
-        }
+        CLI_HIP(hipMemcpy(img.data(), slots[last % kInFlight].rgba8, img.size(), hipMemcpyDeviceToHost));
         CLI_RT(rt_store_ppm("render.ppm", img.data(), width, height));
     }
-    for (uint32_t g = 0; g < n; g++) {
-        CLI_HIP(hipSetDevice(int(g)));
-        for (int k = 0; k < kInFlight; k++) {
-            Slot& s = slots[g * kInFlight + k];
-            rt_context_destroy(s.ctx);
-            (void)hipStreamDestroy(s.stream);
-            (void)hipFree(s.accum);
-            (void)hipFree(s.rgba8);
-        }
+    for (Slot& s : slots) {
+        rt_multi_destroy(s.m);
+        (void)hipStreamDestroy(s.stream);
+        (void)hipFree(s.accum);
+        (void)hipFree(s.rgba8);
     }
     return 0;
 }
@@ -146,7 +129,7 @@ int run_frames(uint32_t samples, uint32_t width, uint32_t height, uint32_t gpu_c
 }  // namespace
 
 int main(int argc, const char** argv) {
-    uint32_t samples = 10, width = 1920, height = 1080, gpu_count = 1, frames = 0;
+    uint32_t samples = 10, width = 1920, height = 1080, gpu_count = 1, frames = 0, rng_mode = RT_RNG_PIXEL_STREAM;
     bool store = false, animate = false;
     for (int i = 1; i < argc; i++) {
         const std::string a = argv[i];
@@ -159,11 +142,18 @@ int main(int argc, const char** argv) {
             std::puts("--gpus <count>                    # Max used GPUs count");
             std::puts("--frames <count>                  # Benchmark loop: render count frames, print duration_per_frame");
             std::puts("--animate                         # With --frames: scene time t = seconds since start");
+            std::puts("--rng <stream|hash>               # With --frames: reference LCG stream or counter-based stream");
             return 0;
         } else if (a == "--store") {
             store = true;
         } else if (a == "--animate") {
             animate = true;
+        } else if (a == "--rng") {
+            if (i + 1 >= argc || (std::strcmp(argv[i + 1], "stream") != 0 && std::strcmp(argv[i + 1], "hash") != 0)) {
+                std::fprintf(stderr, "--rng needs stream or hash\n");
+                return 2;
+            }
+            rng_mode = std::strcmp(argv[++i], "hash") == 0 ? RT_RNG_SAMPLE_HASH : RT_RNG_PIXEL_STREAM;
         } else if (a == "--samples" || a == "--width" || a == "--height" || a == "--gpus" || a == "--frames") {
             uint32_t v = 0;
             if (i + 1 >= argc || !parse_u32(argv[i + 1], v)) {
@@ -185,7 +175,7 @@ int main(int argc, const char** argv) {
         std::fprintf(stderr, "%s\n", rt_last_error());
         return 1;
     }
-    if (frames > 0) return run_frames(samples, width, height, gpu_count, frames, animate, store);
+    if (frames > 0) return run_frames(samples, width, height, gpu_count, frames, animate, store, rng_mode);
     ray_trace(samples, store, width, height, gpu_count);
     return 0;
 }

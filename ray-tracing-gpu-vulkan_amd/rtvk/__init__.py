@@ -25,9 +25,12 @@ from .abi import (CHECKERED, DIFFUSE, METAL, REFRACTIVE, SOLID, Options, RenderC
 __all__ = [
     "DIFFUSE", "METAL", "REFRACTIVE", "SOLID", "CHECKERED", "Sphere", "Scene", "RenderCallInfo",
     "Options", "Stats", "RtError", "generateRandomScene", "canonical_render_call_info",
-    "make_options", "Renderer", "render", "ray_trace", "store_ppm", "spheres_to_numpy",
-    "load_library",
+    "make_options", "Renderer", "MultiRenderer", "render", "ray_trace", "store_ppm", "spheres_to_numpy",
+    "load_library", "HASH", "STREAM",
 ]
+
+STREAM = abi.RT_RNG_PIXEL_STREAM   # the reference's per-pixel LCG stream (random.glsl)
+HASH = abi.RT_RNG_SAMPLE_HASH      # counter-based per-sample streams, chunked across lanes / GPUs
 
 MAX_DEPTH = 50  # shader.rgen:27
 
@@ -114,11 +117,12 @@ class Renderer:
             pass
 
     def set_scene(self, spheres, stream=None) -> None:
-        """Upload spheres (ctypes Sphere array or (n,80) uint8 records) and build the LBVH."""
+        """Upload spheres (ctypes Sphere array or (n,80) uint8 records) and build the LBVH, ordered
+        on `stream` (torch's current stream by default, like render_device)."""
         buf = spheres if not isinstance(spheres, np.ndarray) else np.ascontiguousarray(spheres, np.uint8)
         n = len(spheres)
         ptr = ctypes.addressof(buf) if not isinstance(buf, np.ndarray) else buf.ctypes.data
-        st = 0 if stream is None else _stream_ptr(stream)
+        st = _stream_ptr(stream)
         check(self._lib.rt_set_scene(self._ctx, ptr if n else None, n, st))
         self.sphere_count = n
 
@@ -127,7 +131,7 @@ class Renderer:
         buf = spheres if not isinstance(spheres, np.ndarray) else np.ascontiguousarray(spheres, np.uint8)
         n = len(spheres)
         ptr = ctypes.addressof(buf) if not isinstance(buf, np.ndarray) else buf.ctypes.data
-        st = 0 if stream is None else _stream_ptr(stream)
+        st = _stream_ptr(stream)
         check(self._lib.rt_refit_scene(self._ctx, ptr if n else None, n, st))
         self.sphere_count = n
 
@@ -200,11 +204,30 @@ class Renderer:
         check(self._lib.rt_get_stats(self._ctx, ctypes.byref(st)))
         return st
 
+    def launch_info(self) -> dict:
+        """Of the last launch: sample chunks per pixel, the staged kernel form of the scene, its
+        LDS bytes, the CU count (rt_debug_launch_info)."""
+        v = (ctypes.c_uint32 * 4)()
+        check(self._lib.rt_debug_launch_info(self._ctx, v))
+        forms = {2: "lbvh-global", 3: "lbvh-lds", 4: "lbvh-octant-lds", 5: "lbvh-treelet"}
+        return {"chunks": int(v[0]), "form": forms.get(int(v[1]), str(v[1])), "lds_bytes": int(v[2]),
+                "cus": int(v[3])}
+
     def scatter_rows(self, src_accum, src_rgba8, rows, dst_accum, dst_rgba8, stream=None) -> None:
         """dst[rows[i]] = src[i] (device), the reorder after a multi-GPU gather."""
         n, w = int(src_rgba8.shape[0]), int(src_rgba8.shape[1])
+        _check_dev_tensor(src_rgba8, "torch.uint8", (n, w, 4))
+        dh = int(dst_rgba8.shape[0])
+        _check_dev_tensor(dst_rgba8, "torch.uint8", (dh, w, 4))
+        if src_accum is not None or dst_accum is not None:
+            _check_dev_tensor(src_accum, "torch.float32", (n, w, 4))
+            _check_dev_tensor(dst_accum, "torch.float32", (dh, w, 4))
+        if rows.numel() != n or not rows.is_cuda or rows.element_size() != 4 or not rows.is_contiguous():
+            raise ValueError("rows must be a contiguous 4-byte cuda tensor of one entry per source row")
+        if n and (int(rows.min()) < 0 or int(rows.max()) >= dh):
+            raise ValueError(f"rows must lie in [0, {dh})")
         check(self._lib.rt_scatter_rows(self._ctx, src_accum.data_ptr() if src_accum is not None else None,
-                                        src_rgba8.data_ptr(), rows.data_ptr(), n, w,
+                                        src_rgba8.data_ptr(), rows.data_ptr(), n, w, dh,
                                         dst_accum.data_ptr() if dst_accum is not None else None,
                                         dst_rgba8.data_ptr(), _stream_ptr(stream)))
 
@@ -216,19 +239,56 @@ class Renderer:
             raise ValueError("out must hold 4 bytes per accumulator texel")
         check(self._lib.rt_resolve_rgba8(self._ctx, accum.data_ptr(), n, spp, out.data_ptr(), _stream_ptr(stream)))
 
-    def reduce_resolve(self, slices, spp: int, accum_out, out, stream=None) -> None:
-        """accum_out = float sum of slices[0], slices[1], ... in that order (alpha 1), out = its
-        rgba8 tonemap (rt_reduce_resolve). slices: contiguous float32 cuda tensor [n, ..., 4];
-        accum_out (optional) / out: cuda tensors of one slice's texels."""
-        if not slices.is_contiguous() or str(slices.dtype) != "torch.float32" or not slices.is_cuda:
-            raise ValueError("slices must be a contiguous float32 tensor")
-        ns = int(slices.shape[0])
-        n = slices.numel() // (4 * ns)
-        if out.numel() != 4 * n or (accum_out is not None and accum_out.numel() != 4 * n):
-            raise ValueError("accum_out / out must hold one texel per slice texel")
-        check(self._lib.rt_reduce_resolve(self._ctx, slices.data_ptr(), ns, n, spp,
-                                          accum_out.data_ptr() if accum_out is not None else None,
-                                          out.data_ptr(), _stream_ptr(stream)))
+
+class MultiRenderer:
+    """One process driving `gpu_count` GPUs (rt_multi): one context + stream per device and one
+    RCCL communicator over them. A frame tiles the image into 8-row strips dealt round robin over
+    the devices and gathers every device's strips to device 0 over xGMI (grouped ncclSend /
+    ncclRecv), where they are reordered; the image equals the one-GPU image bit for bit."""
+
+    def __init__(self, gpu_count: int = 1):
+        self._lib = load_library()
+        self._m = ctypes.c_void_p()
+        check(self._lib.rt_multi_create(gpu_count, ctypes.byref(self._m)))
+        n = ctypes.c_uint32()
+        check(self._lib.rt_multi_device_count(self._m, ctypes.byref(n)))
+        self.device_count = n.value
+
+    def close(self) -> None:
+        if self._m:
+            self._lib.rt_multi_destroy(self._m)
+            self._m = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_scene(self, spheres) -> None:
+        buf = spheres if not isinstance(spheres, np.ndarray) else np.ascontiguousarray(spheres, np.uint8)
+        ptr = ctypes.addressof(buf) if not isinstance(buf, np.ndarray) else buf.ctypes.data
+        check(self._lib.rt_multi_set_scene(self._m, ptr if len(spheres) else None, len(spheres)))
+
+    def render(self, rci: RenderCallInfo, accum, out, options: Optional[Options] = None, stream=None) -> None:
+        """One frame into device-0 tensors accum (float32 [H, W, 4]) and out (uint8 [H, W, 4])."""
+        W, H = rci.image_size.x, rci.image_size.y
+        _check_dev_tensor(accum, "torch.float32", (H, W, 4))
+        _check_dev_tensor(out, "torch.uint8", (H, W, 4))
+        check(self._lib.rt_multi_render(self._m, ctypes.byref(rci),
+                                        ctypes.byref(options) if options is not None else None,
+                                        accum.data_ptr(), out.data_ptr(), _stream_ptr(stream)))
+
+    def stats(self) -> Stats:
+        st = Stats()
+        check(self._lib.rt_multi_stats(self._m, ctypes.byref(st)))
+        return st
 
 
 @dataclass

@@ -24,7 +24,8 @@ MAX_SPHERE_AMOUNT = 512  # src/scene.h:24
 
 RT_OK = 0
 RT_SEED_GLOBAL, RT_SEED_LAUNCH_LOCAL = 0, 1
-RT_RNG_PIXEL_STREAM, RT_RNG_SAMPLE_COUNTER = 0, 1
+RT_RNG_PIXEL_STREAM, RT_RNG_SAMPLE_COUNTER, RT_RNG_SAMPLE_HASH = 0, 1, 2
+RT_ABI_VERSION = 2
 RT_ACCEL_AUTO, RT_ACCEL_BRUTE, RT_ACCEL_LBVH = 0, 1, 2
 
 
@@ -108,13 +109,19 @@ EXPORTS = {
     "rt_render_device": (_I, [_P, ctypes.POINTER(RenderCallInfo), _P, _U32, _U32, _P, _P,
                               ctypes.POINTER(Options), _P]),
     "rt_get_stats": (_I, [_P, ctypes.POINTER(Stats)]),
-    "rt_scatter_rows": (_I, [_P, _P, _P, _P, _U32, _U32, _P, _P, _P]),
+    "rt_scatter_rows": (_I, [_P, _P, _P, _P, _U32, _U32, _U32, _P, _P, _P]),
     "rt_resolve_rgba8": (_I, [_P, _P, ctypes.c_uint64, _U32, _P, _P]),
-    "rt_reduce_resolve": (_I, [_P, _P, _U32, ctypes.c_uint64, _U32, _P, _P, _P]),
+    "rt_multi_create": (_I, [_U32, ctypes.POINTER(_P)]),
+    "rt_multi_destroy": (_I, [_P]),
+    "rt_multi_device_count": (_I, [_P, ctypes.POINTER(_U32)]),
+    "rt_multi_set_scene": (_I, [_P, _P, _U32]),
+    "rt_multi_render": (_I, [_P, ctypes.POINTER(RenderCallInfo), ctypes.POINTER(Options), _P, _P, _P]),
+    "rt_multi_stats": (_I, [_P, ctypes.POINTER(Stats)]),
     "rt_render": (_I, [_P, _U32, _P, _U32, _P, _P, ctypes.POINTER(Options), ctypes.POINTER(Stats)]),
     "rt_store_ppm": (_I, [ctypes.c_char_p, _P, _U32, _U32]),
     "rt_debug_math": (_I, [_I, _I, _P, _P, _U32]),
     "rt_debug_stamps": (_I, [_P, _P]),
+    "rt_debug_launch_info": (_I, [_P, _P]),
     "rt_debug_walk_hist": (_I, [_P, _P]),
     "rt_debug_lane_hist": (_I, [_P, _P]),
     "rt_debug_tile_cost": (_I, [_P, _P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),

@@ -22,12 +22,17 @@ CASES = {
                                      max_depth=3, seed_mode=1, rng_mode=0, t=0.0, K=11),
     "g40x24_spp2_counter": dict(W=40, H=24, offset=[0, 0], band_w=40, band_h=24, spp=2, max_depth=50,
                                 seed_mode=0, rng_mode=1, t=0.5, K=11),
+    # RT_RNG_SAMPLE_HASH (counter-based per-sample streams, fixed-point sums), a band with offset
+    "g56x40_spp7_hash": dict(W=56, H=48, offset=[0, 8], band_w=56, band_h=40, spp=7, max_depth=50,
+                             seed_mode=0, rng_mode=2, t=0.0, K=11),
 }
 
 
-def main():
+def main(only=None):
     oracle.build()
     for name, m in CASES.items():
+        if only and name not in only:
+            continue
         sc = oracle.generate_scene(m["t"], m["K"])
         rci = oracle.render_call_info(m["spp"], m["W"], m["H"], tuple(m["offset"]))
         op = oracle.options(max_depth=m["max_depth"], seed_mode=m["seed_mode"], rng_mode=m["rng_mode"])
@@ -38,4 +43,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])

@@ -55,7 +55,7 @@ def test_struct_layouts(rtvk):
 
 
 def test_abi_version(rtvk):
-    assert rtvk.load_library().rt_abi_version() == 1
+    assert rtvk.load_library().rt_abi_version() == 2
 
 
 @pytest.mark.parametrize("t,K", [(0.0, 11), (1.25, 11), (0.0, 3), (0.0, 40)])

@@ -13,7 +13,7 @@ ROOT = Path(__file__).resolve().parent.parent
 @pytest.mark.gpu
 def test_bench_json_line_contract():
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--width", "96", "--height", "64", "--spp", "2",
-                        "--steps", "3", "--warmup", "1", "--no-brute-line"],
+                        "--steps", "3", "--warmup", "1"],
                        capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -32,5 +32,7 @@ def test_bench_json_line_contract():
     cb = d["cpu_baseline"]
     for k in ("value", "unit", "cores", "kind", "sample"):
         assert k in cb, k
-    assert cb["kind"] == "port" and cb["cores"] >= 1
+    assert cb["kind"] == "port" and cb["cores"] >= 1 and cb["nproc"] >= 1 and cb["cpu_model"]
+    assert d["config"]["rng"] == "hash" and "reference_stream" in d and "brute_force" in d
+    assert d["roofline"]["lib_sha256"] and "frac_basis" in d["roofline"]
     assert cb["parity"]["accum_bit_exact"] and cb["parity"]["rgba8_equal"] and cb["parity"]["psnr_db"] == "inf"

@@ -56,15 +56,19 @@ def test_frames_no_device_fails_loudly():
 
 
 @pytest.mark.gpu
-def test_frame_loop_matches_oracle(tmp_path, oracle):
-    """--frames: the benchmark loop (two frames in flight, per-frame scene rebuild) prints
-    duration_per_frame like the reference and its last frame equals the oracle's."""
-    r = run("--frames", "5", "--store", "--samples", "2", "--width", "72", "--height", "40", cwd=tmp_path)
+@pytest.mark.parametrize("rng", ["stream", "hash"])
+def test_frame_loop_matches_oracle(tmp_path, oracle, rng):
+    """--frames: the benchmark loop (two frames in flight, per-frame scene rebuild, the image tiled
+    over the GPUs with an RCCL gather) prints duration_per_frame like the reference and its last
+    frame equals the oracle's, in both random stream modes."""
+    r = run("--frames", "5", "--store", "--samples", "2", "--width", "72", "--height", "40", "--rng", rng,
+            cwd=tmp_path)
     assert r.returncode == 0, r.stderr
     assert "duration_per_frame" in r.stdout and "Msamples/s" in r.stdout
     data = (tmp_path / "render.ppm").read_bytes()
     hdr = b"P6\n72 40\n255\n"
     assert data.startswith(hdr)
     img = np.frombuffer(data[len(hdr):], np.uint8).reshape(40, 72, 3)
-    _, ref, _ = oracle.render(oracle.generate_scene(), oracle.render_call_info(2, 72, 40), 72, 40)
+    _, ref, _ = oracle.render(oracle.generate_scene(), oracle.render_call_info(2, 72, 40), 72, 40,
+                              opts=oracle.options(rng_mode=2 if rng == "hash" else 0))
     np.testing.assert_array_equal(img, ref[..., :3])

@@ -18,18 +18,35 @@ import pytest
 pytestmark = pytest.mark.gpu
 GOLDEN = Path(__file__).resolve().parent / "golden"
 BRUTE, LBVH = 1, 2
-LBVH_ORDERED = 3   # test-only alias: accel LBVH with the ordered two-wide walk (options.reserved[1] = 2)
-LBVH_COMPACT = 4   # test-only alias: accel LBVH, escape-link walk over 16-B nodes (options.reserved[1] = 4)
-LBVH_POOL = 5      # test-only alias: accel LBVH, LDS scene + tail-compaction pool (options.reserved[1] = 7)
-LBVH_OCT = 6       # test-only alias: accel LBVH, octant-specialised node copies in LDS (options.reserved[1] = 8)
-WALK_FORM = {LBVH_ORDERED: 2, LBVH_COMPACT: 4, LBVH_POOL: 7, LBVH_OCT: 8}
-HOST_TREE_FORMS = (LBVH_ORDERED, LBVH_COMPACT)
+LBVH_LDS1 = 6      # test-only alias: accel LBVH, one node copy in LDS (options.reserved[1] = 6)
+LBVH_GLOBAL = 10   # test-only alias: accel LBVH, every node from L2 (options.reserved[1] = 10)
+WALK_FORM = {LBVH_LDS1: 6, LBVH_GLOBAL: 10}
+FORMS = [BRUTE, LBVH, LBVH_LDS1, LBVH_GLOBAL]
+STREAM, COUNTER, HASH = 0, 1, 2
+
+
+@contextlib.contextmanager
+def env(**kv):
+    """Temporarily set (value str) or clear (None) environment variables read by the library."""
+    prev = {k: os.environ.get(k) for k in kv}
+    for k, v in kv.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = str(v)
+    try:
+        yield
+    finally:
+        for k, v in prev.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
 @contextlib.contextmanager
 def tree_builder(kind):
-    """RT_BVH_BUILD (gpu | sah | morton) for the scenes set inside; the walk A/B forms need a
-    host-built tree."""
+    """RT_BVH_BUILD (gpu | sah | morton) for the scenes set inside."""
     prev = os.environ.get("RT_BVH_BUILD")
     if kind:
         os.environ["RT_BVH_BUILD"] = kind
@@ -66,7 +83,7 @@ def renderer(rtvk):
 def gpu_render(rtvk, renderer, torch, spheres, rci_u32, band_w, band_h, rows=None, accel=LBVH,
                max_depth=50, seed_mode=0, rng_mode=0, accumulate=False, sample_base=0, accum=None,
                count=False, builder=None):
-    with tree_builder(builder or ("sah" if accel in HOST_TREE_FORMS else None)):
+    with tree_builder(builder):
         renderer.set_scene(np.ascontiguousarray(spheres, np.uint8).reshape(-1, 80))
     rci = rtvk.RenderCallInfo.from_buffer_copy(np.ascontiguousarray(rci_u32).tobytes())
     acc = (torch.zeros((band_h, band_w, 4), dtype=torch.float32, device="cuda") if accum is None
@@ -123,17 +140,39 @@ def test_math_primitives_bit_exact(rtvk, torch, oracle, op):
         y = np.zeros(n, np.float32)
         x2 = x * x
         ref = np.where(x < 0, np.float32(np.nan), x2 * x2 * x).astype(np.float32)
-    pairs = np.ascontiguousarray(np.stack([x, y], 1), np.float32)
-    out = np.zeros(n, np.float32)
-    from rtvk import abi
-    abi.check(rtvk.load_library().rt_debug_math(0, op, pairs.ctypes.data, out.ctypes.data, n))
+    out = _debug_math(rtvk, op, x, y)
     same = (out.view(np.uint32) == ref.astype(np.float32).view(np.uint32)) | (np.isnan(out) & np.isnan(ref))
     assert same.all(), f"op {op}: {np.count_nonzero(~same)} differ, e.g. x={x[~same][:3]} gpu={out[~same][:3]} ref={ref[~same][:3]}"
 
 
+def _debug_math(rtvk, op, x, y):
+    pairs = np.ascontiguousarray(np.stack([x, y], 1), np.float32)
+    out = np.zeros(len(x), np.float32)
+    from rtvk import abi
+    abi.check(rtvk.load_library().rt_debug_math(0, op, pairs.ctypes.data, out.ctypes.data, len(x)))
+    return out
+
+
+def test_hash_primitives_bit_exact(rtvk, torch, oracle):
+    """RT_RNG_SAMPLE_HASH primitives: the sample-seed hash (bit patterns) and the 20.44 fixed-point
+    conversion of a colour channel (low / high words), device vs oracle."""
+    rng = np.random.default_rng(11)
+    ps = rng.integers(0, 2**32, 4000, dtype=np.uint64).astype(np.uint32)
+    sm = rng.integers(0, 2**20, 4000, dtype=np.uint64).astype(np.uint32)
+    got = _debug_math(rtvk, 6, ps.view(np.float32), sm.view(np.float32)).view(np.uint32)
+    ref = np.array([oracle.sample_seed_hash(int(a), int(b)) for a, b in zip(ps, sm)], np.uint32)
+    np.testing.assert_array_equal(got, ref)
+    c = np.concatenate([rng.uniform(0, 1, 3000), 10.0 ** rng.uniform(-40, 0, 3000),
+                        [0.0, 1.0, -1.0, 2.0, np.nan, np.inf, 2.0 ** -44, 2.0 ** -45]]).astype(np.float32)
+    lo = _debug_math(rtvk, 7, c, np.zeros_like(c)).view(np.uint32).astype(np.uint64)
+    hi = _debug_math(rtvk, 8, c, np.zeros_like(c)).view(np.uint32).astype(np.uint64)
+    ref = np.array([oracle.sample_fixed(float(v)) for v in c], np.uint64)
+    np.testing.assert_array_equal(lo | (hi << np.uint64(32)), ref)
+
+
 # ---- golden fixtures --------------------------------------------------------------------------
-@pytest.mark.parametrize("accel", [BRUTE, LBVH, LBVH_ORDERED, LBVH_COMPACT, LBVH_POOL, LBVH_OCT])
-@pytest.mark.parametrize("case", ["g64x36_spp4", "g48x32_spp3_depth3_local", "g40x24_spp2_counter"])
+@pytest.mark.parametrize("accel", FORMS)
+@pytest.mark.parametrize("case", ["g64x36_spp4", "g48x32_spp3_depth3_local", "g40x24_spp2_counter", "g56x40_spp7_hash"])
 def test_golden(rtvk, renderer, torch, oracle, case, accel):
     m = json.loads((GOLDEN / f"{case}.json").read_text())
     g = np.load(GOLDEN / f"{case}.npz", allow_pickle=False)
@@ -158,10 +197,23 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("accel", [BRUTE, LBVH, LBVH_ORDERED, LBVH_COMPACT, LBVH_POOL, LBVH_OCT])
+@pytest.mark.parametrize("accel", FORMS)
 @pytest.mark.parametrize("case", range(len(CASES)))
 def test_vs_oracle(rtvk, renderer, torch, oracle, case, accel):
     W, H, oy, bh, spp, t, K, kw = CASES[case]
+    _vs_oracle(rtvk, renderer, torch, oracle, W, H, oy, bh, spp, t, K, kw, accel)
+
+
+@pytest.mark.parametrize("accel", FORMS)
+@pytest.mark.parametrize("case", [0, 1, 2, 3, 5, 6])
+def test_vs_oracle_hash(rtvk, renderer, torch, oracle, case, accel):
+    """The same cases in RT_RNG_SAMPLE_HASH mode: per-sample counter streams, chunked over lanes,
+    fixed-point sums, resolve kernel: bit-exact vs the oracle's in-order restatement."""
+    W, H, oy, bh, spp, t, K, kw = CASES[case]
+    _vs_oracle(rtvk, renderer, torch, oracle, W, H, oy, bh, spp, t, K, dict(kw, rng_mode=HASH), accel)
+
+
+def _vs_oracle(rtvk, renderer, torch, oracle, W, H, oy, bh, spp, t, K, kw, accel):
     sc = oracle.generate_scene(t, K)
     rci = oracle.render_call_info(spp, W, H, (0, oy))
     ra, ro, rst = oracle.render(sc, rci, W, bh, opts=oracle.options(**kw))
@@ -174,9 +226,12 @@ def test_empty_and_single_sphere(rtvk, renderer, torch, oracle):
     rci = oracle.render_call_info(2, 20, 10)
     for sc in (np.zeros((0, 80), np.uint8), oracle.generate_scene()[:1], oracle.generate_scene()[3:4]):
         ra, ro, _ = oracle.render(sc, rci, 20, 10)
-        for accel in (BRUTE, LBVH, LBVH_ORDERED, LBVH_COMPACT, LBVH_POOL, LBVH_OCT):
+        rh, oh, _ = oracle.render(sc, rci, 20, 10, opts=oracle.options(rng_mode=HASH))
+        for accel in FORMS:
             a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, 20, 10, accel=accel)
             assert_same(a, o, ra, ro)
+            a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, 20, 10, accel=accel, rng_mode=HASH)
+            assert_same(a, o, rh, oh)
 
 
 def test_rows_strip_map(rtvk, renderer, torch, oracle):
@@ -189,26 +244,84 @@ def test_rows_strip_map(rtvk, renderer, torch, oracle):
     assert_same(a, o, fa[rows], fo[rows])
 
 
-def test_accumulate_and_counter_rng(rtvk, renderer, torch, oracle):
+@pytest.mark.parametrize("rng_mode", [COUNTER, HASH])
+@pytest.mark.parametrize("accel", [BRUTE, LBVH])
+def test_accumulate_and_counter_rng(rtvk, renderer, torch, oracle, rng_mode, accel):
+    """Progressive accumulation (accumulate + sample_base) in both counter modes: the second call
+    adds samples 2..4 to the float accumulator of the first."""
     W, H = 24, 16
     sc = oracle.generate_scene()
-    rci = oracle.render_call_info(2, W, H)
-    base, _, _ = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=1))
-    ra, ro, _ = oracle.render(sc, rci, W, H, accum=base, opts=oracle.options(rng_mode=1, accumulate=1, sample_base=2))
-    a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accum=base, rng_mode=1, accumulate=True, sample_base=2)
+    rci = oracle.render_call_info(3, W, H)
+    base, _, _ = oracle.render(sc, oracle.render_call_info(2, W, H), W, H, opts=oracle.options(rng_mode=rng_mode))
+    ra, ro, _ = oracle.render(sc, rci, W, H, accum=base,
+                              opts=oracle.options(rng_mode=rng_mode, accumulate=1, sample_base=2))
+    a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accum=base, rng_mode=rng_mode, accumulate=True,
+                         sample_base=2, accel=accel)
     assert_same(a, o, ra, ro)
 
 
-def test_host_rt_render_bands(rtvk, oracle):
-    """rt_render with 3 bands (one per GPU in the reference; here all on the visible devices)."""
+@pytest.mark.parametrize("chunks", ["1", "2", "3", "7", "13", "4096"])
+def test_hash_chunk_invariance(rtvk, renderer, torch, oracle, chunks):
+    """RT_RNG_SAMPLE_HASH: splitting every pixel's 13 samples into 1..13 chunks run by different
+    lanes in any order (RT_SAMPLE_CHUNKS; 4096 is clamped to spp) gives the oracle's bits, with
+    the same segment and sample counts, on a ragged band, twice (the second with the LPT order)."""
+    W, H, spp = 77, 45, 13
+    sc = oracle.generate_scene()
+    rci = oracle.render_call_info(spp, W, H)
+    ra, ro, rs = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=HASH))
+    with env(RT_SAMPLE_CHUNKS=chunks):
+        for accel in (LBVH, LBVH, BRUTE):
+            a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, rng_mode=HASH, accel=accel)
+            assert_same(a, o, ra, ro)
+            assert (st.segments, st.samples) == rs[:2]
+            if accel == LBVH:
+                assert renderer.launch_info()["chunks"] == min(int(chunks), spp)
+
+
+@pytest.mark.parametrize("rng_mode", [STREAM, HASH])
+def test_host_rt_render_bands(rtvk, oracle, rng_mode):
+    """rt_render with 3 contiguous bands (one per GPU in the reference, src/ray_trace.cpp:74-93;
+    here band i on device i % n), gathered to device 0 by one RCCL group (sends to itself on a
+    one-GPU box) and copied to the host: equals the one-device frame; then accumulate on top."""
     W, H = 32, 20
     sc = oracle.generate_scene()
     rcis = [rtvk.canonical_render_call_info(2, W, H) for _ in range(3)]
     for r, y in zip(rcis, (0, 7, 13)):
         r.offset.y = y
-    res = rtvk.render(rtvk.generateRandomScene(), rcis)
-    ra, ro, _ = oracle.render(sc, oracle.render_call_info(2, W, H), W, H)
+    opt = rtvk.make_options(rng_mode=rng_mode)
+    res = rtvk.render(rtvk.generateRandomScene(), rcis, options=opt)
+    ra, ro, rs = oracle.render(sc, oracle.render_call_info(2, W, H), W, H, opts=oracle.options(rng_mode=rng_mode))
     assert_same(res.accum, res.rgba8, ra, ro)
+    assert (res.stats.segments, res.stats.samples) == rs[:2]
+    opt2 = rtvk.make_options(rng_mode=rng_mode, accumulate=True, sample_base=2 if rng_mode else 0)
+    res2 = rtvk.render(rtvk.generateRandomScene(), rcis, options=opt2, accum=res.accum)
+    ra2, ro2, _ = oracle.render(sc, oracle.render_call_info(2, W, H), W, H, accum=ra,
+                                opts=oracle.options(rng_mode=rng_mode, accumulate=1, sample_base=2 if rng_mode else 0))
+    assert_same(res2.accum, res2.rgba8, ra2, ro2)
+
+
+@pytest.mark.parametrize("rng_mode", [STREAM, HASH])
+def test_multi_renderer_rccl(rtvk, torch, oracle, rng_mode):
+    """rt_multi (one process, every visible GPU up to 8, one RCCL communicator): 8-row strips
+    dealt round robin, each device's strips sent to device 0 (itself included) in one RCCL group
+    and reordered there; two frames (the second with the LPT order) equal the one-device oracle
+    frame bit for bit, and the statistics are summed over the devices."""
+    W, H, spp = 72, 43, 3
+    sc = oracle.generate_scene()
+    rci_np = oracle.render_call_info(spp, W, H)
+    ra, ro, rs = oracle.render(sc, rci_np, W, H, opts=oracle.options(rng_mode=rng_mode))
+    with rtvk.MultiRenderer(8) as m:
+        assert m.device_count == torch.cuda.device_count() or m.device_count == 8
+        m.set_scene(sc)
+        rci = rtvk.RenderCallInfo.from_buffer_copy(rci_np.tobytes())
+        for _ in range(2):
+            acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda:0")
+            out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda:0")
+            m.render(rci, acc, out, options=rtvk.make_options(rng_mode=rng_mode))
+            torch.cuda.synchronize()
+            assert_same(acc.cpu().numpy(), out.cpu().numpy(), ra, ro)
+            st = m.stats()
+            assert (st.segments, st.samples) == rs[:2]
 
 
 # ---- full size --------------------------------------------------------------------------------
@@ -235,7 +348,7 @@ def test_lbvh_equals_brute_full_size(rtvk, renderer, torch, oracle, W, H, spp, K
         al, ol, sl = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH, builder=builder)
         assert_same(al, ol, ab, ob)
         assert sb.segments == sl.segments
-    for form in (LBVH_ORDERED, LBVH_COMPACT, LBVH_POOL, LBVH_OCT):
+    for form in (LBVH_LDS1, LBVH_GLOBAL):
         ao, oo, so = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=form)
         assert_same(ao, oo, ab, ob)
 
@@ -289,7 +402,7 @@ def test_far_and_grazing_cameras(rtvk, renderer, torch, oracle, cam):
     f[8:11] = cam
     f[12:15] = [-cam[0], -cam[1], -cam[2]]
     ra, ro, _ = oracle.render(sc, rci, W, H)
-    for accel in (BRUTE, LBVH, LBVH_ORDERED, LBVH_COMPACT):
+    for accel in FORMS:
         a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=accel)
         assert_same(a, o, ra, ro)
     a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH, builder="gpu")
@@ -318,7 +431,7 @@ def test_scatter_rows_reassembles_strips(rtvk, renderer, torch, oracle):
     assert_same(full_a.cpu().numpy(), full_o.cpu().numpy(), ra, ro)
 
 
-@pytest.mark.parametrize("form", [LBVH, LBVH_OCT, LBVH_POOL])
+@pytest.mark.parametrize("form", [LBVH, LBVH_LDS1])
 def test_lbvh_equals_brute_bench_workload(rtvk, renderer, torch, oracle, form):
     """The bench frame itself (1920x1080, 100 spp, canonical scene): ~5.9e8 traced segments, so
     rare rays (a direction component that is exactly zero, grazing hits) all occur; every
@@ -349,39 +462,6 @@ def test_resolve_rgba8_edge_values(rtvk, renderer, torch, oracle):
         renderer.resolve_rgba8(torch.from_numpy(a).cuda(), 0, out)
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sample_split_subframes(rtvk, renderer, torch, oracle, world):
-    """The sample-split multi-GPU frame (rtvk.dist.SampleSplitRenderer) on one device: the sub-frame
-    of each simulated rank (spp_r samples, number = 7 + r) equals the oracle's, and
-    rt_reduce_resolve of the stacked sub-frames equals their float sum in rank order (alpha 1)
-    and its tonemap, bit for bit."""
-    from rtvk.dist import split_samples
-    W, H, spp = 72, 40, 5
-    sc = oracle.generate_scene()
-    renderer.set_scene(sc)
-    slices = torch.zeros((world, H, W, 4), dtype=torch.float32, device="cuda")
-    ref = None
-    for r, s in enumerate(split_samples(spp, world)):
-        rci = oracle.render_call_info(s, W, H, number=7 + r)
-        o = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
-        renderer.render_device(rtvk.RenderCallInfo.from_buffer_copy(rci.tobytes()), slices[r], o,
-                               options=rtvk.make_options())
-        ra, ro, _ = oracle.render(sc, rci, W, H)
-        torch.cuda.synchronize()
-        assert_same(slices[r].cpu().numpy(), o.cpu().numpy(), ra, ro)
-        ref = ra if ref is None else ref + ra
-    ref[..., 3] = 1.0
-    acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
-    out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
-    renderer.reduce_resolve(slices, spp, acc, out)
-    torch.cuda.synchronize()
-    assert_same(acc.cpu().numpy(), out.cpu().numpy(), ref, oracle.resolve(ref, spp))
-    # in place over slice 0 (the accum_out alias the library allows)
-    renderer.reduce_resolve(slices, spp, slices[0], out)
-    torch.cuda.synchronize()
-    assert_same(slices[0].cpu().numpy(), out.cpu().numpy(), ref, oracle.resolve(ref, spp))
-
-
 @pytest.mark.parametrize("reserve", ["0", "100", str(1 << 40)])
 def test_chunked_refill_same_image(rtvk, renderer, torch, oracle, reserve):
     """Pixel hand-out by whole tiles (RT_REFILL_RESERVE=0), tiles then single pixels (100), and
@@ -391,18 +471,15 @@ def test_chunked_refill_same_image(rtvk, renderer, torch, oracle, reserve):
     sc = oracle.generate_scene()
     rci = oracle.render_call_info(3, W, H)
     ra, ro, rs = oracle.render(sc, rci, W, H)
-    prev = os.environ.get("RT_REFILL_RESERVE")
-    os.environ["RT_REFILL_RESERVE"] = reserve
-    try:
+    rh, oh, rsh = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=HASH))
+    with env(RT_REFILL_RESERVE=reserve):
         for _ in range(2):   # second launch runs with the LPT hand-out order
-            a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH_OCT)
+            a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH)
             assert_same(a, o, ra, ro)
             assert (st.segments, st.samples) == (rs[0], rs[1])
-    finally:
-        if prev is None:
-            os.environ.pop("RT_REFILL_RESERVE", None)
-        else:
-            os.environ["RT_REFILL_RESERVE"] = prev
+            a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH, rng_mode=HASH)
+            assert_same(a, o, rh, oh)
+            assert (st.segments, st.samples) == (rsh[0], rsh[1])
 
 
 def test_scene_swap_between_queued_frames(rtvk, renderer, torch, oracle):
@@ -425,13 +502,14 @@ def test_scene_swap_between_queued_frames(rtvk, renderer, torch, oracle):
         assert_same(a.cpu().numpy(), o.cpu().numpy(), ra, ro)
 
 
-def test_sample_split_rccl_world1(rtvk, renderer, torch, oracle):
-    """The RCCL code path of rtvk.dist.SampleSplitRenderer (all_to_all_single into the flat receive
-    buffer, rt_reduce_resolve, in-place gathers) on a one-rank NCCL group: the frame equals the
-    one-GPU render bit for bit."""
+@pytest.mark.parametrize("rng_mode", [STREAM, HASH])
+def test_strips_rccl_world1(rtvk, renderer, torch, oracle, rng_mode):
+    """bench.py's N > 1 path (rtvk.dist.DistributedRenderer: row strips per rank, torch.distributed
+    gathers over RCCL, rt_scatter_rows on rank 0) on a one-rank NCCL group: the frame equals the
+    one-GPU oracle frame bit for bit."""
     import socket
     import torch.distributed as dist
-    import rtvk.dist as rd
+    from rtvk.dist import DistributedRenderer, hip_assembler, hip_band_renderer
     W, H, spp = 80, 48, 3
     sc = oracle.generate_scene()
     renderer.set_scene(sc)
@@ -442,16 +520,14 @@ def test_sample_split_rccl_world1(rtvk, renderer, torch, oracle):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     try:
-        rd._force_collective = True
-        sr = rd.SampleSplitRenderer(W, H, spp, 0, torch.device("cuda", 0),
-                                    rd.hip_full_renderer(renderer, rci, rtvk.make_options()),
-                                    rd.hip_reducer(renderer))
-        acc, out = sr.step()
+        dr = DistributedRenderer(W, H, torch.device("cuda", 0),
+                                 hip_band_renderer(renderer, rci, rtvk.make_options(rng_mode=rng_mode)),
+                                 hip_assembler(renderer), force_gather=True)
+        acc, out = dr.step()
         torch.cuda.synchronize()
     finally:
-        rd._force_collective = False
         dist.destroy_process_group()
-    ra, ro, _ = oracle.render(sc, oracle.render_call_info(spp, W, H), W, H)
+    ra, ro, _ = oracle.render(sc, oracle.render_call_info(spp, W, H), W, H, opts=oracle.options(rng_mode=rng_mode))
     assert_same(acc.cpu().numpy(), out.cpu().numpy(), ra, ro)
 
 
@@ -551,11 +627,14 @@ def test_degenerate_sample_and_depth_counts(rtvk, renderer, torch, oracle, spp, 
     W, H = 40, 24
     sc = oracle.generate_scene()
     rci = oracle.render_call_info(spp, W, H)
-    ra, ro, rs = oracle.render(sc, rci, W, H, opts=oracle.options(max_depth=depth if depth else 50))
-    for accel in (BRUTE, LBVH):
-        a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=accel, max_depth=depth)
-        assert_same(a, o, ra, ro)
-        assert (st.segments, st.samples) == (rs[0], rs[1])
+    for rng_mode in (STREAM, HASH):
+        ra, ro, rs = oracle.render(sc, rci, W, H, opts=oracle.options(max_depth=depth if depth else 50,
+                                                                     rng_mode=rng_mode))
+        for accel in (BRUTE, LBVH):
+            a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=accel, max_depth=depth,
+                                  rng_mode=rng_mode)
+            assert_same(a, o, ra, ro)
+            assert (st.segments, st.samples) == (rs[0], rs[1])
 
 
 def test_band_dimension_limits(rtvk, renderer, torch, oracle):
@@ -567,3 +646,138 @@ def test_band_dimension_limits(rtvk, renderer, torch, oracle):
     out = torch.zeros((1, 70000, 4), dtype=torch.uint8, device="cuda")
     with pytest.raises(rtvk.RtError):
         renderer.render_device(rci, acc, out, options=rtvk.make_options())
+
+
+def test_scene_and_render_on_a_side_stream(rtvk, torch, oracle):
+    """set_scene and render_device inside torch.cuda.stream(s) (a non-blocking stream): the upload
+    is ordered before the render on s, and a render issued next on the default stream is ordered
+    after it (the context chains its operations across streams)."""
+    W, H = 64, 40
+    scs = [oracle.generate_scene(t) for t in (0.0, 1.3)]
+    rci = oracle.render_call_info(2, W, H)
+    rci_c = rtvk.RenderCallInfo.from_buffer_copy(rci.tobytes())
+    with rtvk.Renderer(0) as r:
+        s = torch.cuda.Stream()
+        accs = [torch.zeros((H, W, 4), dtype=torch.float32, device="cuda") for _ in range(3)]
+        outs = [torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda") for _ in range(3)]
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s):
+            r.set_scene(scs[0])
+            r.render_device(rci_c, accs[0], outs[0], options=rtvk.make_options())
+            r.set_scene(scs[1])
+            r.render_device(rci_c, accs[1], outs[1], options=rtvk.make_options(rng_mode=HASH))
+        r.render_device(rci_c, accs[2], outs[2], options=rtvk.make_options())   # default stream
+        torch.cuda.synchronize()
+        for k, (sc, mode) in enumerate([(scs[0], STREAM), (scs[1], HASH), (scs[1], STREAM)]):
+            ra, ro, _ = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=mode))
+            assert_same(accs[k].cpu().numpy(), outs[k].cpu().numpy(), ra, ro)
+
+
+def test_render_streams_alternate_on_one_context(rtvk, torch, oracle):
+    """Back-to-back renders of one context on different streams share its work counters and LPT
+    tables; the second waits for the first, so neither frame loses or repeats pixels."""
+    W, H = 160, 96
+    sc = oracle.generate_scene()
+    rci = oracle.render_call_info(3, W, H)
+    rci_c = rtvk.RenderCallInfo.from_buffer_copy(rci.tobytes())
+    ra, ro, _ = oracle.render(sc, rci, W, H)
+    with rtvk.Renderer(0) as r:
+        r.set_scene(sc)
+        streams = [torch.cuda.Stream() for _ in range(2)]
+        bufs = [(torch.zeros((H, W, 4), dtype=torch.float32, device="cuda"),
+                 torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")) for _ in range(4)]
+        torch.cuda.synchronize()
+        for k, (a, o) in enumerate(bufs):
+            r.render_device(rci_c, a, o, options=rtvk.make_options(), stream=streams[k % 2])
+        torch.cuda.synchronize()
+        for a, o in bufs:
+            assert_same(a.cpu().numpy(), o.cpu().numpy(), ra, ro)
+
+
+def test_render_before_scene_fails(rtvk, torch):
+    with rtvk.Renderer(0) as r:
+        acc = torch.zeros((8, 8, 4), dtype=torch.float32, device="cuda")
+        out = torch.zeros((8, 8, 4), dtype=torch.uint8, device="cuda")
+        with pytest.raises(rtvk.RtError) as e:
+            r.render_device(rtvk.canonical_render_call_info(1, 8, 8), acc, out)
+        assert e.value.code == -4   # RT_ERR_NO_SCENE
+        r.set_scene(np.zeros((0, 80), np.uint8))   # an empty scene is a scene (sky only)
+        r.render_device(rtvk.canonical_render_call_info(1, 8, 8), acc, out)
+        torch.cuda.synchronize()
+
+
+def test_scatter_rows_bounds(rtvk, renderer, torch):
+    """Row maps pointing past the destination are refused by the Python mirror and skipped by the
+    kernel (dst_rows bound), never written out of bounds."""
+    W = 16
+    src_a = torch.ones((3, W, 4), dtype=torch.float32, device="cuda")
+    src_o = torch.full((3, W, 4), 9, dtype=torch.uint8, device="cuda")
+    dst_a = torch.zeros((4, W, 4), dtype=torch.float32, device="cuda")
+    dst_o = torch.zeros((4, W, 4), dtype=torch.uint8, device="cuda")
+    bad = torch.tensor([0, 4, 2], dtype=torch.int32, device="cuda")
+    with pytest.raises(ValueError):
+        renderer.scatter_rows(src_a, src_o, bad, dst_a, dst_o)
+    # straight through the C-ABI: row 4 of a 4-row destination is skipped
+    guard = torch.zeros((5, W, 4), dtype=torch.uint8, device="cuda")   # row 4 = canary
+    from rtvk import abi
+    abi.check(rtvk.load_library().rt_scatter_rows(renderer._ctx, src_a.data_ptr(), src_o.data_ptr(), bad.data_ptr(),
+                                                  3, W, 4, None, guard.data_ptr(), None))
+    torch.cuda.synchronize()
+    g = guard.cpu().numpy()
+    assert (g[0] == 9).all() and (g[2] == 9).all() and (g[1] == 0).all() and (g[3] == 0).all() and (g[4] == 0).all()
+
+
+# ---- BASELINE configs 3 and 5 at their own workloads ------------------------------------------
+def test_config3_full_frame(rtvk, renderer, torch, oracle):
+    """BASELINE config 3 in full: 1920x1080, 10 000 spp, LBVH + persistent threads, the reference
+    stream (~2 s on one MI355X). Four evenly spaced 4x16-pixel blocks are rendered by the oracle at
+    the same 10 000 spp and must match bit for bit; the whole frame must be finite and lit."""
+    W, H, spp = 1920, 1080, 10000
+    sc = oracle.generate_scene()
+    rci = oracle.render_call_info(spp, W, H)
+    a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH)
+    assert st.samples == W * H * spp
+    assert np.isfinite(a).all() and (a[..., 3] == 1.0).all() and o[..., :3].mean() > 40
+    for y in (67, 403, 740, 1013):   # 16 rows x 4 pixels: one oracle thread per row
+        rows = np.arange(y, y + 16, dtype=np.uint32)
+        r = oracle.render_call_info(spp, W, H, (896, 0))
+        ra, ro, _ = oracle.render(sc, r, 4, 16, rows=rows, threads=16)
+        assert_same(a[y:y + 16, 896:900], o[y:y + 16, 896:900], ra, ro)
+
+
+def test_config3_hash_full_frame(rtvk, renderer, torch, oracle):
+    """Config 3's workload in RT_RNG_SAMPLE_HASH mode (the bench's headline stream): two 4x16-pixel
+    blocks against the oracle, bit for bit, and the frame agrees with the reference-stream
+    frame statistically (two independent 10 000-spp estimates of one picture: PSNR >= 40 dB)."""
+    W, H, spp = 1920, 1080, 10000
+    sc = oracle.generate_scene()
+    rci = oracle.render_call_info(spp, W, H)
+    a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH, rng_mode=HASH)
+    assert st.samples == W * H * spp and renderer.launch_info()["chunks"] >= 1
+    for y in (211, 877):
+        r = oracle.render_call_info(spp, W, H, (1200, 0))
+        ra, ro, _ = oracle.render(sc, r, 4, 16, rows=np.arange(y, y + 16, dtype=np.uint32),
+                                  opts=oracle.options(rng_mode=HASH), threads=16)
+        assert_same(a[y:y + 16, 1200:1204], o[y:y + 16, 1200:1204], ra, ro)
+    a_ref, o_ref, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH)
+    mse = np.mean((o[..., :3].astype(np.float64) - o_ref[..., :3]) ** 2)
+    assert 10 * np.log10(255 ** 2 / mse) >= 40.0
+
+
+def test_config5_full_frame(rtvk, renderer, torch, oracle):
+    """BASELINE config 5 on one GPU: 3840x2160, 99 860 spheres (the reference recipe with a
+    316x316 grid), 1 000 spp. The production treelet walk (LDS treelet + L2 subtrees) equals the
+    all-L2 walk bit for bit with the same segment counts, and a 4x16-pixel block at an offset
+    matches the oracle (brute force over all 99 860 spheres) at the full 1 000 spp."""
+    W, H, spp, K = 3840, 2160, 1000, 158
+    sc = oracle.generate_scene(0.0, K)
+    rci = oracle.render_call_info(spp, W, H)
+    a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH, rng_mode=HASH)
+    assert renderer.launch_info()["form"] == "lbvh-treelet"
+    a2, o2, st2 = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH_GLOBAL, rng_mode=HASH)
+    assert_same(a, o, a2, o2)
+    assert (st.segments, st.samples) == (st2.segments, st2.samples) and st.samples == W * H * spp
+    r = oracle.render_call_info(spp, W, H, (1800, 0))
+    ra, ro, _ = oracle.render(sc, r, 4, 16, rows=np.arange(1200, 1216, dtype=np.uint32),
+                              opts=oracle.options(rng_mode=HASH), threads=16)
+    assert_same(a[1200:1216, 1800:1804], o[1200:1216, 1800:1804], ra, ro)

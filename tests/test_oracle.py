@@ -101,7 +101,8 @@ def test_sin_accuracy(oracle):
         assert abs(got - ref) <= 2e-7 + 2e-7 * abs(ref), (x, got, ref)
 
 
-@pytest.mark.parametrize("case", ["g64x36_spp4", "g48x32_spp3_depth3_local", "g40x24_spp2_counter"])
+@pytest.mark.parametrize("case", ["g64x36_spp4", "g48x32_spp3_depth3_local", "g40x24_spp2_counter",
+                                  "g56x40_spp7_hash"])
 def test_golden_fixtures(oracle, case):
     import json
     meta = json.loads((GOLDEN / f"{case}.json").read_text())
@@ -170,3 +171,60 @@ def test_depth_one_is_black_or_direct(oracle):
     acc, out, st = oracle.render(sc, oracle.render_call_info(2, 32, 18), 32, 18, opts=oracle.options(max_depth=1))
     assert st[0] == st[1]
     assert (acc[..., :3] == 0).mean() > 0.9
+
+
+# ---- RT_RNG_SAMPLE_HASH --------------------------------------------------------
+def _lowbias32(pixel_seed: int, s: int) -> int:
+    """Python restatement of the sample-seed hash (golden-ratio spread + lowbias32 finaliser)."""
+    m = 0xFFFFFFFF
+    x = (pixel_seed + 0x9E3779B9 * s) & m
+    x ^= x >> 16
+    x = (x * 0x21F0AAAD) & m
+    x ^= x >> 15
+    x = (x * 0x735A2D97) & m
+    x ^= x >> 15
+    return x
+
+
+def test_sample_seed_hash(oracle):
+    rng = np.random.default_rng(7)
+    for ps, s in [(0, 0), (0xFFFFFFFF, 0xFFFFFFFF), (0xC9A6502E, 1)] + \
+            [tuple(int(v) for v in rng.integers(0, 2**32, 2, dtype=np.uint64)) for _ in range(200)]:
+        assert oracle.sample_seed_hash(ps, s) == _lowbias32(ps, s)
+    # consecutive samples of one pixel start at well-spread LCG states
+    seeds = [_lowbias32(0xC9A6502E, s) for s in range(4096)]
+    assert len(set(seeds)) == 4096
+    bits = np.unpackbits(np.array(seeds, np.uint32).view(np.uint8))
+    assert abs(bits.mean() - 0.5) < 0.01
+
+
+def test_sample_fixed(oracle):
+    """trunc(clamp(c, 0, 1) * 2^44): exact for representable products, NaN -> 0."""
+    rng = np.random.default_rng(3)
+    cs = np.concatenate([rng.uniform(0, 1, 500), 10.0 ** rng.uniform(-40, 0, 500)]).astype(np.float32)
+    for c in cs:
+        assert oracle.sample_fixed(float(c)) == int(np.float32(c) * np.float32(2.0 ** 44))
+    assert oracle.sample_fixed(1.0) == 2 ** 44
+    assert oracle.sample_fixed(0.0) == 0 and oracle.sample_fixed(-0.5) == 0 and oracle.sample_fixed(3.0) == 2 ** 44
+    assert oracle.sample_fixed(float("nan")) == 0
+    assert oracle.sample_fixed(2.0 ** -45) == 0 and oracle.sample_fixed(2.0 ** -44) == 1
+
+
+def test_hash_mode_frame(oracle):
+    """RT_RNG_SAMPLE_HASH frames: the stored sum is float(double(fixed sum) * 2^-44); splitting the
+    samples over two calls (accumulate + sample_base) agrees to float precision; the image is a
+    different Monte-Carlo estimate of the same picture as the reference stream (mean within 2 %)."""
+    sc = oracle.generate_scene()
+    W, H, spp = 48, 27, 16
+    hash_opts = oracle.options(rng_mode=2)
+    a, o, st = oracle.render(sc, oracle.render_call_info(spp, W, H), W, H, opts=hash_opts)
+    a8, _, _ = oracle.render(sc, oracle.render_call_info(8, W, H), W, H, opts=hash_opts)
+    a88, _, _ = oracle.render(sc, oracle.render_call_info(8, W, H), W, H, accum=a8,
+                              opts=oracle.options(rng_mode=2, accumulate=1, sample_base=8))
+    np.testing.assert_allclose(a88[..., :3], a[..., :3], rtol=1e-6, atol=1e-6)
+    assert (a[..., 3] == 1.0).all() and st[1] == W * H * spp
+    ref, ro, _ = oracle.render(sc, oracle.render_call_info(spp, W, H), W, H)
+    assert not np.array_equal(a, ref)
+    assert abs(float(a[..., :3].mean()) / float(ref[..., :3].mean()) - 1.0) < 0.02
+    # rgba8 is the tonemap of the stored sum, as for every mode
+    np.testing.assert_array_equal(o, oracle.resolve(a, spp))
