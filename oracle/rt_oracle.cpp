@@ -250,6 +250,7 @@ inline bool aabb_hit(const rt_vec4& g, V3 o, V3 inv) {
 // A report at exactly tMax is accepted (reportIntersectionEXT), hence '<' against succ(T_MAX).
 Hit closest_hit(const Sphere* sph, uint32_t n, V3 o, V3 d, uint64_t* tests) {
     float a = dot(d, d);
+    float ia = 1.0f / a;
     V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     float best = std::nextafter(T_MAX, std::numeric_limits<float>::infinity());
     int bi = -1;
@@ -262,8 +263,8 @@ Hit closest_hit(const Sphere* sph, uint32_t n, V3 o, V3 d, uint64_t* tests) {
         float D = std::fma(b, b, -(a * c));
         if (D >= 0.0f) {
             float sq = std::sqrt(D);
-            float t1 = (-b - sq) / a;
-            float t2 = (-b + sq) / a;
+            float t1 = (-b - sq) * ia;
+            float t2 = (-b + sq) * ia;
             float t = (t1 >= T_MIN) ? t1 : t2;   // rint:32-39 (t1 > tMax implies t2 > tMax)
             if (t >= T_MIN && t < best && aabb_hit(g, o, inv)) { best = t; bi = int(i); }
         }

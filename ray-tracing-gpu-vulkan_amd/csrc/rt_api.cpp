@@ -150,7 +150,7 @@ constexpr uint32_t kMaxLdsNodes = 0x7fffeu / 8u;
 void size_lds_forms(rt_context* ctx, uint32_t count) {
     const rt::DeviceScene& d = ctx->scene;
     const size_t tree = size_t(2 * d.n_nodes + d.n_leaf + (d.n_leaf + 3) / 4) * 16;
-    const size_t lds1 = tree + size_t(count) * 48u;
+    const size_t lds1 = tree + size_t(count) * 48u + rt::kBigLdsBytes;
     const bool ok = d.n_nodes && d.n_leaf <= kMaxLdsLeafSlots && d.n_nodes <= kMaxLdsNodes;
     ctx->lds1_bytes = (ok && lds1 <= kMaxLdsBytes) ? lds1 : 0;
     const size_t oct = lds1 + size_t(14u) * d.n_nodes * 16u;
@@ -688,9 +688,10 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     } else if (ctx->gpu_tree && d.treelet && d.n_nodes && d.n_leaf < (1u << 26) && form != 10u) {
         // (treelet leaf words carry first_count in 30 bits)
         accel = rt::ACCEL_LBVH_TOP;
-        lds = size_t(rt::kTreeletCap) * 32u;
+        lds = size_t(rt::kTreeletCap) * 32u + rt::kBigLdsBytes;
     } else {
         accel = rt::ACCEL_LBVH_GLOBAL;
+        lds = rt::kBigLdsBytes;
     }
     const bool count = (o.reserved[0] & 1u) != 0;  // internal: count box / sphere tests
     DeviceGuard g(ctx->device);

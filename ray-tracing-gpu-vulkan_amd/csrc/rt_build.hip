@@ -40,7 +40,6 @@ namespace {
 constexpr uint32_t kBlock = 256;
 constexpr uint32_t kPrim = 0x80000000u;   // radix-tree reference: leaf (sorted position)
 constexpr uint32_t kLeafMax = 4;
-constexpr uint32_t kBigMax = 64;
 constexpr uint32_t kEnd = 0xffffffffu;
 constexpr uint32_t kMaxDepth = 128;   // loop bound: the radix tree is at most 59 levels deep
 

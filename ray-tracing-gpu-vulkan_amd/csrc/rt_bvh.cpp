@@ -31,7 +31,6 @@ namespace rt {
 namespace {
 
 constexpr uint32_t kLeafMax = 4;
-constexpr uint32_t kBigMax = 64;
 #ifndef RT_BIG_FACTOR
 #define RT_BIG_FACTOR 2.0f   // "big" = radius above this multiple of the median (A/B knob)
 #endif

@@ -152,6 +152,13 @@ struct TraceParams {
 // so is every product of them) adds trunc(c * 2^44) (rt_kernels.hip sample_fixed); a launch may sum
 // up to 2^19 samples per pixel without overflow.
 constexpr int kFixedFracBits = 44;
+
+// "Big" spheres (radius above a scene-relative threshold, e.g. the ground sphere) are tested by
+// every segment before the tree walk; at most kBigMax of them. The LBVH kernels stage their
+// records (center, radius) and ids in LDS once per block: kBigLdsBytes at the end of the block's
+// dynamic LDS.
+constexpr uint32_t kBigMax = 64;
+constexpr uint32_t kBigLdsBytes = kBigMax * 16u + kBigMax * 4u;
 constexpr uint32_t kHashMaxSpp = 1u << 19;
 
 }  // namespace rt

@@ -76,18 +76,20 @@ __device__ __forceinline__ bool aabb_hit(float cx, float cy, float cz, float r, 
 
 // shader.rint:44-60 + the closest-hit rule for one sphere, spheres visited in index order: a
 // candidate when the quadratic reports t (t1 if t1 >= tmin else t2) in [tmin, best) and the ray
-// overlaps the sphere's AABB.
+// overlaps the sphere's AABB. The roots divide by a through its reciprocal ia = 1/a, computed
+// once per segment (GLSL's division is 2.5-ulp, and AMD's Vulkan compilers emit
+// x * rcp(y) for it too).
 __device__ __forceinline__ void test_sphere(float cx, float cy, float cz, float rr,
                                             const float* __restrict__ radius, V3 o, V3 d, V3 inv,
-                                            float a, uint32_t id, float& best, uint32_t& bi) {
+                                            float a, float ia, uint32_t id, float& best, uint32_t& bi) {
     const float ocx = o.x - cx, ocy = o.y - cy, ocz = o.z - cz;
     const float b = __builtin_fmaf(ocz, d.z, __builtin_fmaf(ocy, d.y, ocx * d.x));
     const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - rr;
     const float D = __builtin_fmaf(b, b, -(a * c));
     if (D >= 0.0f) {
         const float sq = __builtin_sqrtf(D);
-        const float t1 = (-b - sq) / a;
-        const float t2 = (-b + sq) / a;
+        const float t1 = (-b - sq) * ia;
+        const float t2 = (-b + sq) * ia;
         const float t = (t1 >= T_MIN) ? t1 : t2;
         if (t >= T_MIN && t < best && aabb_hit(cx, cy, cz, radius[id], o, inv)) {
             best = t;
@@ -103,7 +105,7 @@ __device__ __forceinline__ void test_sphere(float cx, float cy, float cz, float 
 // of leaves does not matter: the result is the brute-force closest hit.
 template <typename IdOf>
 __device__ __forceinline__ void test4(const float4 s0, const float4 s1, const float4 s2, const float4 s3,
-                                      IdOf id_of, V3 o, V3 d, V3 inv, float a, float& best,
+                                      IdOf id_of, V3 o, V3 d, V3 inv, float a, float ia, float& best,
                                       uint32_t& bi, float& limit, float cull_abs, float cull_rel) {
     float bv[4], Dv[4];
     const float4 sv[4] = {s0, s1, s2, s3};
@@ -124,8 +126,8 @@ __device__ __forceinline__ void test4(const float4 s0, const float4 s1, const fl
         const float b = k == 0 ? bv[0] : k == 1 ? bv[1] : k == 2 ? bv[2] : bv[3];
         const float D = k == 0 ? Dv[0] : k == 1 ? Dv[1] : k == 2 ? Dv[2] : Dv[3];
         const float sq = __builtin_sqrtf(D);
-        float t = (-b - sq) / a;
-        if (!(t >= T_MIN)) t = (-b + sq) / a;     // report t1 if t1 >= tmin, else t2
+        float t = (-b - sq) * ia;
+        if (!(t >= T_MIN)) t = (-b + sq) * ia;     // report t1 if t1 >= tmin, else t2
         if (t >= T_MIN && t <= best) {
             const uint32_t id = id_of(k);
             if (t < best || id < bi) {
@@ -145,7 +147,7 @@ __device__ __forceinline__ void test4(const float4 s0, const float4 s1, const fl
 // before any of the 8 tests, feeding the VALU as SGPR operands (13 VALU per sphere, no VGPR
 // loads, no LDS). The host pads geom to a multiple of 8 with spheres that can never report.
 __device__ __forceinline__ void closest_brute(const rt::TraceParams& P, V3 o, V3 d, V3 inv, float a,
-                                              float& best, uint32_t& bi) {
+                                              float ia, float& best, uint32_t& bi) {
     // Constant address space: wave-uniform loads through it are emitted as s_load (the 32
     // floats of one batch merge into two s_load_dwordx16).
     typedef const __attribute__((address_space(4))) float* ConstF;
@@ -157,7 +159,7 @@ __device__ __forceinline__ void closest_brute(const rt::TraceParams& P, V3 o, V3
         for (uint32_t k = 0; k < 32; ++k) b[k] = g[ib * 32u + k];
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k)
-            test_sphere(b[4 * k], b[4 * k + 1], b[4 * k + 2], b[4 * k + 3], P.radius, o, d, inv, a,
+            test_sphere(b[4 * k], b[4 * k + 1], b[4 * k + 2], b[4 * k + 3], P.radius, o, d, inv, a, ia,
                         ib * 8u + k, best, bi);
     }
 }
@@ -536,7 +538,10 @@ __device__ __forceinline__ void record_tile_cost(const rt::TraceParams& P, const
 #define RT_TRACE_WAVES_PER_SIMD 4
 #endif
 constexpr uint32_t kBruteBlock = 256;
-constexpr uint32_t kTraceBlock = 1024;   // one block per CU shares one staged tree / treelet
+#ifndef RT_TRACE_BLOCK
+#define RT_TRACE_BLOCK 1024
+#endif
+constexpr uint32_t kTraceBlock = RT_TRACE_BLOCK;   // one block per CU shares one staged tree / treelet
 
 // ---------------------------------------------------------------------------------------------
 // Brute-force kernel: one segment per loop iteration for every lane (the sphere loop is
@@ -565,7 +570,8 @@ __global__ __launch_bounds__(kBruteBlock, RT_BRUTE_WAVES_PER_SIMD) void rt_trace
             float best = T_MAX_SUCC;
             uint32_t bi = 0xffffffffu;
             const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-            closest_brute(P, o, d, inv, dot(d, d), best, bi);
+            const float a = dot(d, d);
+            closest_brute(P, o, d, inv, a, 1.0f / a, best, bi);
             if (COUNT) n_sph += P.n_spheres;
             n_seg++;
             ps.segs++;
@@ -590,7 +596,7 @@ __global__ __launch_bounds__(kBruteBlock, RT_BRUTE_WAVES_PER_SIMD) void rt_trace
 // ---------------------------------------------------------------------------------------------
 struct Ray {
     V3 o, d, inv;          // origin, direction, 1/d (the AABB gate's own reciprocals)
-    float a;               // dot(d, d)
+    float a, ia;           // dot(d, d) and its reciprocal
     float limit;           // node cull limit: min(best + cull_abs + cull_rel * best, tmax)
     float best;
     uint32_t bi;           // closest so far
@@ -654,33 +660,38 @@ __device__ __forceinline__ uint32_t octant(const V3 d) {
     return (__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 31) << 1) | ((__float_as_uint(d.z) >> 31) << 2);
 }
 
+// Big-sphere table of a block (LDS, rt_internal.h kBigLdsBytes): records {cx, cy, cz, r} and ids,
+// n_big rounded up to a multiple of 4 by repeating the last one (a duplicate of an already tested
+// sphere can never change (best, bi)). Staged once per block, read by every segment with a
+// wave-uniform address (LDS broadcast): one round trip instead of the dependent id -> record ->
+// radius scalar loads per segment.
+struct BigTable { const float4* rec; const uint32_t* id; };
+
+__device__ __forceinline__ BigTable stage_big(const rt::TraceParams& P, float4* lds_at, uint32_t tid, uint32_t nthr) {
+    const uint32_t nb4 = (P.n_big + 3u) & ~3u;
+    uint32_t* ids = reinterpret_cast<uint32_t*>(lds_at + rt::kBigMax);
+    for (uint32_t i = tid; i < nb4; i += nthr) {
+        const uint32_t id = P.big_ids[min(i, P.n_big - 1u)];
+        const rt::GeomRec g = P.geom[id];
+        lds_at[i] = make_float4(g.cx, g.cy, g.cz, P.radius[id]);
+        ids[i] = id;
+    }
+    return BigTable{lds_at, ids};
+}
+
 // New segment: hoisted per-ray terms and the exhaustive big spheres.
-__device__ __forceinline__ void setup_ray(const rt::TraceParams& P, Ray& r, uint32_t& n_sph) {
+__device__ __forceinline__ void setup_ray(const rt::TraceParams& P, const BigTable& big, Ray& r, uint32_t& n_sph) {
     r.a = dot(r.d, r.d);
+    r.ia = 1.0f / r.a;
     r.inv = v3(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
     r.best = T_MAX_SUCC;
     r.bi = 0xffffffffu;
-    typedef const __attribute__((address_space(4))) uint32_t* ConstU;
-    typedef const __attribute__((address_space(4))) float* ConstF;
-    const ConstU ids = (ConstU)(P.big_ids);
-    const ConstF g = (ConstF)(P.geom);
-    const ConstF rad = (ConstF)(P.radius);
-    for (uint32_t k0 = 0; k0 < P.n_big; k0 += 4) {   // wave-uniform: scalar loads, 4 at a time
-        uint32_t id[4];
-        float sp[16], rs[4];
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) id[j] = ids[min(k0 + j, P.n_big - 1)];
-#pragma unroll
-        for (uint32_t j = 0; j < 16; ++j) sp[j] = g[4 * id[j >> 2] + (j & 3)];
-#pragma unroll
-        for (uint32_t j = 0; j < 4; ++j) rs[j] = rad[id[j]];
-        // records of absent batch members (k0 + j >= n_big) repeat the last big sphere: a
-        // duplicate of an already tested sphere can never change (best, bi).
-        const float4 b0 = make_float4(sp[0], sp[1], sp[2], rs[0]), b1 = make_float4(sp[4], sp[5], sp[6], rs[1]);
-        const float4 b2 = make_float4(sp[8], sp[9], sp[10], rs[2]), b3 = make_float4(sp[12], sp[13], sp[14], rs[3]);
+    for (uint32_t k0 = 0; k0 < P.n_big; k0 += 4) {   // wave-uniform: LDS broadcast reads
+        const float4 b0 = big.rec[k0], b1 = big.rec[k0 + 1], b2 = big.rec[k0 + 2], b3 = big.rec[k0 + 3];
+        const uint4 id = *reinterpret_cast<const uint4*>(big.id + k0);
         float unused_limit = 0.0f;
-        test4(b0, b1, b2, b3, [&](uint32_t k) { return k == 0 ? id[0] : k == 1 ? id[1] : k == 2 ? id[2] : id[3]; },
-              r.o, r.d, r.inv, r.a, r.best, r.bi, unused_limit, 0.0f, 0.0f);
+        test4(b0, b1, b2, b3, [&](uint32_t k) { return k == 0 ? id.x : k == 1 ? id.y : k == 2 ? id.z : id.w; },
+              r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, unused_limit, 0.0f, 0.0f);
     }
     n_sph += P.n_big;
     r.limit = fminf(__builtin_fmaf(r.best, P.cull_rel, r.best + P.cull_abs), 10000.0f);
@@ -693,7 +704,7 @@ __device__ __forceinline__ void leaf_test(const rt::TraceParams& P, const float4
                                           const uint32_t* __restrict__ leaf_ids, uint32_t first,
                                           uint32_t count, Ray& r, uint32_t& n_sph) {
     const float4 s0 = leaf4[first], s1 = leaf4[first + 1], s2 = leaf4[first + 2], s3 = leaf4[first + 3];
-    test4(s0, s1, s2, s3, [&](uint32_t k) { return leaf_ids[first + k]; }, r.o, r.d, r.inv, r.a, r.best,
+    test4(s0, s1, s2, s3, [&](uint32_t k) { return leaf_ids[first + k]; }, r.o, r.d, r.inv, r.a, r.ia, r.best,
           r.bi, r.limit, P.cull_abs, P.cull_rel);
     if (COUNT) n_sph += count;
 }
@@ -780,6 +791,22 @@ __device__ __forceinline__ void walk(const rt::TraceParams& P, const float4* __r
         const uint32_t nbase = uint32_t(reinterpret_cast<uintptr_t>((LdsF4)nodes4));   // LDS address of node 0
         uint32_t ni = r.walk ? nbase + (LAYOUT == LAYOUT_OCT ? octant(r.d) * P.n_nodes * 32u : 0u) : END;
         for (;;) {
+#ifdef RT_AB_WALK2   // A/B only: the hit successor (next node in memory) is loaded with the node and
+                     // tested in the same iteration when the node is an inner node that is hit
+            while (int32_t(ni) >= 0) {
+                const float4 A = lds_f4(ni);
+                const float4 B = lds_f4(ni + 16u);
+                const float4 C = lds_f4(ni + 32u);
+                const float4 D = lds_f4(ni + 48u);
+                if (COUNT) n_box++;
+                const bool hit = node_hit<LAYOUT == LAYOUT_OCT ? 8u : 1u>(A, B, q, r.limit);
+                const uint32_t nx = __float_as_uint(hit ? B.w : B.z);
+                const bool inner = hit && int32_t(nx) >= 0;
+                const bool hit2 = node_hit<LAYOUT == LAYOUT_OCT ? 8u : 1u>(C, D, q, r.limit);
+                if (COUNT && inner) n_box++;
+                ni = inner ? __float_as_uint(hit2 ? D.w : D.z) : nx;
+            }
+#else
             while (int32_t(ni) >= 0) {
                 const float4 A = lds_f4(ni);         // links are LDS addresses:
                 const float4 B = lds_f4(ni + 16u);   // no address arithmetic per visit
@@ -787,6 +814,7 @@ __device__ __forceinline__ void walk(const rt::TraceParams& P, const float4* __r
                 const bool hit = node_hit<LAYOUT == LAYOUT_OCT ? 8u : 1u>(A, B, q, r.limit);
                 ni = __float_as_uint(hit ? B.w : B.z);
             }
+#endif
             const bool at_leaf = ni != END;
             if (!__ballot(at_leaf)) break;   // no lane stopped at a leaf: all walks done
             if (at_leaf) {
@@ -807,7 +835,8 @@ template <bool COUNT, int LAYOUT, int MODE>
 __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4* __restrict__ nodes4,
                                           const float4* __restrict__ leaf4,
                                           const uint32_t* __restrict__ leaf_ids,
-                                          const float4* __restrict__ geom4, const float4* __restrict__ mat4) {
+                                          const float4* __restrict__ geom4, const float4* __restrict__ mat4,
+                                          const BigTable big) {
     const uint32_t lane = lane_id();
     const Camera cam = load_camera(P);
     uint32_t st = ST_NEED_UNIT;
@@ -844,7 +873,7 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
         if (COUNT && lane == 0) atomicAdd(&P.counters->lane_hist[__popcll(tracing)], 1ull);
         STAMP(1);
         const uint32_t box0 = n_box;
-        if (st == ST_TRACING) setup_ray(P, r, n_sph);
+        if (st == ST_TRACING) setup_ray(P, big, r, n_sph);
         STAMP(2);
         if (st == ST_TRACING) walk<COUNT, LAYOUT>(P, nodes4, leaf4, leaf_ids, r, n_box, n_sph);
         if (COUNT && st == ST_TRACING) {   // walk-length histogram (diagnostic, COUNT builds only)
@@ -888,17 +917,20 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
 // LBVH kernel, tree in global memory (A/B reference: every node and leaf from L2).
 template <bool COUNT, int MODE>
 __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace_global_kernel(const rt::TraceParams P) {
+    extern __shared__ float4 lds[];   // the big-sphere table only
+    const BigTable big = stage_big(P, lds, threadIdx.x, kTraceBlock);
+    __syncthreads();
     lbvh_loop<COUNT, LAYOUT_GLOBAL, MODE>(P, reinterpret_cast<const float4*>(P.nodes),
                                           reinterpret_cast<const float4*>(P.leaf_geom), P.leaf_ids,
                                           reinterpret_cast<const float4*>(P.geom),
-                                          reinterpret_cast<const float4*>(P.mat));
+                                          reinterpret_cast<const float4*>(P.mat), big);
 }
 
 // LBVH kernel with the whole tree and the per-sphere geometry + material records read by shading
 // staged in LDS, once per persistent block (one 1024-thread block per CU). Staged nodes use the
 // AB layout (node_hit); NOCT = 8 stages one copy per ray direction octant, each in its own
 // near-child-first order when the host provides one (nodes_oct). LDS: [nodes | leaf spheres |
-// leaf ids | geometry | materials].
+// leaf ids | geometry | materials | big-sphere table].
 template <bool COUNT, uint32_t NOCT, int MODE>
 __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace_lds_kernel(const rt::TraceParams P) {
     extern __shared__ float4 lds[];
@@ -944,10 +976,11 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
     const float4* mat4 = reinterpret_cast<const float4*>(P.mat);
     for (uint32_t i = threadIdx.x; i < ng; i += kTraceBlock) lds[base + i] = geom4[i];
     for (uint32_t i = threadIdx.x; i < nm; i += kTraceBlock) lds[base + ng + i] = mat4[i];
+    const BigTable big = stage_big(P, lds + base + ng + nm, threadIdx.x, kTraceBlock);
     __syncthreads();
     lbvh_loop<COUNT, NOCT == 8 ? LAYOUT_OCT : LAYOUT_LDS1, MODE>(
         P, lds, lds + n_node4, reinterpret_cast<const uint32_t*>(lds + n_node4 + n_leaf4), lds + base,
-        lds + base + ng);
+        lds + base + ng, big);
 }
 
 // LBVH kernel for trees too big for LDS: the treelet (rt_build.hip build_treelet) is staged in LDS
@@ -967,10 +1000,11 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
         lds[2 * i + 1] = make_float4(B.x, B.y, __uint_as_float(miss == END ? END : lbase + miss * 32u),
                                      __uint_as_float(int32_t(hit) >= 0 ? lbase + hit * 32u : hit));
     }
+    const BigTable big = stage_big(P, lds + 2u * rt::kTreeletCap, threadIdx.x, kTraceBlock);
     __syncthreads();
     lbvh_loop<COUNT, LAYOUT_TOP, MODE>(P, lds, reinterpret_cast<const float4*>(P.leaf_geom), P.leaf_ids,
                                        reinterpret_cast<const float4*>(P.geom),
-                                       reinterpret_cast<const float4*>(P.mat));
+                                       reinterpret_cast<const float4*>(P.mat), big);
 }
 
 // HASH-mode resolve (shader.rgen:53-66 for the chunked frame): per texel, the fixed-point sum of
