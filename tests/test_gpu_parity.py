@@ -781,3 +781,33 @@ def test_config5_full_frame(rtvk, renderer, torch, oracle):
     ra, ro, _ = oracle.render(sc, r, 4, 16, rows=np.arange(1200, 1216, dtype=np.uint32),
                               opts=oracle.options(rng_mode=HASH), threads=16)
     assert_same(a[1200:1216, 1800:1804], o[1200:1216, 1800:1804], ra, ro)
+
+
+def test_reference_image_qualitative(rtvk, torch):
+    """Qualitative pin against the reference's only rendered output (sceneRender.png, README.md:3;
+    statistics in tests/golden/sceneRender_stats.npz). That image is not a pixel oracle: its scene
+    layout differs from the generator's (no camera or scene time reproduces it, thumbnail PSNR
+    <= 17 dB over a sweep), and its spp is unknown. The upstream view (shader.rgen:29, camera
+    (13, 2, -3) -> origin) rendered at 1920x1080 must still agree in what the shading decides:
+    the sky blocks exactly, per-channel means within 6 %, per-channel 32-bin histograms within
+    L1 0.3 (measured: 1.4 / 3.5 / 4.1 % and 0.21 / 0.21 / 0.23)."""
+    import sys
+    sys.path.insert(0, str(GOLDEN))
+    from make_scene_render_ref import stats
+    W, H = 1920, 1080
+    rci = rtvk.canonical_render_call_info(256, W, H)
+    rci.camera_pos.x, rci.camera_pos.y, rci.camera_pos.z = 13.0, 2.0, -3.0
+    rci.camera_dir.x, rci.camera_dir.y, rci.camera_dir.z = -13.0, -2.0, 3.0
+    with rtvk.Renderer(0) as r:
+        r.set_scene(rtvk.generateRandomScene())
+        acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+        r.render_device(rci, acc, out, options=rtvk.make_options(rng_mode=HASH))
+        torch.cuda.synchronize()
+    ours = stats(out.cpu().numpy()[..., :3])
+    ref = np.load(GOLDEN / "sceneRender_stats.npz", allow_pickle=False)
+    np.testing.assert_allclose(np.median(ours["thumb"][:3].reshape(-1, 3), axis=0),
+                               np.median(ref["thumb"][:3].reshape(-1, 3), axis=0), atol=0.5)
+    m_ours, m_ref = ours["thumb"].mean(axis=(0, 1)), ref["thumb"].mean(axis=(0, 1))
+    assert (np.abs(m_ours / m_ref - 1) < 0.06).all(), (m_ours, m_ref)
+    assert (np.abs(ours["hist"] - ref["hist"]).sum(axis=1) < 0.3).all()

@@ -228,3 +228,16 @@ def test_hash_mode_frame(oracle):
     assert abs(float(a[..., :3].mean()) / float(ref[..., :3].mean()) - 1.0) < 0.02
     # rgba8 is the tonemap of the stored sum, as for every mode
     np.testing.assert_array_equal(o, oracle.resolve(a, spp))
+
+
+def test_sky_matches_reference_render(oracle):
+    """The reference's own rendered output (/root/reference/sceneRender.png, via the fixture
+    tests/golden/sceneRender_stats.npz made by tests/golden/make_scene_render_ref.py): its sky
+    blocks (40x40-pixel means, top three rows, median) equal the oracle's sky pixel, i.e. the
+    constant sky of shader.rmiss:15 through the tonemap of shader.rgen:65-66 and the UNORM store."""
+    ref = np.load(GOLDEN / "sceneRender_stats.npz", allow_pickle=False)
+    sky_ref = np.median(ref["thumb"][:3].reshape(-1, 3), axis=0)
+    _, out, _ = oracle.render(np.zeros((0, 80), np.uint8), oracle.render_call_info(4, 8, 8), 8, 8)
+    sky_ours = out[0, 0, :3].astype(np.float32)
+    assert sky_ours.tolist() == [213.0, 228.0, 255.0]
+    np.testing.assert_allclose(sky_ref, sky_ours, atol=0.5)
