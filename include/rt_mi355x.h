@@ -218,7 +218,7 @@ int rt_store_ppm(const char* path, const uint8_t* rgba8, uint32_t width, uint32_
 /* Diagnostic (tests only): evaluates one arithmetic-contract primitive on `device` for n
  * (x, y) pairs: op 0 sqrt(x), 1 x/y, 2 sin(x), 3 fma(x,y,1), 4 normalize(x,y,0.5).x, 5 pow(x,5),
  * 6 sample_seed_hash(bits(x), bits(y)) as bits, 7 / 8 low / high word of the 20.44 fixed-point
- * value of colour x, as bits. */
+ * value of colour x, as bits, 9 checker decision at (x, y, 0.5 (x - y)) as 1 / 0. */
 int rt_debug_math(int device, int op, const float* in_pairs, float* out, uint32_t n);
 /* Diagnostic: of ctx's last launch, {sample chunks per pixel, staged kernel form of the scene
  * (rt_internal.h ACCEL_*), its LDS bytes, CU count}. */

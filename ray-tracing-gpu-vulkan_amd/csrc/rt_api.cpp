@@ -450,12 +450,8 @@ int set_scene_host(rt_context* ctx, const Sphere* spheres, uint32_t count, hipSt
             const float r = s.geometry.w;
             geom[i] = rt::GeomRec{s.geometry.x, s.geometry.y, s.geometry.z, r * r};
             radius[i] = r;
-            rt::MatRec m;
-            m.c0x = s.colors[0].x; m.c0y = s.colors[0].y; m.c0z = s.colors[0].z;
-            m.attr = s.materialSpecificAttribute;
-            m.c1x = s.colors[1].x; m.c1y = s.colors[1].y; m.c1z = s.colors[1].z;
-            m.type_tex = (s.materialType & 0xffu) | ((s.textureType & 0xffu) << 8);
-            mat[i] = m;
+            mat[i] = rt::make_mat(s.colors[0].x, s.colors[0].y, s.colors[0].z, s.materialSpecificAttribute,
+                                  s.colors[1].x, s.colors[1].y, s.colors[1].z, s.materialType, s.textureType);
         }
         // Brute-force padding: whole batches of 8; the pad spheres sit 1e19 away with
         // radius^2 = -1e38, so D = b^2 - a(|oc|^2 + 1e38) < 0 for every ray.

@@ -80,12 +80,8 @@ __global__ void __launch_bounds__(kBlock) k_prep(const Sphere* __restrict__ sph,
         const float x = s.geometry.x, y = s.geometry.y, z = s.geometry.z, r = s.geometry.w;
         geom[i] = GeomRec{x, y, z, r * r};
         radius[i] = r;
-        MatRec m;
-        m.c0x = s.colors[0].x; m.c0y = s.colors[0].y; m.c0z = s.colors[0].z;
-        m.attr = s.materialSpecificAttribute;
-        m.c1x = s.colors[1].x; m.c1y = s.colors[1].y; m.c1z = s.colors[1].z;
-        m.type_tex = (s.materialType & 0xffu) | ((s.textureType & 0xffu) << 8);
-        mat[i] = m;
+        mat[i] = make_mat(s.colors[0].x, s.colors[0].y, s.colors[0].z, s.materialSpecificAttribute,
+                          s.colors[1].x, s.colors[1].y, s.colors[1].z, s.materialType, s.textureType);
         if (rkeys) { rkeys[i] = r; ids[i] = i; }
         Ro = f2o(__builtin_sqrtf(x * x + y * y + z * z) + __builtin_fabsf(r));
     } else if (i < n_geom) {   // brute-force pad record: never hit (rt_api.cpp)

@@ -92,6 +92,30 @@ __device__ __forceinline__ float sinf_det(float x) {
     return (q & 2) ? -v : v;
 }
 
+// Sign class of sinf_det(x): 0 when the value is +-0 (or x is NaN), else +1 / -1. Same reduction as
+// sinf_det; for |r| <= pi/4 (+ rounding) the sine polynomial keeps the sign of r and is zero only
+// for r = 0, and the cosine polynomial is > 0.7, so the polynomials need not be evaluated.
+__device__ __forceinline__ int sin_sign(float x) {
+    float k = __builtin_rintf(x * 0.636619772f);
+    float r = __builtin_fmaf(-k, 1.5707962513e+00f, x);
+    r = __builtin_fmaf(-k, 7.5497894159e-08f, r);
+    r = __builtin_fmaf(-k, 5.3903029534e-15f, r);
+    const int q = int(k) & 3;
+    if (!(q & 1) && !(__builtin_fabsf(r) > 0.0f)) return 0;   // +-0 (or NaN): the product is not > 0
+    const bool neg = (!(q & 1) && __builtin_signbit(r)) != bool(q & 2);
+    return neg ? -1 : 1;
+}
+
+// shader.rchit:58-60 checker decision, sin(6x) * sin(6y) * sin(6z) > 0, from the signs of the three
+// sines: a product of three nonzero finite binary32 values of magnitude >= 1e-15 (hit points are
+// fma results of O(1) operands) neither underflows nor changes sign in rounding, so
+// it is > 0 exactly when no factor is zero and an even number is negative. Bit-identical decision
+// to the oracle's full product (tests: every ground hit of the GPU parity suite).
+__device__ __forceinline__ bool checker_positive(float x, float y, float z) {
+    const int a = sin_sign(6.0f * x), b = sin_sign(6.0f * y), c = sin_sign(6.0f * z);
+    return a * b * c > 0;
+}
+
 // pow(x, 5.0) with GLSL's undefined negative base mapped to NaN.
 __device__ __forceinline__ float pow5(float x) {
     float x2 = x * x;

@@ -16,9 +16,34 @@ struct alignas(16) GeomRec {
 // reference's 80-B std140 Sphere, so one hit costs two 16-B loads.
 struct alignas(16) MatRec {
     float c0x, c0y, c0z, attr;   // colors[0].rgb, materialSpecificAttribute
-    float c1x, c1y, c1z;         // colors[1].rgb (checker)
-    uint32_t type_tex;           // materialType | textureType << 8
+    float c1x, c1y, c1z;         // colors[1].rgb (checker); solid dielectrics: kMatDielConst
+    uint32_t type_tex;           // materialType | textureType << 8 | flags
 };
+// Solid dielectric (colors[1] unused): c1 = {1 / attr, r0(front), r0(back)}, the per-sphere
+// constants of shader.rchit:94 and :131 (eta = 1/ior on a front face, ior on a back face;
+// r0 = ((1 - eta) / (1 + eta))^2, Q7), computed with the kernel's own binary32 operations.
+constexpr uint32_t kMatDielConst = 1u << 16;
+
+// Fills a material record (host and device builds alike).
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline MatRec make_mat(float c0x, float c0y, float c0z, float attr, float c1x, float c1y, float c1z,
+                       uint32_t mtype, uint32_t ttype) {
+    MatRec m;
+    m.c0x = c0x; m.c0y = c0y; m.c0z = c0z; m.attr = attr;
+    m.c1x = c1x; m.c1y = c1y; m.c1z = c1z;
+    m.type_tex = (mtype & 0xffu) | ((ttype & 0xffu) << 8);
+    if (mtype == 2u && ttype != 1u) {
+        const float ef = 1.0f / attr, eb = attr;
+        const float qf = (1.0f - ef) / (1.0f + ef), qb = (1.0f - eb) / (1.0f + eb);
+        m.c1x = ef;
+        m.c1y = qf * qf;
+        m.c1z = qb * qb;
+        m.type_tex |= kMatDielConst;
+    }
+    return m;
+}
 
 // LBVH node, 32 B. Stackless "escape-link" layout: nodes are stored in depth-first order, so a
 // hit on an inner node continues at index+1 and a miss (or a finished leaf) jumps to `escape`.

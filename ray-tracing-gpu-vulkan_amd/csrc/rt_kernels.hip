@@ -459,16 +459,13 @@ __device__ __forceinline__ bool shade(const rt::TraceParams& P, const float4* __
         const float4 m0 = mat4[2 * bi];
         const float4 m1 = mat4[2 * bi + 1];
         const uint32_t tt = __float_as_uint(m1.w);
-        const uint32_t mtype = tt & 0xffu, ttype = tt >> 8;
+        const uint32_t mtype = tt & 0xffu, ttype = (tt >> 8) & 0xffu;
         const V3 outward = normalize(sub(p, v3(gc4.x, gc4.y, gc4.z)));
         const bool front = dot(d, outward) < 0.0f;
         const V3 n = front ? outward : neg(outward);
         // shader.rchit:53-64
         att = v3(m0.x, m0.y, m0.z);
-        if (ttype == 1u) {
-            const float sines = sinf_det(6.0f * p.x) * sinf_det(6.0f * p.y) * sinf_det(6.0f * p.z);
-            if (!(sines > 0.0f)) att = v3(m1.x, m1.y, m1.z);
-        }
+        if (ttype == 1u && !checker_positive(p.x, p.y, p.z)) att = v3(m1.x, m1.y, m1.z);
         // diffuse and metal both draw one random unit vector first (shader.rchit:69, :80): one
         // copy of that code serves a wave holding both materials
         V3 ru = v3(0.0f, 0.0f, 0.0f);
@@ -482,12 +479,20 @@ __device__ __forceinline__ bool shade(const rt::TraceParams& P, const float4* __
             const V3 sc = normalize(add(refl, fuzz));
             if (dot(sc, n) > 0.0f) sd = sc;
         } else if (mtype == 2u) {                // dielectric, shader.rchit:91-100,125-133
-            const float eta = front ? (1.0f / m0.w) : m0.w;
+            // eta and r0 = ((1 - eta) / (1 + eta))^2 per face: from the record (solid dielectrics,
+            // rt_internal.h make_mat) or computed here (checkered ones: colors[1] is taken)
+            float eta, r;
+            if (tt & rt::kMatDielConst) {
+                eta = front ? m1.x : m0.w;
+                r = front ? m1.y : m1.z;
+            } else {
+                eta = front ? (1.0f / m0.w) : m0.w;
+                const float q = (1.0f - eta) / (1.0f + eta);
+                r = q * q;
+            }
             const float cos_t = dot(neg(d), n);
             bool refracts = false;
             if (eta * __builtin_sqrtf(1.0f - cos_t * cos_t) <= 1.0f) {
-                const float q = (1.0f - eta) / (1.0f + eta);
-                const float r = q * q;
                 const float refl = r + (1.0f - r) * pow5(1.0f - cos_t);
                 refracts = refl < rnd(ps.seed);
             }
@@ -1076,6 +1081,7 @@ __global__ void rt_debug_math_kernel(int op, const float* __restrict__ in, float
         case 6: r = __uint_as_float(sample_seed_hash(__float_as_uint(x), __float_as_uint(y))); break;
         case 7: { const unsigned long long q = sample_fixed(x); r = __uint_as_float(uint32_t(q)); break; }
         case 8: { const unsigned long long q = sample_fixed(x); r = __uint_as_float(uint32_t(q >> 32)); break; }
+        case 9: r = checker_positive(x, y, 0.5f * (x - y)) ? 1.0f : 0.0f; break;
         default: r = 0.0f;
     }
     out[i] = r;

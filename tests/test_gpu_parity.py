@@ -153,6 +153,25 @@ def _debug_math(rtvk, op, x, y):
     return out
 
 
+def test_checker_decision_bit_exact(rtvk, torch, oracle):
+    """The kernel decides the checker (shader.rchit:58-60) from the signs of the three sines; the
+    oracle multiplies the full sines. Same decision on 60 000 points: uniform, near the zeros of
+    sin(6x) (multiples of pi/6), tiny, signed zeros, far (|x| up to 1e4)."""
+    rng = np.random.default_rng(21)
+    n = 20000
+    x = np.concatenate([rng.uniform(-30, 30, n), (rng.integers(-600, 600, n) * np.pi / 6).astype(np.float32)
+                        + rng.normal(0, 1e-6, n), rng.uniform(-1e4, 1e4, n)]).astype(np.float32)
+    y = np.concatenate([rng.uniform(-1e-5, 1e-5, n), rng.uniform(-3, 3, n), rng.uniform(-1e4, 1e4, n)]).astype(np.float32)
+    x[:6] = [0.0, -0.0, 1e-30, -1e-30, np.pi / 6, 0.0]
+    y[:6] = [1.0, 1.0, 0.0, -0.0, 1e-38, -0.0]
+    z = (np.float32(0.5) * (x - y)).astype(np.float32)
+    got = _debug_math(rtvk, 9, x, y)
+    # the oracle's product in binary32, left to right, as rt_oracle.cpp texture_color computes it
+    ref = np.array([np.float32(np.float32(oracle.sinf(float(np.float32(6) * a))) * np.float32(oracle.sinf(float(np.float32(6) * b))))
+                    * np.float32(oracle.sinf(float(np.float32(6) * c))) for a, b, c in zip(x, y, z)], np.float32)
+    np.testing.assert_array_equal(got, (ref > 0).astype(np.float32))
+
+
 def test_hash_primitives_bit_exact(rtvk, torch, oracle):
     """RT_RNG_SAMPLE_HASH primitives: the sample-seed hash (bit patterns) and the 20.44 fixed-point
     conversion of a colour channel (low / high words), device vs oracle."""
@@ -811,3 +830,27 @@ def test_reference_image_qualitative(rtvk, torch):
     m_ours, m_ref = ours["thumb"].mean(axis=(0, 1)), ref["thumb"].mean(axis=(0, 1))
     assert (np.abs(m_ours / m_ref - 1) < 0.06).all(), (m_ours, m_ref)
     assert (np.abs(ours["hist"] - ref["hist"]).sum(axis=1) < 0.3).all()
+
+
+@pytest.mark.parametrize("accel", [BRUTE, LBVH])
+def test_checkered_dielectric_and_odd_materials(rtvk, renderer, torch, oracle, accel):
+    """Material records outside the generator's recipe: a checkered dielectric (its colors[1] is
+    the checker's, so the kernel computes eta and r0 itself instead of reading the record's
+    precomputed constants), a fuzzy metal, a diffuse sphere with the checker, an unknown material
+    id (no scatter: its colour is light), all against the oracle in both random stream modes."""
+    sc = oracle.generate_scene()
+    recs = sc.copy()
+    f, u = recs.view(np.float32).reshape(-1, 20), recs.view(np.uint32).reshape(-1, 20)
+    u[3, 5] = 1                                     # big glass sphere: checkered
+    f[3, 12:16] = [0.9, 0.2, 0.3, 1.0]              # its colors[1]
+    u[2, 4], f[2, 16] = 1, 0.35                     # big metal: fuzz 0.35 (scene.h leaves 0)
+    u[1, 5] = 1                                     # big diffuse sphere: checkered
+    f[1, 12:16] = [0.1, 0.8, 0.2, 1.0]
+    u[10, 4] = 7                                    # unknown material id
+    W, H = 96, 54
+    rci = oracle.render_call_info(3, W, H)
+    for mode in (STREAM, HASH):
+        ra, ro, rs = oracle.render(recs, rci, W, H, opts=oracle.options(rng_mode=mode))
+        a, o, st = gpu_render(rtvk, renderer, torch, recs, rci, W, H, accel=accel, rng_mode=mode)
+        assert_same(a, o, ra, ro)
+        assert (st.segments, st.samples) == rs[:2]
