@@ -54,8 +54,8 @@ struct rt_context {
     // occupancy cache per kernel form, count flag and rng mode, valid for occ_lds bytes
     int occ[rt::ACCEL_COUNT][2][2] = {};
     size_t occ_lds[rt::ACCEL_COUNT][2][2] = {};
-    size_t lds1_bytes = 0;                       // one node copy + leaves + scene records (0: no fit)
-    size_t oct_bytes = 0;                        // 8 octant node copies + leaves + scene records (0: no fit)
+    size_t lds1_bytes = 0;                       // one node copy + leaves + big table (0: no fit)
+    size_t oct_bytes = 0;                        // 8 octant node copies + leaves + big table (0: no fit)
     // unpadded LBVH node boxes (host) and the radius the device copy is padded for
     std::vector<rt::BvhNode> nodes_host;
     float scene_radius = 0.0f;
@@ -147,10 +147,10 @@ constexpr size_t kMaxLdsBytes = 156 * 1024;
 constexpr uint32_t kMaxLdsLeafSlots = 4096;
 constexpr uint32_t kMaxLdsNodes = 0x7fffeu / 8u;
 
-void size_lds_forms(rt_context* ctx, uint32_t count) {
+void size_lds_forms(rt_context* ctx) {
     const rt::DeviceScene& d = ctx->scene;
     const size_t tree = size_t(2 * d.n_nodes + d.n_leaf + (d.n_leaf + 3) / 4) * 16;
-    const size_t lds1 = tree + size_t(count) * 48u + rt::kBigLdsBytes;
+    const size_t lds1 = tree + rt::kBigLdsBytes;   // shading records stay in HBM (rt_kernels.hip)
     const bool ok = d.n_nodes && d.n_leaf <= kMaxLdsLeafSlots && d.n_nodes <= kMaxLdsNodes;
     ctx->lds1_bytes = (ok && lds1 <= kMaxLdsBytes) ? lds1 : 0;
     const size_t oct = lds1 + size_t(14u) * d.n_nodes * 16u;
@@ -484,7 +484,7 @@ int set_scene_host(rt_context* ctx, const Sphere* spheres, uint32_t count, hipSt
         std::vector<rt::BvhNode> oct;
         make_octant_orders(bvh.nodes, oct);
         up.add(oct, &d.nodes_oct);
-        size_lds_forms(ctx, count);
+        size_lds_forms(ctx);
         up.add(bvh.nodes, &d.nodes);
         up.add(bvh.leaf_geom, &d.leaf_geom);
         up.add(bvh.leaf_ids, &d.leaf_ids);
@@ -539,7 +539,7 @@ int set_scene_gpu(rt_context* ctx, const Sphere* d_sph, uint32_t count, hipStrea
     ctx->pad_radius = ctx->scene_radius * 1.01f + 100.0f;   // the build padded for this radius
     ctx->padded_for = ctx->pad_radius;
     ctx->nodes_host.clear();
-    size_lds_forms(ctx, count);
+    size_lds_forms(ctx);
     return RT_OK;
 }
 

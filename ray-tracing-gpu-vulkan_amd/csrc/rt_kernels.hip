@@ -931,11 +931,12 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
                                           reinterpret_cast<const float4*>(P.mat), big);
 }
 
-// LBVH kernel with the whole tree and the per-sphere geometry + material records read by shading
-// staged in LDS, once per persistent block (one 1024-thread block per CU). Staged nodes use the
-// AB layout (node_hit); NOCT = 8 stages one copy per ray direction octant, each in its own
-// near-child-first order when the host provides one (nodes_oct). LDS: [nodes | leaf spheres |
-// leaf ids | geometry | materials | big-sphere table].
+// LBVH kernel with the whole tree staged in LDS, once per persistent block (one 1024-thread block
+// per CU). Staged nodes use the AB layout (node_hit); NOCT = 8 stages one copy per ray direction
+// octant, each in its own near-child-first order when the host provides one (nodes_oct). LDS:
+// [nodes | leaf spheres | leaf ids | big-sphere table]. The geometry + material records read by
+// shading stay in HBM: one random record per hit is an L2 hit (staging them in LDS measured the
+// same), and the LDS they would take fits bigger trees as octant copies.
 template <bool COUNT, uint32_t NOCT, int MODE>
 __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace_lds_kernel(const rt::TraceParams P) {
     extern __shared__ float4 lds[];
@@ -976,16 +977,12 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
                                                  __uint_as_float(v.z), __uint_as_float(v.w));
     }
     const uint32_t base = n_node4 + n_leaf4 + n_id4;
-    const uint32_t ng = P.n_spheres, nm = 2u * P.n_spheres;
     const float4* geom4 = reinterpret_cast<const float4*>(P.geom);
     const float4* mat4 = reinterpret_cast<const float4*>(P.mat);
-    for (uint32_t i = threadIdx.x; i < ng; i += kTraceBlock) lds[base + i] = geom4[i];
-    for (uint32_t i = threadIdx.x; i < nm; i += kTraceBlock) lds[base + ng + i] = mat4[i];
-    const BigTable big = stage_big(P, lds + base + ng + nm, threadIdx.x, kTraceBlock);
+    const BigTable big = stage_big(P, lds + base, threadIdx.x, kTraceBlock);
     __syncthreads();
     lbvh_loop<COUNT, NOCT == 8 ? LAYOUT_OCT : LAYOUT_LDS1, MODE>(
-        P, lds, lds + n_node4, reinterpret_cast<const uint32_t*>(lds + n_node4 + n_leaf4), lds + base,
-        lds + base + ng, big);
+        P, lds, lds + n_node4, reinterpret_cast<const uint32_t*>(lds + n_node4 + n_leaf4), geom4, mat4, big);
 }
 
 // LBVH kernel for trees too big for LDS: the treelet (rt_build.hip build_treelet) is staged in LDS
