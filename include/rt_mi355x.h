@@ -220,11 +220,18 @@ int rt_store_ppm(const char* path, const uint8_t* rgba8, uint32_t width, uint32_
  * 6 sample_seed_hash(bits(x), bits(y)) as bits, 7 / 8 low / high word of the 20.44 fixed-point
  * value of colour x, as bits, 9 checker decision at (x, y, 0.5 (x - y)) as 1 / 0. */
 int rt_debug_math(int device, int op, const float* in_pairs, float* out, uint32_t n);
+/* Diagnostic (tests only): the kernels' cheap correctly rounded reciprocal and square root
+ * (rt_device_math.h rcp_cr / sqrt_cr) against hipcc's correctly rounded 1.0f / x and sqrtf(x) over
+ * all 2^32 binary32 inputs on `device`; mismatches2[0] / [1] = differing results (NaN == NaN). */
+int rt_debug_exact_exhaustive(int device, uint64_t* mismatches2);
 /* Diagnostic: of ctx's last launch, {sample chunks per pixel, staged kernel form of the scene
  * (rt_internal.h ACCEL_*), its LDS bytes, CU count}. */
 int rt_debug_launch_info(rt_context* ctx, uint32_t* out4);
 /* Diagnostic: per-phase cycle sums of ctx's last launch, filled only by -DRT_STAMPS builds. */
 int rt_debug_stamps(rt_context* ctx, uint64_t* out8);
+/* Diagnostic: lane utilisation of ctx's last launch per kernel code point k (0..15), filled only by
+ * -DRT_UTIL builds: out32[2k] wave passes through the point, out32[2k + 1] active lanes summed. */
+int rt_debug_util(rt_context* ctx, uint64_t* out32);
 /* Diagnostic: histogram of LBVH box tests per segment of the last instrumented launch
  * (options.reserved[0] & 1), 2 x 64 bins: [0] segments that miss, [1] segments that hit. */
 int rt_debug_walk_hist(rt_context* ctx, uint64_t* out128);

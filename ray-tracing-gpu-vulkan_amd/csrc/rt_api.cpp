@@ -36,6 +36,7 @@ hipError_t launch_scatter_rows(const float* src_acc, const uint8_t* src_px, cons
                                uint32_t n_rows, uint32_t width, uint32_t dst_rows, float* dst_acc, uint8_t* dst_px,
                                hipStream_t st);
 hipError_t launch_debug_math(int op, const float* in, float* out, uint32_t n, hipStream_t st);
+hipError_t launch_debug_exact(unsigned long long* bad, hipStream_t st);
 }  // namespace rt
 
 struct rt_context {
@@ -890,6 +891,18 @@ int rt_scatter_rows(rt_context* ctx, const float* src_accum, const uint8_t* src_
     return RT_OK;
 }
 
+// Diagnostic export: per-code-point lane utilisation of the last launch (RT_UTIL builds; zeros
+// otherwise).
+int rt_debug_util(rt_context* ctx, uint64_t* out32) {
+    if (!ctx || !out32) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    DeviceGuard g(ctx->device);
+    if (ctx->ev_valid) RT_HIP(hipEventSynchronize(ctx->ev_last));
+    rt::Counters c;
+    RT_HIP(hipMemcpy(&c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
+    for (int k = 0; k < 32; k++) out32[k] = c.util[k];
+    return RT_OK;
+}
+
 // Diagnostic export: phase cycle sums of the last launch (RT_STAMPS builds; zeros otherwise).
 int rt_debug_stamps(rt_context* ctx, uint64_t* out8) {
     if (!ctx || !out8) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
@@ -1000,6 +1013,24 @@ int rt_debug_math(int device, int op, const float* in_pairs, float* out, uint32_
     RT_HIP(hipMemcpy(out, dout, size_t(n) * sizeof(float), hipMemcpyDeviceToHost));
     (void)hipFree(din);
     (void)hipFree(dout);
+    return RT_OK;
+}
+
+int rt_debug_exact_exhaustive(int device, uint64_t* mismatches2) {
+    if (!mismatches2) return fail(RT_ERR_INVALID_ARGUMENT, "NULL buffer");
+    int nd = 0;
+    if (int rc = rt::current_device_count(&nd)) return rc;
+    if (device < 0 || device >= nd) return fail(RT_ERR_INVALID_ARGUMENT, "device index out of range");
+    DeviceGuard g(device);
+    unsigned long long* bad = nullptr;
+    RT_HIP(hipMalloc(&bad, 2 * sizeof(unsigned long long)));
+    RT_HIP(hipMemset(bad, 0, 2 * sizeof(unsigned long long)));
+    RT_HIP(rt::launch_debug_exact(bad, nullptr));
+    unsigned long long h[2] = {0, 0};
+    RT_HIP(hipMemcpy(h, bad, sizeof(h), hipMemcpyDeviceToHost));
+    (void)hipFree(bad);
+    mismatches2[0] = h[0];
+    mismatches2[1] = h[1];
     return RT_OK;
 }
 

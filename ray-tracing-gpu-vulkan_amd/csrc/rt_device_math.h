@@ -21,14 +21,50 @@ __device__ __forceinline__ V3 mul(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, 
 __device__ __forceinline__ V3 scale(float s, V3 a) { return v3(s * a.x, s * a.y, s * a.z); }
 __device__ __forceinline__ V3 neg(V3 a) { return v3(-a.x, -a.y, -a.z); }
 
+// Correctly rounded 1 / x, cheaper than hipcc's general division (11 VALU with v_div_scale /
+// v_div_fmas / v_div_fixup): for |x| in [2^-125, 2^125] (x and 1/x normal with room to spare) the
+// hardware reciprocal (v_rcp_f32, within 1 ulp) is corrected by one Newton step whose residual
+// e = 1 - x r is exact in an fma; the result is the correctly rounded quotient. Other inputs (0,
+// inf, NaN, denormal and huge x) take the division. Bit-identical to 1.0f / x for all 2^32 inputs
+// (scripts/exact_math_exhaustive.hip, run on the GPU; profiles/r02_exact_math_exhaustive.log).
+__device__ __forceinline__ float rcp_cr(float x) {
+    const uint32_t ax = __float_as_uint(x) & 0x7fffffffu;
+    if (ax - 0x01000000u <= 0x7e000000u - 0x01000000u) {   // 2^-125 <= |x| <= 2^125
+        const float r = __builtin_amdgcn_rcpf(x);
+        const float e = __builtin_fmaf(-x, r, 1.0f);
+        return __builtin_fmaf(e, r, r);
+    }
+    return 1.0f / x;
+}
+
+// Correctly rounded sqrt(x), cheaper than hipcc's general sequence: for x in [2^-100, 2^100] the
+// hardware square root (v_sqrt_f32, within 1 ulp) is corrected by the exact fma residuals of its
+// two neighbours (the same correction hipcc emits, without the denormal scaling and the 0 / inf
+// class fix-up, which this range never needs). Other inputs take __builtin_sqrtf. Bit-identical
+// to it for all 2^32 inputs (scripts/exact_math_exhaustive.hip).
+__device__ __forceinline__ float sqrt_cr(float x) {
+    const uint32_t ux = __float_as_uint(x);
+    if (ux - 0x0d800000u <= 0x71800000u - 0x0d800000u) {   // 2^-100 <= x <= 2^100 (x > 0)
+        const float s = __builtin_amdgcn_sqrtf(x);
+        const float sm = __uint_as_float(__float_as_uint(s) - 1u);
+        const float sp = __uint_as_float(__float_as_uint(s) + 1u);
+        const float rm = __builtin_fmaf(-sm, s, x);
+        const float rp = __builtin_fmaf(-sp, s, x);
+        float t = rm <= 0.0f ? sm : s;
+        t = rp > 0.0f ? sp : t;
+        return t;
+    }
+    return __builtin_sqrtf(x);
+}
+
 // dot(a,b) = fma(a.z,b.z, fma(a.y,b.y, a.x*b.x))
 __device__ __forceinline__ float dot(V3 a, V3 b) {
     return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x));
 }
-// normalize(v) = v * (1 / sqrt(dot(v,v)))
+// normalize(v) = v * (1 / sqrt(dot(v,v)))   (both correctly rounded)
 __device__ __forceinline__ V3 normalize(V3 v) {
-    float len = __builtin_sqrtf(dot(v, v));
-    float inv = 1.0f / len;
+    float len = sqrt_cr(dot(v, v));
+    float inv = rcp_cr(len);
     return v3(v.x * inv, v.y * inv, v.z * inv);
 }
 // GLSL reflect(I, N) = I - 2.0 * dot(N, I) * N
@@ -41,7 +77,7 @@ __device__ __forceinline__ V3 refract(V3 i, V3 n, float eta) {
     float d = dot(n, i);
     float k = 1.0f - eta * eta * (1.0f - d * d);
     if (k < 0.0f) return v3(0.0f, 0.0f, 0.0f);
-    float s = eta * d + __builtin_sqrtf(k);
+    float s = eta * d + sqrt_cr(k);
     return sub(scale(eta, i), scale(s, n));
 }
 

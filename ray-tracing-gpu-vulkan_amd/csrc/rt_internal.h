@@ -100,8 +100,11 @@ enum : int { MODE_STREAM = 0, MODE_HASH = 1 };
 // B = (lo.z, hi.z, miss, hit). miss = treelet rank of the escape (END = ~0); hit = rank of the
 // next node (inner node above the cut), or a word with bit 31 set: 0x80000000 | first_count
 // (leaf) or 0xC0000000 | global node index (inner node at the cut: walk its subtree from L2).
-constexpr uint32_t kTreeletDepth = 11;
-constexpr uint32_t kTreeletCap = (2u << kTreeletDepth) - 1u;   // 4095 nodes, 128 KiB
+#ifndef RT_TREELET_DEPTH
+#define RT_TREELET_DEPTH 10
+#endif
+constexpr uint32_t kTreeletDepth = RT_TREELET_DEPTH;
+constexpr uint32_t kTreeletCap = (2u << kTreeletDepth) - 1u;   // 2047 nodes, 64 KiB: two blocks per CU
 
 // Counters block (device memory, zeroed before each launch by the host).
 struct Counters {
@@ -117,6 +120,8 @@ struct Counters {
     unsigned long long t_first, t_dry, t_last;   // LBVH kernel: s_memrealtime of the first wave's
                                                  // start, of the pixel queue running dry, of the last exit
     unsigned long long stamp[8];   // diagnostic builds only (-DRT_STAMPS): cycles per phase
+    unsigned long long util[2 * 16];   // diagnostic builds only (-DRT_UTIL): per code point k, wave
+                                       // passes [2k] and active lanes summed over them [2k + 1]
 };
 
 // Kernel launch parameters (passed by value as the kernel argument).

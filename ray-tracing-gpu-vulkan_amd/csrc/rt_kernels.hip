@@ -63,6 +63,58 @@ struct Stamps { unsigned long long acc[8], t; uint32_t cur; };
 #define STAMP_FLUSH do {} while (0)
 #endif
 
+// Diagnostic build only (-DRT_UTIL): lane utilisation per code point. UTIL(k, pred) counts one
+// wave pass through the point and the lanes executing it with `pred` true (block totals in LDS,
+// added to Counters::util at exit; rt_debug_util). Points: 0 node visit, 1 leaf test, 2 sphere
+// candidate (test4 loop), 3 shade, 4 diffuse, 5 metal, 6 dielectric, 7 sample start, 8 segment
+// (tracing lanes of 64), 9 unit vector draw, 10 shade of a hit, 11 node visit from L2.
+#ifdef RT_UTIL
+__shared__ unsigned long long s_util[32];
+#define UTIL(k, pred)                                                                          \
+    do {                                                                                       \
+        const unsigned long long b_ = __ballot(pred), a_ = __ballot(true);                     \
+        if (lane_id() == uint32_t(__ffsll(a_) - 1)) {                                          \
+            atomicAdd(&s_util[2 * (k)], 1ull);                                                 \
+            atomicAdd(&s_util[2 * (k) + 1], (unsigned long long)__popcll(b_));               \
+        }                                                                                      \
+    } while (0)
+#define UTIL_INIT do { if (threadIdx.x < 32) s_util[threadIdx.x] = 0ull; } while (0)
+#define UTIL_FLUSH                                                                             \
+    do {                                                                                       \
+        __syncthreads();                                                                       \
+        if (threadIdx.x < 32) atomicAdd(&P.counters->util[threadIdx.x], s_util[threadIdx.x]);  \
+    } while (0)
+#else
+#define UTIL(k, pred) do {} while (0)
+#define UTIL_INIT do {} while (0)
+#define UTIL_FLUSH do {} while (0)
+#endif
+
+// Diagnostic build only (-DRT_PLACEMENT): where the trace kernel's waves land. Counters::util[k]
+// (k = 0..3) = waves on SIMD k over the chip; util[8 + m] = blocks whose busiest SIMD holds m of
+// their waves (from the HW_ID register).
+#ifdef RT_PLACEMENT
+__shared__ uint32_t s_simd[4];
+#define PLACEMENT_RECORD(P)                                                                    \
+    do {                                                                                       \
+        if (threadIdx.x < 4) s_simd[threadIdx.x] = 0u;                                         \
+        __syncthreads();                                                                       \
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);                         \
+        const uint32_t simd = (hw >> 4) & 3u;                                                  \
+        if (lane_id() == 0) {                                                                  \
+            atomicAdd(&s_simd[simd], 1u);                                                      \
+            atomicAdd(&(P).counters->util[simd], 1ull);                                        \
+        }                                                                                      \
+        __syncthreads();                                                                       \
+        if (threadIdx.x == 0) {                                                                \
+            const uint32_t m = max(max(s_simd[0], s_simd[1]), max(s_simd[2], s_simd[3]));      \
+            atomicAdd(&(P).counters->util[8 + min(m, 23u)], 1ull);                             \
+        }                                                                                      \
+    } while (0)
+#else
+#define PLACEMENT_RECORD(P) do {} while (0)
+#endif
+
 // Driver traversal test for one sphere's AABB (src/ray_trace.cpp:586-596: center -/+ radius)
 // over [T_MIN, T_MAX]; identical arithmetic to the oracle's aabb_hit.
 __device__ __forceinline__ bool aabb_hit(float cx, float cy, float cz, float r, V3 o, V3 inv) {
@@ -87,7 +139,7 @@ __device__ __forceinline__ void test_sphere(float cx, float cy, float cz, float 
     const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - rr;
     const float D = __builtin_fmaf(b, b, -(a * c));
     if (D >= 0.0f) {
-        const float sq = __builtin_sqrtf(D);
+        const float sq = sqrt_cr(D);
         const float t1 = (-b - sq) * ia;
         const float t2 = (-b + sq) * ia;
         const float t = (t1 >= T_MIN) ? t1 : t2;
@@ -120,12 +172,13 @@ __device__ __forceinline__ void test4(const float4 s0, const float4 s1, const fl
         cand |= (Dv[k] >= 0.0f ? 1u : 0u) << k;
     }
     while (cand) {
+        UTIL(2, true);
         const uint32_t k = __builtin_ctz(cand);
         cand &= cand - 1u;
         // per-lane select of slot k (no dynamic register indexing)
         const float b = k == 0 ? bv[0] : k == 1 ? bv[1] : k == 2 ? bv[2] : bv[3];
         const float D = k == 0 ? Dv[0] : k == 1 ? Dv[1] : k == 2 ? Dv[2] : Dv[3];
-        const float sq = __builtin_sqrtf(D);
+        const float sq = sqrt_cr(D);
         float t = (-b - sq) * ia;
         if (!(t >= T_MIN)) t = (-b + sq) * ia;     // report t1 if t1 >= tmin, else t2
         if (t >= T_MIN && t <= best) {
@@ -399,6 +452,7 @@ __device__ __forceinline__ void finish_unit(const rt::TraceParams& P, const Path
 template <int MODE>
 __device__ __forceinline__ bool start_sample(const rt::TraceParams& P, const Camera& cam, Path& ps,
                                              V3& o, V3& d) {
+    UTIL(7, true);
     const uint32_t lx = ps.px & 0xffffu, ly = ps.px >> 16;
     if (ps.s >= ps.s_end) {
         finish_unit<MODE>(P, ps);
@@ -449,10 +503,12 @@ __device__ __forceinline__ bool shade(const rt::TraceParams& P, const float4* __
     bool scatter = false;
     V3 sd = v3(0.0f, 0.0f, 0.0f);
     V3 p = o;
+    UTIL(3, true);
     if (bi == 0xffffffffu) {
         att = v3(0.7f, 0.8f, 1.0f);  // shader.rmiss:15
     } else {
         // shader.rint:33/37 hit attribute; shader.rchit:38-49
+        UTIL(10, true);
         p = v3(__builtin_fmaf(best, d.x, o.x), __builtin_fmaf(best, d.y, o.y),
                __builtin_fmaf(best, d.z, o.z));
         const float4 gc4 = geom4[bi];
@@ -469,16 +525,19 @@ __device__ __forceinline__ bool shade(const rt::TraceParams& P, const float4* __
         // diffuse and metal both draw one random unit vector first (shader.rchit:69, :80): one
         // copy of that code serves a wave holding both materials
         V3 ru = v3(0.0f, 0.0f, 0.0f);
-        if (mtype < 2u) ru = random_unit_vector(ps.seed);
+        if (mtype < 2u) { UTIL(9, true); ru = random_unit_vector(ps.seed); }
         if (mtype == 0u) {                       // diffuse, shader.rchit:68-76
+            UTIL(4, true);
             sd = add(n, ru);
             if (fabsf(sd.x) < 1e-8f && fabsf(sd.y) < 1e-8f && fabsf(sd.z) < 1e-8f) sd = n;
         } else if (mtype == 1u) {                // metal, shader.rchit:78-89
+            UTIL(5, true);
             const V3 refl = reflect(d, n);
             const V3 fuzz = scale(m0.w, ru);
             const V3 sc = normalize(add(refl, fuzz));
             if (dot(sc, n) > 0.0f) sd = sc;
         } else if (mtype == 2u) {                // dielectric, shader.rchit:91-100,125-133
+            UTIL(6, true);
             // eta and r0 = ((1 - eta) / (1 + eta))^2 per face: from the record (solid dielectrics,
             // rt_internal.h make_mat) or computed here (checkered ones: colors[1] is taken)
             float eta, r;
@@ -492,7 +551,7 @@ __device__ __forceinline__ bool shade(const rt::TraceParams& P, const float4* __
             }
             const float cos_t = dot(neg(d), n);
             bool refracts = false;
-            if (eta * __builtin_sqrtf(1.0f - cos_t * cos_t) <= 1.0f) {
+            if (eta * sqrt_cr(1.0f - cos_t * cos_t) <= 1.0f) {
                 const float refl = r + (1.0f - r) * pow5(1.0f - cos_t);
                 refracts = refl < rnd(ps.seed);
             }
@@ -534,17 +593,21 @@ __device__ __forceinline__ void record_tile_cost(const rt::TraceParams& P, const
 }
 
 // Waves per SIMD the register budget is sized for. Brute force: 6 (71 VGPRs, no spills). LBVH:
-// 4 (128 VGPRs): at 6 the 80-VGPR budget spilled ~34 VGPRs of path state around every walk, and
-// 4 waves of the unspilled kernel measured 8 % faster.
+// 6 (80 VGPRs) in 768-thread blocks (12 waves, 3 per SIMD), two blocks per CU: the staged octant
+// tree (73 KB) and the depth-10 treelet (64 KB) fit twice in the 160 KB LDS. Measured at 1080p /
+// 1000 spp (scripts/perf_variants.py): 165 ms against 193 ms for one 1024-thread
+// block per CU at 4 waves per SIMD (98 VGPRs), although the 80-VGPR budget spills ~31 VGPRs
+// outside the walk loop; 8 waves per SIMD (64 VGPRs) spill more and took 180 ms; blocks whose
+// wave count is not a multiple of 4 (640, 896 threads) leave SIMDs unevenly loaded (+50 %).
 #ifndef RT_BRUTE_WAVES_PER_SIMD
 #define RT_BRUTE_WAVES_PER_SIMD 6
 #endif
 #ifndef RT_TRACE_WAVES_PER_SIMD
-#define RT_TRACE_WAVES_PER_SIMD 4
+#define RT_TRACE_WAVES_PER_SIMD 6
 #endif
 constexpr uint32_t kBruteBlock = 256;
 #ifndef RT_TRACE_BLOCK
-#define RT_TRACE_BLOCK 1024
+#define RT_TRACE_BLOCK 768
 #endif
 constexpr uint32_t kTraceBlock = RT_TRACE_BLOCK;   // one block per CU shares one staged tree / treelet
 
@@ -574,9 +637,9 @@ __global__ __launch_bounds__(kBruteBlock, RT_BRUTE_WAVES_PER_SIMD) void rt_trace
         if (st == ST_TRACING) {
             float best = T_MAX_SUCC;
             uint32_t bi = 0xffffffffu;
-            const V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+            const V3 inv = v3(rcp_cr(d.x), rcp_cr(d.y), rcp_cr(d.z));
             const float a = dot(d, d);
-            closest_brute(P, o, d, inv, a, 1.0f / a, best, bi);
+            closest_brute(P, o, d, inv, a, rcp_cr(a), best, bi);
             if (COUNT) n_sph += P.n_spheres;
             n_seg++;
             ps.segs++;
@@ -687,8 +750,8 @@ __device__ __forceinline__ BigTable stage_big(const rt::TraceParams& P, float4* 
 // New segment: hoisted per-ray terms and the exhaustive big spheres.
 __device__ __forceinline__ void setup_ray(const rt::TraceParams& P, const BigTable& big, Ray& r, uint32_t& n_sph) {
     r.a = dot(r.d, r.d);
-    r.ia = 1.0f / r.a;
-    r.inv = v3(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+    r.ia = rcp_cr(r.a);
+    r.inv = v3(rcp_cr(r.d.x), rcp_cr(r.d.y), rcp_cr(r.d.z));
     r.best = T_MAX_SUCC;
     r.bi = 0xffffffffu;
     for (uint32_t k0 = 0; k0 < P.n_big; k0 += 4) {   // wave-uniform: LDS broadcast reads
@@ -727,6 +790,7 @@ __device__ __forceinline__ void walk_global_range(const rt::TraceParams& P, cons
     uint32_t pending = 0u;
     for (;;) {
         while (gi < bound && pending == 0u) {
+            UTIL(11, true);
             const float4 n0 = gnodes[2 * gi];
             const float4 n1 = gnodes[2 * gi + 1];
             if (COUNT) n_box++;
@@ -764,6 +828,7 @@ __device__ __forceinline__ void walk(const rt::TraceParams& P, const float4* __r
         for (;;) {
             uint32_t cont = END;
             while (int32_t(ni) >= 0) {
+                UTIL(0, true);
                 const float4 A = lds_f4(ni);
                 const float4 B = lds_f4(ni + 16u);
                 if (COUNT) n_box++;
@@ -774,6 +839,7 @@ __device__ __forceinline__ void walk(const rt::TraceParams& P, const float4* __r
             const bool at = ni != END;
             if (!__ballot(at)) break;
             if (at) {
+                UTIL(1, true);
                 if (ni & 0x40000000u) {   // subtree of global node g (inner, its box was hit): [g + 1, escape(g))
                     const uint32_t g = ni & 0x3fffffffu;
                     const uint32_t eg = __float_as_uint(gnodes[2 * g].w);
@@ -794,38 +860,24 @@ __device__ __forceinline__ void walk(const rt::TraceParams& P, const float4* __r
         // leaves the inner loop at a hit leaf holding its leaf word; the leaves are tested
         // together after the loop (while-while).
         const uint32_t nbase = uint32_t(reinterpret_cast<uintptr_t>((LdsF4)nodes4));   // LDS address of node 0
-        uint32_t ni = r.walk ? nbase + (LAYOUT == LAYOUT_OCT ? octant(r.d) * P.n_nodes * 32u : 0u) : END;
+        constexpr uint32_t kNB = 32u, kBOff = 16u;
+        uint32_t ni = r.walk ? nbase + (LAYOUT == LAYOUT_OCT ? octant(r.d) * P.n_nodes * kNB : 0u) : END;
         for (;;) {
-#ifdef RT_AB_WALK2   // A/B only: the hit successor (next node in memory) is loaded with the node and
-                     // tested in the same iteration when the node is an inner node that is hit
             while (int32_t(ni) >= 0) {
-                const float4 A = lds_f4(ni);
-                const float4 B = lds_f4(ni + 16u);
-                const float4 C = lds_f4(ni + 32u);
-                const float4 D = lds_f4(ni + 48u);
-                if (COUNT) n_box++;
-                const bool hit = node_hit<LAYOUT == LAYOUT_OCT ? 8u : 1u>(A, B, q, r.limit);
-                const uint32_t nx = __float_as_uint(hit ? B.w : B.z);
-                const bool inner = hit && int32_t(nx) >= 0;
-                const bool hit2 = node_hit<LAYOUT == LAYOUT_OCT ? 8u : 1u>(C, D, q, r.limit);
-                if (COUNT && inner) n_box++;
-                ni = inner ? __float_as_uint(hit2 ? D.w : D.z) : nx;
-            }
-#else
-            while (int32_t(ni) >= 0) {
-                const float4 A = lds_f4(ni);         // links are LDS addresses:
-                const float4 B = lds_f4(ni + 16u);   // no address arithmetic per visit
+                UTIL(0, true);
+                const float4 A = lds_f4(ni);          // links are LDS addresses:
+                const float4 B = lds_f4(ni + kBOff);  // no address arithmetic per visit
                 if (COUNT) n_box++;
                 const bool hit = node_hit<LAYOUT == LAYOUT_OCT ? 8u : 1u>(A, B, q, r.limit);
                 ni = __float_as_uint(hit ? B.w : B.z);
             }
-#endif
             const bool at_leaf = ni != END;
             if (!__ballot(at_leaf)) break;   // no lane stopped at a leaf: all walks done
             if (at_leaf) {
+                UTIL(1, true);
                 const uint32_t esc = (ni >> 12) & 0x7ffffu;
                 leaf_test<COUNT>(P, leaf4, leaf_ids, ((ni >> 2) & 1023u) * 4u, (ni & 3u) + 1u, r, n_sph);
-                ni = esc == 0x7ffffu ? END : nbase + esc * 32u;
+                ni = esc == 0x7ffffu ? END : nbase + esc * kNB;
             }
         }
     }
@@ -877,6 +929,7 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
         if (!tracing) break;                           // every lane retired
         if (COUNT && lane == 0) atomicAdd(&P.counters->lane_hist[__popcll(tracing)], 1ull);
         STAMP(1);
+        UTIL(8, st == ST_TRACING);
         const uint32_t box0 = n_box;
         if (st == ST_TRACING) setup_ray(P, big, r, n_sph);
         STAMP(2);
@@ -917,11 +970,14 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
         atomicAdd(&P.counters->sphere_tests, (unsigned long long)n_sph);
         if (lane == 0) atomicAdd(&P.counters->wave_iters, wave_iters);
     }
+    UTIL_FLUSH;
 }
 
 // LBVH kernel, tree in global memory (A/B reference: every node and leaf from L2).
 template <bool COUNT, int MODE>
 __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace_global_kernel(const rt::TraceParams P) {
+    UTIL_INIT;
+    PLACEMENT_RECORD(P);
     extern __shared__ float4 lds[];   // the big-sphere table only
     const BigTable big = stage_big(P, lds, threadIdx.x, kTraceBlock);
     __syncthreads();
@@ -939,10 +995,13 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
 // same), and the LDS they would take fits bigger trees as octant copies.
 template <bool COUNT, uint32_t NOCT, int MODE>
 __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace_lds_kernel(const rt::TraceParams P) {
+    UTIL_INIT;
+    PLACEMENT_RECORD(P);
     extern __shared__ float4 lds[];
     typedef const __attribute__((address_space(3))) float4* LdsF4;
     const uint32_t lbase = uint32_t(reinterpret_cast<uintptr_t>((LdsF4)lds));   // LDS address of lds[0]
     const uint32_t n_node4 = 2u * NOCT * P.n_nodes, n_leaf4 = P.n_leaf, n_id4 = (P.n_leaf + 3u) / 4u;
+    constexpr uint32_t kNodeBytes = 32u;
     const float4* nodes4 = reinterpret_cast<const float4*>(P.nodes);
     for (uint32_t oi = threadIdx.x; oi < NOCT * P.n_nodes; oi += kTraceBlock) {
         const uint32_t o = oi / P.n_nodes, i = oi - o * P.n_nodes;   // copy o, node i
@@ -958,15 +1017,15 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
         const uint32_t esc = __float_as_uint(lo.w), fc = __float_as_uint(hi.w);
         const bool nx = NOCT == 8 && (o & 1u), ny = NOCT == 8 && (o & 2u), nz = NOCT == 8 && (o & 4u);
         const uint32_t cb = o * P.n_nodes;   // first node of copy o
-        const uint32_t miss = esc == END ? END : lbase + (cb + esc) * 32u;
+        const uint32_t miss = esc == END ? END : lbase + (cb + esc) * kNodeBytes;
         // (kept as separate statements: one combined expression crashed the ROCm 7.2 instruction
         // selector)
         const uint32_t escf = esc == END ? 0x7ffffu : cb + esc;
         const uint32_t leafw = 0x80000000u + (escf << 12) + ((fc >> 6) << 2) + ((fc - 1u) & 3u);
-        const uint32_t hit = fc ? leafw : lbase + (cb + i + 1u) * 32u;
-        const size_t b = size_t(cb + i) * 2u;
+        const uint32_t hit = fc ? leafw : lbase + (cb + i + 1u) * kNodeBytes;
+        const size_t b = size_t(cb + i) * 2u, bb = b + 1u;
         lds[b] = make_float4(nx ? hi.x : lo.x, ny ? hi.y : lo.y, nx ? lo.x : hi.x, ny ? lo.y : hi.y);
-        lds[b + 1] = make_float4(nz ? hi.z : lo.z, nz ? lo.z : hi.z, __uint_as_float(miss), __uint_as_float(hit));
+        lds[bb] = make_float4(nz ? hi.z : lo.z, nz ? lo.z : hi.z, __uint_as_float(miss), __uint_as_float(hit));
     }
     const float4* leaf4 = reinterpret_cast<const float4*>(P.leaf_geom);
     for (uint32_t i = threadIdx.x; i < n_leaf4; i += kTraceBlock) lds[n_node4 + i] = leaf4[i];
@@ -990,6 +1049,8 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
 // materials stay in HBM/L2.
 template <bool COUNT, int MODE>
 __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace_top_kernel(const rt::TraceParams P) {
+    UTIL_INIT;
+    PLACEMENT_RECORD(P);
     extern __shared__ float4 lds[];
     typedef const __attribute__((address_space(3))) float4* LdsF4;
     const uint32_t lbase = uint32_t(reinterpret_cast<uintptr_t>((LdsF4)lds));
@@ -1084,6 +1145,21 @@ __global__ void rt_debug_math_kernel(int op, const float* __restrict__ in, float
     out[i] = r;
 }
 
+// Diagnostic: rcp_cr / sqrt_cr against hipcc's correctly rounded 1.0f / x and sqrtf over all 2^32
+// inputs (base .. base + grid * 256); mismatches counted in bad[0] / bad[1] (NaN equals NaN).
+__global__ __launch_bounds__(256) void rt_debug_exact_kernel(uint64_t base, unsigned long long* bad) {
+    const uint32_t bits = uint32_t(base + uint64_t(blockIdx.x) * blockDim.x + threadIdx.x);
+    const float x = __uint_as_float(bits);
+    const float r0 = rcp_cr(x), r1 = 1.0f / x, s0 = sqrt_cr(x), s1 = __builtin_sqrtf(x);
+    const bool rb = __float_as_uint(r0) != __float_as_uint(r1) && !(r0 != r0 && r1 != r1);
+    const bool sb = __float_as_uint(s0) != __float_as_uint(s1) && !(s0 != s0 && s1 != s1);
+    const unsigned long long mr = __ballot(rb), ms = __ballot(sb);
+    if (lane_id() == 0 && (mr | ms)) {
+        atomicAdd(&bad[0], (unsigned long long)__popcll(mr));
+        atomicAdd(&bad[1], (unsigned long long)__popcll(ms));
+    }
+}
+
 }  // namespace
 
 // ---- host-callable launchers (rt_api.cpp) ---------------------------------------------------
@@ -1153,6 +1229,13 @@ hipError_t launch_tonemap(const float* accum, uint64_t n_texels, uint32_t spp, u
     if (n_texels == 0) return hipSuccess;
     hipLaunchKernelGGL(rt_tonemap_kernel, dim3(stream_blocks(n_texels)), dim3(256), 0, st,
                        reinterpret_cast<const float4*>(accum), n_texels, float(spp), reinterpret_cast<uint32_t*>(out));
+    return hipGetLastError();
+}
+
+hipError_t launch_debug_exact(unsigned long long* bad, hipStream_t st) {
+    const uint32_t grid = 1u << 22;   // 2^30 inputs per launch, 4 launches
+    for (uint64_t base = 0; base < (1ull << 32); base += uint64_t(grid) * 256u)
+        hipLaunchKernelGGL(rt_debug_exact_kernel, dim3(grid), dim3(256), 0, st, base, bad);
     return hipGetLastError();
 }
 

@@ -121,6 +121,8 @@ EXPORTS = {
     "rt_store_ppm": (_I, [ctypes.c_char_p, _P, _U32, _U32]),
     "rt_debug_math": (_I, [_I, _I, _P, _P, _U32]),
     "rt_debug_stamps": (_I, [_P, _P]),
+    "rt_debug_util": (_I, [_P, _P]),
+    "rt_debug_exact_exhaustive": (_I, [ctypes.c_int, _P]),
     "rt_debug_launch_info": (_I, [_P, _P]),
     "rt_debug_walk_hist": (_I, [_P, _P]),
     "rt_debug_lane_hist": (_I, [_P, _P]),
@@ -157,6 +159,8 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
         raise FileNotFoundError(f"{p} not built: run `make -C {PKG_ROOT}` or __graft_entry__.build()")
     lib = ctypes.CDLL(str(p))
     for name, (res, args) in EXPORTS.items():
+        if path is not None and not hasattr(lib, name):
+            continue   # an older A/B build may predate a diagnostic entry point
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -145,6 +145,16 @@ def test_math_primitives_bit_exact(rtvk, torch, oracle, op):
     assert same.all(), f"op {op}: {np.count_nonzero(~same)} differ, e.g. x={x[~same][:3]} gpu={out[~same][:3]} ref={ref[~same][:3]}"
 
 
+def test_cheap_exact_rcp_sqrt_exhaustive(rtvk, torch):
+    """The kernels' rcp_cr / sqrt_cr (v_rcp_f32 / v_sqrt_f32 + exact fma corrections) equal the
+    correctly rounded 1.0f / x and sqrtf(x) for every one of the 2^32 binary32 inputs."""
+    import ctypes
+    from rtvk import abi
+    bad = (ctypes.c_uint64 * 2)()
+    abi.check(rtvk.load_library().rt_debug_exact_exhaustive(0, bad))
+    assert (bad[0], bad[1]) == (0, 0), f"rcp_cr mismatches {bad[0]}, sqrt_cr mismatches {bad[1]}"
+
+
 def _debug_math(rtvk, op, x, y):
     pairs = np.ascontiguousarray(np.stack([x, y], 1), np.float32)
     out = np.zeros(len(x), np.float32)
