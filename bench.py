@@ -195,10 +195,18 @@ def main() -> int:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    # RCCL (backend "nccl"); RT_BENCH_BACKEND=gloo rehearses N ranks sharing the visible GPUs
+    # (bands staged through host memory): a test of the N > 1 code path, never a reported number.
+    backend = os.environ.get("RT_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     accel = abi.RT_ACCEL_BRUTE if accel_name == "brute" else abi.RT_ACCEL_LBVH
     rng_mode = abi.RT_RNG_SAMPLE_HASH if args.rng == "hash" else abi.RT_RNG_PIXEL_STREAM
@@ -380,6 +388,8 @@ def main() -> int:
             "tree": "device-lbvh" if renderer.scene_array(8)["device_built"] else "host-sah",
             "msegments_per_s": round(st.segments / max(1, st.samples) * value, 2),
             "roofline": roof,
+            **({"rehearsal": f"{backend} backend, {world} ranks sharing {torch.cuda.device_count()} GPU(s): "
+                               "code-path test, not a measurement"} if backend != "nccl" else {}),
             "context": {"reference_rx6800xt_vulkan_rt_msamples": 1658.9,
                         "source": "README.md:57,61 via BASELINE.md (different GPU, HW RT cores)"},
         }

@@ -220,10 +220,11 @@ int rt_store_ppm(const char* path, const uint8_t* rgba8, uint32_t width, uint32_
  * 6 sample_seed_hash(bits(x), bits(y)) as bits, 7 / 8 low / high word of the 20.44 fixed-point
  * value of colour x, as bits, 9 checker decision at (x, y, 0.5 (x - y)) as 1 / 0. */
 int rt_debug_math(int device, int op, const float* in_pairs, float* out, uint32_t n);
-/* Diagnostic (tests only): the kernels' cheap correctly rounded reciprocal and square root
- * (rt_device_math.h rcp_cr / sqrt_cr) against hipcc's correctly rounded 1.0f / x and sqrtf(x) over
- * all 2^32 binary32 inputs on `device`; mismatches2[0] / [1] = differing results (NaN == NaN). */
-int rt_debug_exact_exhaustive(int device, uint64_t* mismatches2);
+/* Diagnostic (tests only): the kernels' cheap correctly rounded operations against hipcc's
+ * correctly rounded ones on `device`: rcp_cr(x) vs 1.0f / x and sqrt_cr(x) vs sqrtf(x) over all 2^32
+ * binary32 inputs (mismatches3[0], [1]; NaN == NaN), and the camera's float(double(x) * (1 /
+ * double(b))) vs x / b for every binary32 x in [0, 65536) and eleven image sizes b (mismatches3[2]). */
+int rt_debug_exact_exhaustive(int device, uint64_t* mismatches3);
 /* Diagnostic: of ctx's last launch, {sample chunks per pixel, staged kernel form of the scene
  * (rt_internal.h ACCEL_*), its LDS bytes, CU count}. */
 int rt_debug_launch_info(rt_context* ctx, uint32_t* out4);

@@ -265,6 +265,8 @@ void fill_camera(const RenderCallInfo& rci, rt::TraceParams& P) {
     P.half_aperture = aperture / 2.0f;
     P.size_x = sx;
     P.size_y = sy;
+    P.inv_size_x = 1.0 / double(sx);
+    P.inv_size_y = 1.0 / double(sy);
 }
 
 // ---- scene.h:37-157 -------------------------------------------------------------------------
@@ -1016,21 +1018,20 @@ int rt_debug_math(int device, int op, const float* in_pairs, float* out, uint32_
     return RT_OK;
 }
 
-int rt_debug_exact_exhaustive(int device, uint64_t* mismatches2) {
-    if (!mismatches2) return fail(RT_ERR_INVALID_ARGUMENT, "NULL buffer");
+int rt_debug_exact_exhaustive(int device, uint64_t* mismatches3) {
+    if (!mismatches3) return fail(RT_ERR_INVALID_ARGUMENT, "NULL buffer");
     int nd = 0;
     if (int rc = rt::current_device_count(&nd)) return rc;
     if (device < 0 || device >= nd) return fail(RT_ERR_INVALID_ARGUMENT, "device index out of range");
     DeviceGuard g(device);
     unsigned long long* bad = nullptr;
-    RT_HIP(hipMalloc(&bad, 2 * sizeof(unsigned long long)));
-    RT_HIP(hipMemset(bad, 0, 2 * sizeof(unsigned long long)));
+    RT_HIP(hipMalloc(&bad, 3 * sizeof(unsigned long long)));
+    RT_HIP(hipMemset(bad, 0, 3 * sizeof(unsigned long long)));
     RT_HIP(rt::launch_debug_exact(bad, nullptr));
-    unsigned long long h[2] = {0, 0};
+    unsigned long long h[3] = {0, 0, 0};
     RT_HIP(hipMemcpy(h, bad, sizeof(h), hipMemcpyDeviceToHost));
     (void)hipFree(bad);
-    mismatches2[0] = h[0];
-    mismatches2[1] = h[1];
+    for (int k = 0; k < 3; k++) mismatches3[k] = h[k];
     return RT_OK;
 }
 

@@ -135,6 +135,7 @@ struct TraceParams {
     float lf[3], hor[3], ver[3], ulc[3], cup[3], crt[3];
     float half_aperture;
     float size_x, size_y;          // full image size as float (shader.rgen:42)
+    double inv_size_x, inv_size_y; // 1 / size, rounded to double (camera division, rt_kernels.hip)
     uint32_t number, spp, max_depth;
     uint32_t seed_local;           // 1: seed from launch-local ids (shader.rgen:40 verbatim)
     uint32_t rng_counter;          // STREAM only, 1: RT_RNG_SAMPLE_COUNTER

@@ -67,7 +67,8 @@ struct Stamps { unsigned long long acc[8], t; uint32_t cur; };
 // wave pass through the point and the lanes executing it with `pred` true (block totals in LDS,
 // added to Counters::util at exit; rt_debug_util). Points: 0 node visit, 1 leaf test, 2 sphere
 // candidate (test4 loop), 3 shade, 4 diffuse, 5 metal, 6 dielectric, 7 sample start, 8 segment
-// (tracing lanes of 64), 9 unit vector draw, 10 shade of a hit, 11 node visit from L2.
+// (tracing lanes of 64), 9 unit vector draw, 10 shade of a hit, 11 node visit from L2, 12 / 13 / 14
+// node visits (LDS) of passes with at most 8 / 16 / 32 active lanes.
 #ifdef RT_UTIL
 __shared__ unsigned long long s_util[32];
 #define UTIL(k, pred)                                                                          \
@@ -473,8 +474,12 @@ __device__ __forceinline__ bool start_sample(const rt::TraceParams& P, const Cam
     else if (P.rng_counter) ps.seed = tea(ps.pixel_seed, P.sample_base + ps.s);
     float ux = float(gx) + rnd(ps.seed);
     float uy = float(gy) + rnd(ps.seed);
-    ux = ux / P.size_x;
-    uy = uy / P.size_y;
+    // ux / size_x, correctly rounded, as one double multiply by the host's double 1/size (3 VALU
+    // instead of 11): binary32 quotients lie at least 2^-49 (relative) from a binary32 rounding
+    // boundary and never on one, and the double product is within 2^-52 of the quotient, so its
+    // rounding to float is the correctly rounded quotient.
+    ux = float(double(ux) * P.inv_size_x);
+    uy = float(double(uy) * P.inv_size_y);
     const float lxr = rnd_pm1(ps.seed);
     const float lyr = rnd_pm1(ps.seed);
     float rx, ry;
@@ -882,6 +887,14 @@ __device__ __forceinline__ void walk(const rt::TraceParams& P, const float4* __r
         for (;;) {
             while (int32_t(ni) >= 0) {
                 UTIL(0, true);
+#ifdef RT_UTIL
+                {   // node passes by active lanes: [12] <= 8 lanes, [13] <= 16, [14] <= 32 (+ lanes)
+                    const uint32_t na = __popcll(__ballot(true));
+                    if (na <= 8) UTIL(12, true);
+                    if (na <= 16) UTIL(13, true);
+                    if (na <= 32) UTIL(14, true);
+                }
+#endif
                 const float4 A = lds_f4(ni);          // links are LDS addresses:
                 const float4 B = lds_f4(ni + kBOff);  // no address arithmetic per visit
                 if (COUNT) n_box++;
@@ -1163,10 +1176,19 @@ __global__ void rt_debug_math_kernel(int op, const float* __restrict__ in, float
 }
 
 // Diagnostic: rcp_cr / sqrt_cr against hipcc's correctly rounded 1.0f / x and sqrtf over all 2^32
-// inputs (base .. base + grid * 256); mismatches counted in bad[0] / bad[1] (NaN equals NaN).
-__global__ __launch_bounds__(256) void rt_debug_exact_kernel(uint64_t base, unsigned long long* bad) {
+// inputs (base .. base + grid * 256); mismatches counted in bad[0] / bad[1] (NaN equals NaN). With
+// div_b != 0: the camera's float(double(x) * (1 / double(div_b))) against x / div_b for every
+// x in [0, 65536) (the camera's numerators), mismatches in bad[2].
+__global__ __launch_bounds__(256) void rt_debug_exact_kernel(uint64_t base, float div_b, unsigned long long* bad) {
     const uint32_t bits = uint32_t(base + uint64_t(blockIdx.x) * blockDim.x + threadIdx.x);
     const float x = __uint_as_float(bits);
+    if (div_b != 0.0f) {
+        if (bits >= 0x47800000u) return;   // x >= 65536
+        const float q0 = float(double(x) * (1.0 / double(div_b))), q1 = x / div_b;
+        const unsigned long long mq = __ballot(__float_as_uint(q0) != __float_as_uint(q1));
+        if (lane_id() == 0 && mq) atomicAdd(&bad[2], (unsigned long long)__popcll(mq));
+        return;
+    }
     const float r0 = rcp_cr(x), r1 = 1.0f / x, s0 = sqrt_cr(x), s1 = __builtin_sqrtf(x);
     const bool rb = __float_as_uint(r0) != __float_as_uint(r1) && !(r0 != r0 && r1 != r1);
     const bool sb = __float_as_uint(s0) != __float_as_uint(s1) && !(s0 != s0 && s1 != s1);
@@ -1252,7 +1274,12 @@ hipError_t launch_tonemap(const float* accum, uint64_t n_texels, uint32_t spp, u
 hipError_t launch_debug_exact(unsigned long long* bad, hipStream_t st) {
     const uint32_t grid = 1u << 22;   // 2^30 inputs per launch, 4 launches
     for (uint64_t base = 0; base < (1ull << 32); base += uint64_t(grid) * 256u)
-        hipLaunchKernelGGL(rt_debug_exact_kernel, dim3(grid), dim3(256), 0, st, base, bad);
+        hipLaunchKernelGGL(rt_debug_exact_kernel, dim3(grid), dim3(256), 0, st, base, 0.0f, bad);
+    // camera divisors: the BASELINE sizes, small and odd ones, the largest band extent
+    const float divs[] = {1920.0f, 1080.0f, 3840.0f, 2160.0f, 64.0f, 36.0f, 1.0f, 3.0f, 7.0f, 1000.0f, 65535.0f};
+    for (float b : divs)
+        for (uint64_t base = 0; base < 0x47800000ull; base += uint64_t(grid) * 256u)
+            hipLaunchKernelGGL(rt_debug_exact_kernel, dim3(grid), dim3(256), 0, st, base, b, bad);
     return hipGetLastError();
 }
 

@@ -17,7 +17,7 @@ spp = int(sys.argv[1]) if len(sys.argv) > 1 else 100
 W, H, K = (int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])) if len(sys.argv) > 4 else (1920, 1080, 11)
 NAMES = {0: "node visit (LDS)", 11: "node visit (L2)", 1: "leaf test", 2: "sphere candidate", 8: "segment (tracing)",
          7: "sample start", 3: "shade", 10: "shade hit", 9: "unit vector", 4: "diffuse", 5: "metal",
-         6: "dielectric"}
+         6: "dielectric", 12: "node pass <=8 lanes", 13: "node pass <=16", 14: "node pass <=32"}
 r = rtvk.Renderer(0)
 r.set_scene(rtvk.generateRandomScene(0.0, K))
 acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
@@ -31,7 +31,7 @@ for rng in (rtvk.HASH,):
     abi.check(lib.rt_debug_util(r._ctx, u))
     st = r.stats()
     print(f"{W}x{H} spp {spp} grid {K} rng {'hash' if rng == rtvk.HASH else 'stream'}: segments {st.segments}")
-    for k in (8, 7, 0, 11, 1, 2, 3, 10, 9, 4, 5, 6):
+    for k in (8, 7, 0, 12, 13, 14, 11, 1, 2, 3, 10, 9, 4, 5, 6):
         n, a = u[2 * k], u[2 * k + 1]
         if n == 0:
             continue

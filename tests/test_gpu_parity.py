@@ -147,12 +147,13 @@ def test_math_primitives_bit_exact(rtvk, torch, oracle, op):
 
 def test_cheap_exact_rcp_sqrt_exhaustive(rtvk, torch):
     """The kernels' rcp_cr / sqrt_cr (v_rcp_f32 / v_sqrt_f32 + exact fma corrections) equal the
-    correctly rounded 1.0f / x and sqrtf(x) for every one of the 2^32 binary32 inputs."""
+    correctly rounded 1.0f / x and sqrtf(x) for every one of the 2^32 binary32 inputs, and the
+    camera's double-reciprocal division equals x / b for every x in [0, 65536) at eleven sizes b."""
     import ctypes
     from rtvk import abi
-    bad = (ctypes.c_uint64 * 2)()
+    bad = (ctypes.c_uint64 * 3)()
     abi.check(rtvk.load_library().rt_debug_exact_exhaustive(0, bad))
-    assert (bad[0], bad[1]) == (0, 0), f"rcp_cr mismatches {bad[0]}, sqrt_cr mismatches {bad[1]}"
+    assert tuple(bad) == (0, 0, 0), f"rcp_cr {bad[0]}, sqrt_cr {bad[1]}, camera division {bad[2]} mismatches"
 
 
 def _debug_math(rtvk, op, x, y):
