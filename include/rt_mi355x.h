@@ -77,7 +77,7 @@ typedef enum rt_rng_mode {
                                   pixel are independent and may be split across launches                        */
     RT_RNG_SAMPLE_HASH = 2     /* counter-based (the north star's RNG): sample s starts its LCG at
                                   lowbias32(pixel_seed + 0x9E3779B9 * s) and per-sample colours are summed in
-                                  20.44 fixed point, so the library splits a pixel's samples into chunks run
+                                  8.24 fixed point, so the library splits a pixel's samples into chunks run
                                   by any lanes in any order with bit-identical results;
                                   samplesPerRenderCall <= 2^19                                                */
 } rt_rng_mode;
@@ -217,7 +217,7 @@ int rt_store_ppm(const char* path, const uint8_t* rgba8, uint32_t width, uint32_
 
 /* Diagnostic (tests only): evaluates one arithmetic-contract primitive on `device` for n
  * (x, y) pairs: op 0 sqrt(x), 1 x/y, 2 sin(x), 3 fma(x,y,1), 4 normalize(x,y,0.5).x, 5 pow(x,5),
- * 6 sample_seed_hash(bits(x), bits(y)) as bits, 7 / 8 low / high word of the 20.44 fixed-point
+ * 6 sample_seed_hash(bits(x), bits(y)) as bits, 7 / 8 low / high word of the 8.24 fixed-point
  * value of colour x, as bits, 9 checker decision at (x, y, 0.5 (x - y)) as 1 / 0. */
 int rt_debug_math(int device, int op, const float* in_pairs, float* out, uint32_t n);
 /* Diagnostic (tests only): the kernels' cheap correctly rounded operations against hipcc's

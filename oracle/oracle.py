@@ -77,7 +77,7 @@ def sample_seed_hash(pixel_seed: int, s: int) -> int:
 
 
 def sample_fixed(c: float) -> int:
-    """RT_RNG_SAMPLE_HASH: 20.44 fixed-point value of a sample colour channel."""
+    """RT_RNG_SAMPLE_HASH: 8.24 fixed-point value of a sample colour channel."""
     return lib().orc_sample_fixed(c)
 
 

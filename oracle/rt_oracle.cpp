@@ -172,9 +172,9 @@ inline uint32_t sample_seed_hash(uint32_t pixel_seed, uint32_t s) {
     return x;
 }
 
-// RT_RNG_SAMPLE_HASH: a colour channel as 20.44 fixed point, truncated (NaN -> 0).
+// RT_RNG_SAMPLE_HASH: a colour channel as 8.24 fixed point, truncated (NaN -> 0).
 inline uint64_t sample_fixed(float c) {
-    float v = std::fmin(std::fmax(c, 0.0f), 1.0f) * 0x1p44f;
+    float v = std::fmin(std::fmax(c, 0.0f), 1.0f) * 0x1p24f;
     return uint64_t(v);
 }
 
@@ -434,7 +434,7 @@ void render_pixel(const RenderJob& job, uint32_t lx, uint32_t ly, Counters& cnt)
     }
     if (hash) {   // float accumulator in + fixed-point sum, rounded once to float
         for (int k = 0; k < 3; k++)
-            sum[k] = double(job.opt.accumulate ? acc[k] : 0.0f) + double(q[k]) * 0x1p-44;
+            sum[k] = double(job.opt.accumulate ? acc[k] : 0.0f) + double(q[k]) * 0x1p-24;
     }
     float s0 = float(sum[0]), s1 = float(sum[1]), s2 = float(sum[2]);
     acc[0] = s0; acc[1] = s1; acc[2] = s2; acc[3] = 1.0f;          // shader.rgen:63

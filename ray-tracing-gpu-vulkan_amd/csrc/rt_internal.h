@@ -91,7 +91,7 @@ enum : uint32_t { ACCEL_BRUTE = 1, ACCEL_LBVH_GLOBAL = 2, ACCEL_LBVH_LDS = 3, AC
 //           counter restart per sample (RT_RNG_SAMPLE_COUNTER); dvec3 sum per pixel
 //           (shader.rgen:55), one lane runs all samples of a pixel.
 //   HASH:   RT_RNG_SAMPLE_HASH: sample s restarts the LCG at sample_seed(pixel_seed, s); per-sample
-//           colours summed as 20.44 fixed point with integer atomics, so a pixel's samples may be
+//           colours summed as 8.24 fixed point with integer atomics, so a pixel's samples may be
 //           split into chunks on any lanes / GPUs in any order and the sum is the same bits.
 enum : int { MODE_STREAM = 0, MODE_HASH = 1 };
 
@@ -180,9 +180,11 @@ struct TraceParams {
 };
 
 // HASH mode fixed point: a sample colour channel c in [0, 1] (every colour and the sky are <= 1,
-// so is every product of them) adds trunc(c * 2^44) (rt_kernels.hip sample_fixed); a launch may sum
-// up to 2^19 samples per pixel without overflow.
-constexpr int kFixedFracBits = 44;
+// so is every product of them) adds trunc(c * 2^24) (rt_kernels.hip sample_fixed). A lane sums its
+// samples in 32 bits and adds the partial to the pixel's 64-bit sum whenever its next sample index
+// is a multiple of kFixedFlush, and at the end of its unit: a partial holds <= 128 * 2^24 = 2^31.
+constexpr int kFixedFracBits = 24;
+constexpr uint32_t kFixedFlush = 128;
 
 // "Big" spheres (radius above a scene-relative threshold, e.g. the ground sphere) are tested by
 // every segment before the tree walk; at most kBigMax of them. The LBVH kernels stage their

@@ -240,7 +240,8 @@ __device__ __forceinline__ Camera load_camera(const rt::TraceParams& P) {
 }
 
 // One lane's work unit: samples [s, s_end) of pixel px. STREAM sums in double (the dvec3 of
-// shader.rgen:55); HASH sums 20.44 fixed point (q).
+// shader.rgen:55); HASH sums 8.24 fixed point (q) over at most kFixedFlush samples, then adds the
+// partial to the pixel's 64-bit sum in HBM.
 struct Path {
     uint32_t px;           // lx | ly << 16 (band-local launch id)
     uint32_t pixel_seed;   // TEA(TEA(x, y), number)
@@ -250,7 +251,7 @@ struct Path {
     uint32_t segs;         // segments traced for this unit (tile cost for the hand-out order)
     V3 thr;                // reflectedColor (shader.rgen:71)
     double sx, sy, sz;     // STREAM: dvec3 sum
-    unsigned long long qx, qy, qz;   // HASH: fixed-point sum
+    uint32_t qx, qy, qz;   // HASH: fixed-point partial sum since the last flush
 };
 
 // Global load of a rarely taken branch, waited for at once. vmcnt counts loads and stores alike
@@ -284,12 +285,25 @@ __device__ __forceinline__ uint32_t sample_seed_hash(uint32_t pixel_seed, uint32
     return x;
 }
 
-// RT_RNG_SAMPLE_HASH accumulation: a colour channel in [0, 1] as 20.44 fixed point, truncated
-// (rt_internal.h kFixedFracBits). Integer sums are associative, so the order in which chunks of a
-// pixel land does not change a bit. The clamp only defines NaN (-> 0); colours lie in [0, 1].
-__device__ __forceinline__ unsigned long long sample_fixed(float c) {
-    const float v = fminf(fmaxf(c, 0.0f), 1.0f) * 0x1p44f;
-    return (unsigned long long)v;
+// RT_RNG_SAMPLE_HASH accumulation: a colour channel in [0, 1] as 8.24 fixed point, truncated
+// (rt_internal.h kFixedFracBits). Integer sums are associative, so the order in which chunks and
+// partial sums of a pixel land does not change a bit. The clamp only defines NaN (-> 0); colours
+// lie in [0, 1].
+__device__ __forceinline__ uint32_t sample_fixed(float c) {
+    const float v = fminf(fmaxf(c, 0.0f), 1.0f) * 0x1p24f;
+    return uint32_t(v);
+}
+
+// Adds a lane's partial fixed-point sums to its pixel's 64-bit sums in HBM (fire-and-forget
+// relaxed atomics) and clears them; rt_resolve_fixed_kernel stores the pixel.
+__device__ __forceinline__ void flush_fixed(const rt::TraceParams& P, Path& ps) {
+    const uint32_t lx = ps.px & 0xffffu, ly = ps.px >> 16;
+    const size_t n = size_t(P.band_w) * P.band_h, texel = size_t(ly) * P.band_w + lx;
+    __hip_atomic_fetch_add(P.fixed + texel, (unsigned long long)ps.qx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(P.fixed + n + texel, (unsigned long long)ps.qy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(P.fixed + 2 * n + texel, (unsigned long long)ps.qz, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    ps.qx = ps.qy = ps.qz = 0u;
 }
 
 // shader.rgen:40 seed of pixel w (0..63) of 8x8 tile t of the band.
@@ -350,7 +364,7 @@ __device__ __forceinline__ void begin_unit(const rt::TraceParams& P, Path& ps, u
     ps.s_end = s1;
     ps.segs = 0;
     if (MODE == rt::MODE_HASH) {
-        ps.qx = ps.qy = ps.qz = 0ull;
+        ps.qx = ps.qy = ps.qz = 0u;
     } else if (P.accumulate) {  // shader.rgen:53-55
         const float4 acc = load_now4(reinterpret_cast<const float4*>(P.accum) + size_t(ly) * P.band_w + lx);
         ps.sx = acc.x; ps.sy = acc.y; ps.sz = acc.z;
@@ -442,16 +456,12 @@ __device__ __forceinline__ void store_pixel(const rt::TraceParams& P, const Path
     P.out[texel] = r8 | (g8 << 8) | (b8 << 16) | (255u << 24);
 }
 
-// Finished unit. STREAM: the unit is the whole pixel: store it. HASH: add the chunk's fixed-point
-// sum to the pixel's (fire-and-forget 64-bit atomics); rt_resolve_kernel stores the pixel.
+// Finished unit. STREAM: the unit is the whole pixel: store it. HASH: flush the chunk's remaining
+// partial fixed-point sum.
 template <int MODE>
-__device__ __forceinline__ void finish_unit(const rt::TraceParams& P, const Path& ps) {
+__device__ __forceinline__ void finish_unit(const rt::TraceParams& P, Path& ps) {
     if (MODE == rt::MODE_HASH) {
-        const uint32_t lx = ps.px & 0xffffu, ly = ps.px >> 16;
-        const size_t n = size_t(P.band_w) * P.band_h, texel = size_t(ly) * P.band_w + lx;
-        __hip_atomic_fetch_add(P.fixed + texel, ps.qx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(P.fixed + n + texel, ps.qy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(P.fixed + 2 * n + texel, ps.qz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (ps.qx | ps.qy | ps.qz) flush_fixed(P, ps);
     } else {
         store_pixel(P, ps);
     }
@@ -585,16 +595,18 @@ __device__ __forceinline__ bool shade(const rt::TraceParams& P, const float4* __
     } else {
         col = mul(ps.thr, att);
     }
+    ps.s++;
     if (MODE == rt::MODE_HASH) {
         ps.qx += sample_fixed(col.x);
         ps.qy += sample_fixed(col.y);
         ps.qz += sample_fixed(col.z);
+        // a partial never spans a multiple of kFixedFlush samples: <= kFixedFlush * 2^24 < 2^32
+        if ((ps.s & (rt::kFixedFlush - 1u)) == 0u) flush_fixed(P, ps);
     } else {
         ps.sx += double(col.x);
         ps.sy += double(col.y);
         ps.sz += double(col.z);
     }
-    ps.s++;
     return false;
 }
 
@@ -929,7 +941,9 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
     uint32_t st = ST_NEED_UNIT;
     Path ps{};
     Ray r{};
-    uint32_t n_seg = 0, n_smp = 0, n_box = 0, n_sph = 0;
+    // traced segments and started samples of this wave (wave-uniform: ballot counts, no per-lane
+    // registers); per-lane test counters in COUNT builds only
+    uint32_t seg_w = 0, smp_w = 0, n_box = 0, n_sph = 0;
     unsigned long long wave_iters = 0;
     bool saw_dry = false;
     WaveBlock blk;
@@ -945,18 +959,21 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
             if (lane == 0) atomicMin(&P.counters->t_dry, __builtin_amdgcn_s_memrealtime());
         }
         STAMP(4);
+        bool started = false;
         if (st == ST_NEED_SAMPLE) {
             if (start_sample<MODE>(P, cam, ps, r.o, r.d)) {
                 st = ST_TRACING;
-                n_smp++;
+                started = true;
             } else {   // empty unit (spp = 0): stored at once
                 st = ST_NEED_UNIT;
                 record_tile_cost(P, ps);
             }
         }
+        smp_w += __popcll(__ballot(started));
         if (__ballot(st == ST_NEED_UNIT)) continue;   // refill before the next trace
         const unsigned long long tracing = __ballot(st == ST_TRACING);
         if (!tracing) break;                           // every lane retired
+        seg_w += __popcll(tracing);
         if (COUNT && lane == 0) atomicAdd(&P.counters->lane_hist[__popcll(tracing)], 1ull);
         STAMP(1);
         UTIL(8, st == ST_TRACING);
@@ -975,7 +992,6 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
         }
         STAMP(3);
         if (st == ST_TRACING) {
-            n_seg++;
             ps.segs++;
             if (!shade<MODE>(P, geom4, mat4, ps, r.bi, r.best, r.o, r.d)) {
                 // The sample ended. After the unit's last one, finish it here rather than at the
@@ -992,9 +1008,11 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
         }
     }
     STAMP_FLUSH;
-    atomicAdd(&P.counters->segments, (unsigned long long)n_seg);
-    atomicAdd(&P.counters->samples, (unsigned long long)n_smp);
-    if (lane == 0) atomicMax(&P.counters->t_last, __builtin_amdgcn_s_memrealtime());
+    if (lane == 0) {
+        atomicAdd(&P.counters->segments, (unsigned long long)seg_w);
+        atomicAdd(&P.counters->samples, (unsigned long long)smp_w);
+        atomicMax(&P.counters->t_last, __builtin_amdgcn_s_memrealtime());
+    }
     if (COUNT) {
         atomicAdd(&P.counters->box_tests, (unsigned long long)n_box);
         atomicAdd(&P.counters->sphere_tests, (unsigned long long)n_sph);
@@ -1114,9 +1132,9 @@ __global__ __launch_bounds__(256) void rt_resolve_fixed_kernel(unsigned long lon
         fixed[n + i] = 0ull;
         fixed[2 * n + i] = 0ull;
         const float4 a = accumulate ? accum[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        const float s0 = float(double(a.x) + double(q0) * 0x1p-44);
-        const float s1 = float(double(a.y) + double(q1) * 0x1p-44);
-        const float s2 = float(double(a.z) + double(q2) * 0x1p-44);
+        const float s0 = float(double(a.x) + double(q0) * 0x1p-24);
+        const float s1 = float(double(a.y) + double(q1) * 0x1p-24);
+        const float s2 = float(double(a.z) + double(q2) * 0x1p-24);
         accum[i] = make_float4(s0, s1, s2, 1.0f);
         out[i] = unorm8(__builtin_sqrtf(s0 / spp)) | (unorm8(__builtin_sqrtf(s1 / spp)) << 8) |
                  (unorm8(__builtin_sqrtf(s2 / spp)) << 16) | (255u << 24);
@@ -1167,8 +1185,8 @@ __global__ void rt_debug_math_kernel(int op, const float* __restrict__ in, float
         case 4: { V3 v = normalize(v3(x, y, 0.5f)); r = v.x; break; }
         case 5: r = pow5(x); break;
         case 6: r = __uint_as_float(sample_seed_hash(__float_as_uint(x), __float_as_uint(y))); break;
-        case 7: { const unsigned long long q = sample_fixed(x); r = __uint_as_float(uint32_t(q)); break; }
-        case 8: { const unsigned long long q = sample_fixed(x); r = __uint_as_float(uint32_t(q >> 32)); break; }
+        case 7: r = __uint_as_float(sample_fixed(x)); break;
+        case 8: r = 0.0f; break;   // high word of the (32-bit) per-sample value
         case 9: r = checker_positive(x, y, 0.5f * (x - y)) ? 1.0f : 0.0f; break;
         default: r = 0.0f;
     }

@@ -184,7 +184,7 @@ def test_checker_decision_bit_exact(rtvk, torch, oracle):
 
 
 def test_hash_primitives_bit_exact(rtvk, torch, oracle):
-    """RT_RNG_SAMPLE_HASH primitives: the sample-seed hash (bit patterns) and the 20.44 fixed-point
+    """RT_RNG_SAMPLE_HASH primitives: the sample-seed hash (bit patterns) and the 8.24 fixed-point
     conversion of a colour channel (low / high words), device vs oracle."""
     rng = np.random.default_rng(11)
     ps = rng.integers(0, 2**32, 4000, dtype=np.uint64).astype(np.uint32)
@@ -193,7 +193,7 @@ def test_hash_primitives_bit_exact(rtvk, torch, oracle):
     ref = np.array([oracle.sample_seed_hash(int(a), int(b)) for a, b in zip(ps, sm)], np.uint32)
     np.testing.assert_array_equal(got, ref)
     c = np.concatenate([rng.uniform(0, 1, 3000), 10.0 ** rng.uniform(-40, 0, 3000),
-                        [0.0, 1.0, -1.0, 2.0, np.nan, np.inf, 2.0 ** -44, 2.0 ** -45]]).astype(np.float32)
+                        [0.0, 1.0, -1.0, 2.0, np.nan, np.inf, 2.0 ** -24, 2.0 ** -25]]).astype(np.float32)
     lo = _debug_math(rtvk, 7, c, np.zeros_like(c)).view(np.uint32).astype(np.uint64)
     hi = _debug_math(rtvk, 8, c, np.zeros_like(c)).view(np.uint32).astype(np.uint64)
     ref = np.array([oracle.sample_fixed(float(v)) for v in c], np.uint64)

@@ -199,15 +199,15 @@ def test_sample_seed_hash(oracle):
 
 
 def test_sample_fixed(oracle):
-    """trunc(clamp(c, 0, 1) * 2^44): exact for representable products, NaN -> 0."""
+    """trunc(clamp(c, 0, 1) * 2^24): exact for representable products, NaN -> 0."""
     rng = np.random.default_rng(3)
     cs = np.concatenate([rng.uniform(0, 1, 500), 10.0 ** rng.uniform(-40, 0, 500)]).astype(np.float32)
     for c in cs:
-        assert oracle.sample_fixed(float(c)) == int(np.float32(c) * np.float32(2.0 ** 44))
-    assert oracle.sample_fixed(1.0) == 2 ** 44
-    assert oracle.sample_fixed(0.0) == 0 and oracle.sample_fixed(-0.5) == 0 and oracle.sample_fixed(3.0) == 2 ** 44
+        assert oracle.sample_fixed(float(c)) == int(np.float32(c) * np.float32(2.0 ** 24))
+    assert oracle.sample_fixed(1.0) == 2 ** 24
+    assert oracle.sample_fixed(0.0) == 0 and oracle.sample_fixed(-0.5) == 0 and oracle.sample_fixed(3.0) == 2 ** 24
     assert oracle.sample_fixed(float("nan")) == 0
-    assert oracle.sample_fixed(2.0 ** -45) == 0 and oracle.sample_fixed(2.0 ** -44) == 1
+    assert oracle.sample_fixed(2.0 ** -25) == 0 and oracle.sample_fixed(2.0 ** -24) == 1
 
 
 def test_hash_mode_frame(oracle):
