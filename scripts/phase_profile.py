@@ -16,9 +16,9 @@ from rtvk import abi  # noqa: E402
 
 spp = int(sys.argv[1]) if len(sys.argv) > 1 else 200
 rng = rtvk.HASH if (sys.argv[2] if len(sys.argv) > 2 else "hash") == "hash" else rtvk.STREAM
-W, H = 1920, 1080
+W, H, K = (int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])) if len(sys.argv) > 5 else (1920, 1080, 11)
 r = rtvk.Renderer(0)
-r.set_scene(rtvk.generateRandomScene())
+r.set_scene(rtvk.generateRandomScene(0.0, K))
 acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
 out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
 rci = rtvk.canonical_render_call_info(spp, W, H)
