@@ -21,6 +21,7 @@
 #include "../../include/rt_mi355x.h"
 #include "rt_build.h"
 #include "rt_bvh.h"
+#include "rt_grid.h"
 #include "rt_host.h"
 #include "rt_internal.h"
 
@@ -57,6 +58,9 @@ struct rt_context {
     size_t occ_lds[rt::ACCEL_COUNT][2][2] = {};
     size_t lds1_bytes = 0;                       // one node copy + leaves + big table (0: no fit)
     size_t oct_bytes = 0;                        // 8 octant node copies + leaves + big table (0: no fit)
+    size_t grid_bytes = 0;                       // grid references + offsets + big table (0: no grid / no fit)
+    bool has_grid = false;                       // the scene has a grid (staged in LDS when grid_bytes)
+    float grid_pad_radius = 0.0f;                // camera radius the grid's margin covers
     // unpadded LBVH node boxes (host) and the radius the device copy is padded for
     std::vector<rt::BvhNode> nodes_host;
     float scene_radius = 0.0f;
@@ -156,12 +160,17 @@ void size_lds_forms(rt_context* ctx) {
     ctx->lds1_bytes = (ok && lds1 <= kMaxLdsBytes) ? lds1 : 0;
     const size_t oct = lds1 + size_t(14u) * d.n_nodes * 16u;
     ctx->oct_bytes = (ok && oct <= kMaxLdsBytes) ? oct : 0;
+    const rt::GridInfo& g = d.grid;
+    const size_t grid = (size_t(g.n_refs) + (g.n_refs + 3) / 4 + (size_t(g.n_cells) + 4) / 4) * 16 + rt::kBigLdsBytes;
+    ctx->grid_bytes = (g.n_refs && grid <= kMaxLdsBytes) ? grid : 0;
 }
 
 void free_scene(rt_context* ctx) {
     for (void* p : ctx->scene_allocs) (void)hipFree(p);
     ctx->scene_allocs.clear();
     ctx->scene = rt::DeviceScene{};
+    ctx->has_grid = false;
+    ctx->grid_bytes = 0;
 }
 
 // Stream chaining of a context's device operations (rt_context::ev_last).
@@ -443,6 +452,7 @@ int set_scene_host(rt_context* ctx, const Sphere* spheres, uint32_t count, hipSt
             free_scene(ctx);
         }
         ctx->scene = rt::DeviceScene{};
+        ctx->has_grid = false;
         ctx->gpu_tree = false;
         BlobUpload up;
         std::vector<rt::GeomRec> geom(count);
@@ -487,6 +497,21 @@ int set_scene_host(rt_context* ctx, const Sphere* spheres, uint32_t count, hipSt
         std::vector<rt::BvhNode> oct;
         make_octant_orders(bvh.nodes, oct);
         up.add(oct, &d.nodes_oct);
+        // Uniform grid (rt_grid.h) when the scene suits one: the default walk.
+        // RT_GRID=0 disables it, RT_GRID_SCALE scales the cell size (A/B).
+        rt::HostGrid grid;
+        const char* ge = std::getenv("RT_GRID");
+        const float gscale = std::getenv("RT_GRID_SCALE") ? float(std::atof(std::getenv("RT_GRID_SCALE"))) : 2.2f;
+        if (!(ge && std::strcmp(ge, "0") == 0) &&
+            rt::build_grid_host(spheres, count, bvh.big_ids, 64.0f * 0x1p-24f * ctx->pad_radius, gscale, 1u << 22,
+                                grid)) {
+            d.grid = grid.info;
+            up.add(grid.cell_start, &d.cell_start);
+            up.add(grid.rec, &d.grid_rec);
+            up.add(grid.ids, &d.grid_ids);
+            ctx->grid_pad_radius = ctx->pad_radius;
+            ctx->has_grid = true;
+        }
         size_lds_forms(ctx);
         up.add(bvh.nodes, &d.nodes);
         up.add(bvh.leaf_geom, &d.leaf_geom);
@@ -541,6 +566,36 @@ int set_scene_gpu(rt_context* ctx, const Sphere* d_sph, uint32_t count, hipStrea
     ctx->scene_radius = rt::summary_float(sm.R_o);
     ctx->pad_radius = ctx->scene_radius * 1.01f + 100.0f;   // the build padded for this radius
     ctx->padded_for = ctx->pad_radius;
+    // Uniform grid over the small spheres (the default walk), built on the device
+    // from the tree's root box (the small spheres' AABB union). RT_GRID=0 disables it.
+    ctx->has_grid = false;
+    d.grid = rt::GridInfo{};
+    const char* ge = std::getenv("RT_GRID");
+    if (!(ge && std::strcmp(ge, "0") == 0) && sm.n_small && d.small_rmax > 0.0f) {
+        rt::BvhNode root;
+        RT_HIP(hipMemcpy(&root, d.nodes_raw, sizeof(root), hipMemcpyDeviceToHost));
+        const float lo[3] = {root.lox, root.loy, root.loz}, hi[3] = {root.hix, root.hiy, root.hiz};
+        const char* gs = std::getenv("RT_GRID_SCALE");
+        rt::GridInfo gi;
+        uint64_t bound = 0;
+        if (rt::grid_layout(lo, hi, sm.n_small, d.small_rmax, 64.0f * 0x1p-24f * ctx->pad_radius,
+                            gs ? float(std::atof(gs)) : 2.2f, gi, &bound) && bound <= (1u << 26)) {
+            uint32_t* cursor = nullptr;
+            void* tmp = nullptr;
+            const size_t tb = rt::grid_scan_bytes(gi.n_cells);
+            if (int rc = scene_alloc(ctx, &d.cell_start, size_t(gi.n_cells) + 1)) return rc;
+            if (int rc = scene_alloc(ctx, &cursor, size_t(gi.n_cells) + 1)) return rc;
+            if (int rc = scene_alloc(ctx, &d.grid_rec, size_t(bound))) return rc;
+            if (int rc = scene_alloc(ctx, &d.grid_ids, size_t(bound))) return rc;
+            if (int rc = scene_alloc(ctx, reinterpret_cast<uint8_t**>(&tmp), tb)) return rc;
+            RT_HIP(rt::build_grid_gpu(ctx->ws, d_sph, count, gi, cursor, d.cell_start, d.grid_rec, d.grid_ids, tmp,
+                                      tb, st));
+            gi.n_refs = 0;   // exact count left on the device: the grid is walked from L2
+            d.grid = gi;
+            ctx->has_grid = true;
+            ctx->grid_pad_radius = ctx->pad_radius;
+        }
+    }
     ctx->nodes_host.clear();
     size_lds_forms(ctx);
     return RT_OK;
@@ -676,8 +731,14 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     const rt::DeviceScene& d = ctx->scene;
     uint32_t accel;
     size_t lds = 0;
+    const float cam_r = std::sqrt(rci->camera_pos.x * rci->camera_pos.x + rci->camera_pos.y * rci->camera_pos.y +
+                                  rci->camera_pos.z * rci->camera_pos.z);
     if (o.accel == RT_ACCEL_BRUTE) {
         accel = rt::ACCEL_BRUTE;
+    } else if (ctx->has_grid && cam_r <= ctx->grid_pad_radius && (form == 0u || form == 12u)) {
+        // the grid; its margin covers cameras within its pad radius
+        accel = ctx->grid_bytes ? rt::ACCEL_GRID : rt::ACCEL_GRID_GLOBAL;
+        lds = ctx->grid_bytes ? ctx->grid_bytes : rt::kBigLdsBytes;
     } else if (ctx->oct_bytes && (form == 0u || form == 8u)) {
         accel = rt::ACCEL_LBVH_OCT;
         lds = ctx->oct_bytes;
@@ -724,6 +785,12 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     P.nodes_oct = d.nodes_oct;
     P.treelet = d.treelet;
     P.treelet_count = d.treelet_count;
+    if (accel == rt::ACCEL_GRID || accel == rt::ACCEL_GRID_GLOBAL) {   // (cell_start also marks a walk)
+        P.grid = d.grid;
+        P.cell_start = d.cell_start;
+        P.grid_rec = d.grid_rec;
+        P.grid_ids = d.grid_ids;
+    }
     P.n_leaf = d.n_leaf;
     P.leaf_geom = d.leaf_geom;
     P.leaf_ids = d.leaf_ids;
@@ -956,9 +1023,9 @@ int rt_debug_walk_hist(rt_context* ctx, uint64_t* out128) {
 int rt_debug_launch_info(rt_context* ctx, uint32_t* out4) {
     if (!ctx || !out4) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     out4[0] = ctx->last_chunks;
-    out4[1] = ctx->oct_bytes ? rt::ACCEL_LBVH_OCT : ctx->lds1_bytes ? rt::ACCEL_LBVH_LDS
-              : ctx->gpu_tree ? rt::ACCEL_LBVH_TOP : rt::ACCEL_LBVH_GLOBAL;
-    out4[2] = uint32_t(ctx->oct_bytes ? ctx->oct_bytes : ctx->lds1_bytes);
+    out4[1] = ctx->grid_bytes ? rt::ACCEL_GRID : ctx->has_grid ? rt::ACCEL_GRID_GLOBAL : ctx->oct_bytes ? rt::ACCEL_LBVH_OCT
+              : ctx->lds1_bytes ? rt::ACCEL_LBVH_LDS : ctx->gpu_tree ? rt::ACCEL_LBVH_TOP : rt::ACCEL_LBVH_GLOBAL;
+    out4[2] = uint32_t(ctx->grid_bytes ? ctx->grid_bytes : ctx->oct_bytes ? ctx->oct_bytes : ctx->lds1_bytes);
     out4[3] = uint32_t(ctx->cu_count);
     return RT_OK;
 }

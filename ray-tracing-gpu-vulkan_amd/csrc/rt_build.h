@@ -88,4 +88,12 @@ hipError_t repad_nodes_gpu(const BvhNode* raw, BvhNode* nodes, uint32_t n_nodes,
 // kTreeletCap x 8 floats, *out_count receives the node count. Asynchronous on `st`.
 hipError_t build_treelet(const BvhNode* nodes, uint32_t n_nodes, float* out, uint32_t* out_count, hipStream_t st);
 
+// Uniform grid over the small spheres of the last build_scene_gpu (its big flags), layout g from
+// rt_grid.h grid_layout: cell_start (n_cells + 1), references rec / ids (cell-major; order within a
+// cell unspecified), cursor scratch (n_cells + 1), tmp: grid_scan_bytes(n_cells).
+hipError_t build_grid_gpu(const BuildWorkspace& ws, const Sphere* d_spheres, uint32_t n, const GridInfo& g,
+                          uint32_t* cursor, uint32_t* cell_start, GeomRec* rec, uint32_t* ids, void* tmp,
+                          size_t tmp_bytes, hipStream_t st);
+size_t grid_scan_bytes(uint32_t n_cells);
+
 }  // namespace rt

@@ -419,6 +419,39 @@ __global__ void __launch_bounds__(kTreeletThreads) k_treelet(const BvhNode* __re
     if (tid == 0) *out_count = n;
 }
 
+// Uniform grid (rt_grid.h) over the small spheres of a device build: the cell range of sphere i's
+// AABB widened by the margin (the host builder's arithmetic), counted, then filled through a scan.
+__device__ __forceinline__ void grid_range(const GridInfo& g, int k, float c, float r, uint32_t& a, uint32_t& b) {
+    const double x0 = (double(c - r) - g.margin - g.gmin[k]) / g.cs[k];
+    const double x1 = (double(c + r) + g.margin - g.gmin[k]) / g.cs[k];
+    a = uint32_t(fmin(double(g.n[k] - 1), fmax(0.0, floor(x0))));
+    b = uint32_t(fmin(double(g.n[k] - 1), fmax(0.0, floor(x1))));
+}
+
+template <bool FILL>
+__global__ void __launch_bounds__(kBlock) k_grid_refs(const Sphere* __restrict__ sph, uint32_t n,
+                                                      const uint8_t* __restrict__ is_big, const GridInfo g,
+                                                      uint32_t* __restrict__ cnt, GeomRec* __restrict__ rec,
+                                                      uint32_t* __restrict__ ids) {
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n || is_big[i]) return;
+    const rt_vec4 s = sph[i].geometry;
+    uint32_t a[3], b[3];
+    grid_range(g, 0, s.x, s.w, a[0], b[0]);
+    grid_range(g, 1, s.y, s.w, a[1], b[1]);
+    grid_range(g, 2, s.z, s.w, a[2], b[2]);
+    for (uint32_t z = a[2]; z <= b[2]; z++)
+        for (uint32_t y = a[1]; y <= b[1]; y++)
+            for (uint32_t x = a[0]; x <= b[0]; x++) {
+                const uint32_t c = (z * g.n[1] + y) * g.n[0] + x;
+                const uint32_t j = atomicAdd(&cnt[c], 1u);   // FILL: cnt holds each cell's next slot
+                if (FILL) {
+                    rec[j] = GeomRec{s.x, s.y, s.z, s.w};
+                    ids[j] = i;
+                }
+            }
+}
+
 __global__ void __launch_bounds__(kBlock) k_iota(uint32_t* v, uint32_t n) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i < n) v[i] = i;
@@ -567,6 +600,26 @@ hipError_t schedule_order(TileSchedule& s, hipStream_t st) {
 hipError_t build_treelet(const BvhNode* nodes, uint32_t n_nodes, float* out, uint32_t* out_count, hipStream_t st) {
     k_treelet<<<1, kTreeletThreads, 0, st>>>(nodes, n_nodes, reinterpret_cast<float4*>(out), out_count);
     return hipGetLastError();
+}
+
+hipError_t build_grid_gpu(const BuildWorkspace& ws, const Sphere* sph, uint32_t n, const GridInfo& g,
+                          uint32_t* cursor, uint32_t* cell_start, GeomRec* rec, uint32_t* ids, void* tmp,
+                          size_t tmp_bytes, hipStream_t st) {
+    if (!n) return hipSuccess;
+    if (hipError_t e = hipMemsetAsync(cursor, 0, (size_t(g.n_cells) + 1) * 4, st)) return e;
+    k_grid_refs<false><<<blocks(n), kBlock, 0, st>>>(sph, n, ws.is_big, g, cursor, nullptr, nullptr);
+    size_t tb = tmp_bytes;
+    if (hipError_t e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, cursor, cell_start, int(g.n_cells + 1), st)) return e;
+    if (hipError_t e = hipMemcpyAsync(cursor, cell_start, size_t(g.n_cells) * 4, hipMemcpyDeviceToDevice, st)) return e;
+    k_grid_refs<true><<<blocks(n), kBlock, 0, st>>>(sph, n, ws.is_big, g, cursor, rec, ids);
+    return hipGetLastError();
+}
+
+size_t grid_scan_bytes(uint32_t n_cells) {
+    size_t tb = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, static_cast<uint32_t*>(nullptr),
+                                           static_cast<uint32_t*>(nullptr), int(n_cells + 1));
+    return tb;
 }
 
 hipError_t repad_nodes_gpu(const BvhNode* raw, BvhNode* nodes, uint32_t n_nodes, float pad, hipStream_t st) {

@@ -1,0 +1,35 @@
+// rt_grid.h — uniform grid over the scene's small spheres (host build, rt_grid.cpp): the closest-hit
+// structure of the trace kernels for scenes of similar-size spheres, traversed by a 3D DDA
+// (rt_kernels.hip grid_walk). Replaces the driver BVH of src/vulkan.h:395-554 like the LBVH does.
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include "../../include/rt_abi.h"
+#include "rt_internal.h"
+
+namespace rt {
+
+struct HostGrid {
+    GridInfo info{};
+    std::vector<uint32_t> cell_start;   // n_cells + 1 offsets into the reference lists
+    std::vector<GeomRec> rec;           // per reference: center, RADIUS (cell-major, index order)
+    std::vector<uint32_t> ids;          // per reference: sphere index
+};
+
+// Builds the grid over the spheres not in `big` (tested exhaustively by the kernels). Every sphere
+// is referenced by each cell its AABB, widened by `margin` + 1e-3 cell, overlaps (info.margin).
+// Returns false when the scene does not suit a grid: no small spheres, radii spread over more than
+// a factor 8, non-finite spheres, or more than `max_refs` references.
+bool build_grid_host(const Sphere* spheres, uint32_t n, const std::vector<uint32_t>& big, float margin,
+                     float cell_scale, uint32_t max_refs, HostGrid& out);
+
+// The grid's layout for m small spheres of radius <= rmax whose AABBs span [lo, hi] (shared by the
+// host build and the device build, rt_build.hip build_grid_gpu). Returns false when the cell count
+// would exceed 2^24. *ref_bound = references at most (each sphere's widened AABB spans at most
+// ceil((2 rmax + 2 margin) / cs) + 1 cells per axis).
+bool grid_layout(const float lo[3], const float hi[3], uint32_t m, float rmax, float margin, float cell_scale,
+                 GridInfo& gi, uint64_t* ref_bound);
+
+}  // namespace rt

@@ -56,6 +56,18 @@ struct alignas(16) BvhNode {
     uint32_t first_count;        // leaf: first << 4 | count (count 1..15); inner: 0
 };
 
+// Uniform grid over the small spheres (rt_grid.h): cell (x, y, z) is index (z * n[1] + y) * n[0] + x,
+// its references cell_start[c] .. cell_start[c + 1] into grid_rec / grid_ids.
+struct GridInfo {
+    float gmin[3];      // min corner
+    float gmax[3];      // max corner (gmin + n * cs)
+    float cs[3];        // cell size per axis
+    float inv_cs[3];    // 1 / cs (cell of the entry point)
+    float margin;       // registration margin (the entry box is widened by it too)
+    uint32_t n[3];      // cells per axis
+    uint32_t n_cells, n_refs;
+};
+
 // Scene as resident in HBM (one allocation per context, rebuilt by rt_set_scene).
 struct DeviceScene {
     uint32_t n_spheres = 0;
@@ -77,6 +89,10 @@ struct DeviceScene {
     float* treelet = nullptr;      // device-built trees: kTreeletCap x 8 floats (ACCEL_LBVH_TOP)
     uint32_t* treelet_count = nullptr;   // device word: nodes in the treelet
     float small_rmax = 0.0f;       // largest radius in the tree
+    GridInfo grid{};               // host-built scenes that suit a grid (n_refs = 0: none)
+    uint32_t* cell_start = nullptr;
+    GeomRec* grid_rec = nullptr;
+    uint32_t* grid_ids = nullptr;
 };
 
 // Trace kernel forms (rt_kernels.hip pick()). Production: BRUTE (BASELINE config 2), OCT (trees
@@ -84,7 +100,7 @@ struct DeviceScene {
 // scene records in LDS), TOP (bigger trees: LDS treelet + L2 subtrees). GLOBAL (every node from
 // L2) is the A/B reference of TOP (options.reserved[1] = 10).
 enum : uint32_t { ACCEL_BRUTE = 1, ACCEL_LBVH_GLOBAL = 2, ACCEL_LBVH_LDS = 3, ACCEL_LBVH_OCT = 4,
-                  ACCEL_LBVH_TOP = 5, ACCEL_COUNT = 6 };
+                  ACCEL_LBVH_TOP = 5, ACCEL_GRID = 6, ACCEL_GRID_GLOBAL = 7, ACCEL_COUNT = 8 };
 
 // Random stream layout of a launch (template parameter of the trace kernels).
 //   STREAM: the reference's per-pixel LCG stream (random.glsl), or with rng_counter the TEA
@@ -172,6 +188,10 @@ struct TraceParams {
     const uint32_t* leaf_ids;
     float cull_abs;                // LBVH node-cull slack: best + cull_abs + cull_rel * best
     float cull_rel;
+    GridInfo grid;                 // ACCEL_GRID
+    const uint32_t* cell_start;
+    const GeomRec* grid_rec;
+    const uint32_t* grid_ids;
     // outputs
     float* accum;                  // STREAM: band_w * band_h * 4 floats
     uint32_t* out;                 // STREAM: band_w * band_h packed rgba8

@@ -206,6 +206,31 @@ __device__ __forceinline__ void test4(const float4 s0, const float4 s1, const fl
     }
 }
 
+// One sphere (a grid cell's reference): test4's arithmetic for a single record.
+__device__ __forceinline__ void test1(const float4 sp, const uint32_t* __restrict__ id_at, V3 o, V3 d, V3 inv,
+                                      float a, float ia, float& best, uint32_t& bi, float& limit, float cull_abs,
+                                      float cull_rel) {
+    const float rr = sp.w * sp.w;
+    const float ocx = o.x - sp.x, ocy = o.y - sp.y, ocz = o.z - sp.z;
+    const float b = __builtin_fmaf(ocz, d.z, __builtin_fmaf(ocy, d.y, ocx * d.x));
+    const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - rr;
+    const float D = __builtin_fmaf(b, b, -(a * c));
+    if (D >= 0.0f) {
+        UTIL(2, true);
+        const float sq = sqrt_cr(D);
+        float t = (-b - sq) * ia;
+        if (!(t >= T_MIN)) t = (-b + sq) * ia;     // report t1 if t1 >= tmin, else t2
+        if (t >= T_MIN && t <= best) {
+            const uint32_t id = *id_at;
+            if ((t < best || id < bi) && aabb_hit(sp.x, sp.y, sp.z, sp.w, o, inv)) {
+                best = t;
+                bi = id;
+                limit = fminf(__builtin_fmaf(t, cull_rel, t + cull_abs), 10000.0f);
+            }
+        }
+    }
+}
+
 // Brute force: every lane tests every sphere. The sphere index is wave-uniform, so the geometry
 // comes through the scalar cache: 8 spheres (128 B) per iteration as two s_load_dwordx16 issued
 // before any of the 8 tests, feeding the VALU as SGPR operands (13 VALU per sphere, no VGPR
@@ -701,7 +726,7 @@ constexpr uint32_t END = 0xffffffffu;
 // Walk forms (template LAYOUT): GLOBAL = escape-link BvhNode pairs from L2 (A/B reference of TOP),
 // LDS1 = one node copy in LDS (AB layout), OCT = 8 octant-specialised copies in LDS, TOP = LDS
 // treelet over L2 subtrees.
-enum : int { LAYOUT_GLOBAL = 0, LAYOUT_LDS1 = 1, LAYOUT_OCT = 2, LAYOUT_TOP = 3 };
+enum : int { LAYOUT_GLOBAL = 0, LAYOUT_LDS1 = 1, LAYOUT_OCT = 2, LAYOUT_TOP = 3, LAYOUT_GRID = 4 };
 
 // Node slab test: one fma per plane, t = fma(plane, inv, -o * inv) (a sub-then-mul form is exact
 // in the gate's own arithmetic but costs twice the issue cycles: packed f32 ops take 4 cycles on
@@ -790,7 +815,7 @@ __device__ __forceinline__ void setup_ray(const rt::TraceParams& P, const BigTab
     }
     n_sph += P.n_big;
     r.limit = fminf(__builtin_fmaf(r.best, P.cull_rel, r.best + P.cull_abs), 10000.0f);
-    r.walk = P.nodes != nullptr;
+    r.walk = P.nodes != nullptr || P.cell_start != nullptr;
 }
 
 // Leaf of 4 slots (dummy-padded), loads issued together; the candidate loop reloads a record
@@ -840,11 +865,83 @@ __device__ __forceinline__ void walk_global_range(const rt::TraceParams& P, cons
     }
 }
 
+// Uniform-grid walk (ACCEL_GRID, rt_grid.h): a 3D DDA from the ray's entry into the grid box
+// (widened by the registration margin, over [tmin, limit], in the AABB gate's arithmetic) through
+// the cells in order of t, testing each cell's references, until the next cell starts beyond the
+// cull limit or the ray leaves the grid. Every cell boundary's t is computed afresh from the cell
+// coordinate (no accumulated rounding), so the cells visited cover the ray up to rounding distance
+// of the boundaries, which the margin covers. Ties step one axis at a time (an
+// extra cell, never a skipped one).
+template <bool COUNT>
+__device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32_t* __restrict__ cstart,
+                                          const float4* __restrict__ rec, const uint32_t* __restrict__ ids,
+                                          Ray& r, uint32_t& n_cell, uint32_t& n_sph) {
+    const rt::GridInfo& G = P.grid;
+    const float x0 = ((G.gmin[0] - G.margin) - r.o.x) * r.inv.x, x1 = ((G.gmax[0] + G.margin) - r.o.x) * r.inv.x;
+    const float y0 = ((G.gmin[1] - G.margin) - r.o.y) * r.inv.y, y1 = ((G.gmax[1] + G.margin) - r.o.y) * r.inv.y;
+    const float z0 = ((G.gmin[2] - G.margin) - r.o.z) * r.inv.z, z1 = ((G.gmax[2] + G.margin) - r.o.z) * r.inv.z;
+    const float tn = fmaxf(fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1)), T_MIN);
+    const float tf = fminf(fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1)), r.limit);
+    if (!(tn <= tf)) return;
+    // entry cell (clamped: a point rounded just outside belongs to the border cell)
+    auto cell_of = [&](float p, int k) {
+        const int c = int(floorf((p - G.gmin[k]) * G.inv_cs[k]));
+        return min(max(c, 0), int(G.n[k]) - 1);
+    };
+    int cx = cell_of(__builtin_fmaf(tn, r.d.x, r.o.x), 0);
+    int cy = cell_of(__builtin_fmaf(tn, r.d.y, r.o.y), 1);
+    int cz = cell_of(__builtin_fmaf(tn, r.d.z, r.o.z), 2);
+    const int sx = r.d.x > 0.0f ? 1 : (r.d.x < 0.0f ? -1 : 0);
+    const int sy = r.d.y > 0.0f ? 1 : (r.d.y < 0.0f ? -1 : 0);
+    const int sz = r.d.z > 0.0f ? 1 : (r.d.z < 0.0f ? -1 : 0);
+    // t of the boundary ahead on each axis (+inf on an axis the ray does not move along)
+    auto bound_t = [&](int c, int s, int k, float o, float inv) {
+        const float plane = __builtin_fmaf(float(c + (s > 0 ? 1 : 0)), G.cs[k], G.gmin[k]);
+        return s == 0 ? __builtin_inff() : (plane - o) * inv;
+    };
+    float tx = bound_t(cx, sx, 0, r.o.x, r.inv.x);
+    float ty = bound_t(cy, sy, 1, r.o.y, r.inv.y);
+    float tz = bound_t(cz, sz, 2, r.o.z, r.inv.z);
+    // linear cell index and its per-axis steps (no multiplies in the loop)
+    uint32_t cell = (uint32_t(cz) * G.n[1] + uint32_t(cy)) * G.n[0] + uint32_t(cx);
+    const int dxc = sx, dyc = sy * int(G.n[0]), dzc = sz * int(G.n[0] * G.n[1]);
+    for (;;) {
+        const uint32_t b = cstart[cell], e = cstart[cell + 1];
+        if (COUNT) n_cell++;
+        for (uint32_t j = b; j < e; ++j) {
+            UTIL(1, true);
+            test1(rec[j], ids + j, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P.cull_abs, P.cull_rel);
+            if (COUNT) n_sph++;
+        }
+        UTIL(0, true);
+        const float tm = fminf(fminf(tx, ty), tz);
+        if (!(tm <= r.limit)) break;   // the next cell starts beyond every closer candidate
+        // step the axis whose boundary comes first (x before y before z on ties), branch-free
+        const bool mx = tx == tm, my = !mx && ty == tm, mz = !mx && !my;
+        cx += mx ? sx : 0;
+        cy += my ? sy : 0;
+        cz += mz ? sz : 0;
+        if (uint32_t(cx) >= G.n[0] || uint32_t(cy) >= G.n[1] || uint32_t(cz) >= G.n[2]) break;
+        cell += mx ? dxc : my ? dyc : dzc;
+        const int c = mx ? cx : my ? cy : cz, s = mx ? sx : my ? sy : sz;
+        const float csk = mx ? G.cs[0] : my ? G.cs[1] : G.cs[2], g0 = mx ? G.gmin[0] : my ? G.gmin[1] : G.gmin[2];
+        const float ok = mx ? r.o.x : my ? r.o.y : r.o.z, ik = mx ? r.inv.x : my ? r.inv.y : r.inv.z;
+        const float tnew = (__builtin_fmaf(float(c + (s > 0 ? 1 : 0)), csk, g0) - ok) * ik;
+        tx = mx ? tnew : tx;
+        ty = my ? tnew : ty;
+        tz = mz ? tnew : tz;
+    }
+}
+
 // The whole walk of one segment.
 template <bool COUNT, int LAYOUT>
 __device__ __forceinline__ void walk(const rt::TraceParams& P, const float4* __restrict__ nodes4,
                                      const float4* __restrict__ leaf4, const uint32_t* __restrict__ leaf_ids,
                                      Ray& r, uint32_t& n_box, uint32_t& n_sph) {
+    if (LAYOUT == LAYOUT_GRID) {   // nodes4 = cell offsets, leaf4 / leaf_ids = references
+        if (r.walk) grid_walk<COUNT>(P, reinterpret_cast<const uint32_t*>(nodes4), leaf4, leaf_ids, r, n_box, n_sph);
+        return;
+    }
     const RayBox q = ray_box(r.o, r.inv);
     typedef const __attribute__((address_space(3))) float4* LdsF4;
     if (LAYOUT == LAYOUT_GLOBAL) {
@@ -1092,6 +1189,37 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
         P, lds, lds + n_node4, reinterpret_cast<const uint32_t*>(lds + n_node4 + n_leaf4), geom4, mat4, big);
 }
 
+// Grid kernel (ACCEL_GRID): the grid's cell offsets and references staged in LDS once per
+// persistent block: [references (float4) | reference ids | cell offsets | big-sphere table].
+template <bool COUNT, int MODE, bool IN_LDS>
+__global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace_grid_kernel(const rt::TraceParams P) {
+    UTIL_INIT;
+    PLACEMENT_RECORD(P);
+    extern __shared__ float4 lds[];
+    if (!IN_LDS) {   // grids too big for LDS: offsets and references from L2 / HBM
+        const BigTable big = stage_big(P, lds, threadIdx.x, kTraceBlock);
+        __syncthreads();
+        lbvh_loop<COUNT, LAYOUT_GRID, MODE>(P, reinterpret_cast<const float4*>(P.cell_start),
+                                            reinterpret_cast<const float4*>(P.grid_rec), P.grid_ids,
+                                            reinterpret_cast<const float4*>(P.geom),
+                                            reinterpret_cast<const float4*>(P.mat), big);
+        return;
+    }
+    const uint32_t nr = P.grid.n_refs, nc1 = P.grid.n_cells + 1u;
+    const uint32_t n_id4 = (nr + 3u) / 4u, n_cs4 = (nc1 + 3u) / 4u;
+    const float4* rec = reinterpret_cast<const float4*>(P.grid_rec);
+    for (uint32_t i = threadIdx.x; i < nr; i += kTraceBlock) lds[i] = rec[i];
+    uint32_t* ids = reinterpret_cast<uint32_t*>(lds + nr);
+    for (uint32_t i = threadIdx.x; i < nr; i += kTraceBlock) ids[i] = P.grid_ids[i];
+    uint32_t* cst = reinterpret_cast<uint32_t*>(lds + nr + n_id4);
+    for (uint32_t i = threadIdx.x; i < nc1; i += kTraceBlock) cst[i] = P.cell_start[i];
+    const BigTable big = stage_big(P, lds + nr + n_id4 + n_cs4, threadIdx.x, kTraceBlock);
+    __syncthreads();
+    lbvh_loop<COUNT, LAYOUT_GRID, MODE>(P, reinterpret_cast<const float4*>(cst), lds, ids,
+                                        reinterpret_cast<const float4*>(P.geom),
+                                        reinterpret_cast<const float4*>(P.mat), big);
+}
+
 // LBVH kernel for trees too big for LDS: the treelet (rt_build.hip build_treelet) is staged in LDS
 // with its rank links turned into LDS addresses; leaves, subtrees below the cut, geometry and
 // materials stay in HBM/L2.
@@ -1234,6 +1362,11 @@ static const void* pick_mode(uint32_t accel, bool count) {
             return count ? RT_FN(rt_trace_lds_kernel<true, 8u, MODE>) : RT_FN(rt_trace_lds_kernel<false, 8u, MODE>);
         case ACCEL_LBVH_TOP:
             return count ? RT_FN(rt_trace_top_kernel<true, MODE>) : RT_FN(rt_trace_top_kernel<false, MODE>);
+        case ACCEL_GRID:
+            return count ? RT_FN(rt_trace_grid_kernel<true, MODE, true>) : RT_FN(rt_trace_grid_kernel<false, MODE, true>);
+        case ACCEL_GRID_GLOBAL:
+            return count ? RT_FN(rt_trace_grid_kernel<true, MODE, false>)
+                         : RT_FN(rt_trace_grid_kernel<false, MODE, false>);
         default:
             return count ? RT_FN(rt_trace_global_kernel<true, MODE>) : RT_FN(rt_trace_global_kernel<false, MODE>);
     }

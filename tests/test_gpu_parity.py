@@ -20,8 +20,10 @@ GOLDEN = Path(__file__).resolve().parent / "golden"
 BRUTE, LBVH = 1, 2
 LBVH_LDS1 = 6      # test-only alias: accel LBVH, one node copy in LDS (options.reserved[1] = 6)
 LBVH_GLOBAL = 10   # test-only alias: accel LBVH, every node from L2 (options.reserved[1] = 10)
-WALK_FORM = {LBVH_LDS1: 6, LBVH_GLOBAL: 10}
-FORMS = [BRUTE, LBVH, LBVH_LDS1, LBVH_GLOBAL]
+LBVH_OCT = 8       # test-only alias: accel LBVH, the tree's 8 octant copies in LDS (host trees) or the
+                   # treelet (device trees) instead of the default uniform grid (options.reserved[1] = 8)
+WALK_FORM = {LBVH_LDS1: 6, LBVH_GLOBAL: 10, LBVH_OCT: 8}
+FORMS = [BRUTE, LBVH, LBVH_OCT, LBVH_LDS1, LBVH_GLOBAL]
 STREAM, COUNTER, HASH = 0, 1, 2
 
 
@@ -262,6 +264,34 @@ def test_empty_and_single_sphere(rtvk, renderer, torch, oracle):
             assert_same(a, o, ra, ro)
             a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, 20, 10, accel=accel, rng_mode=HASH)
             assert_same(a, o, rh, oh)
+
+
+@pytest.mark.parametrize("builder", [None, "gpu"])
+def test_grid_lattice_axis_rays(rtvk, renderer, torch, oracle, builder):
+    """Uniform-grid stress: spheres on an integer lattice (centers, AABB faces and cell boundaries
+    coincide or nearly so), camera looking exactly along +z through the lattice (zero direction
+    components, DDA ties at every step) and from a diagonal. Every walk equals brute force and the
+    oracle bit for bit; host grid (LDS) and device grid (L2)."""
+    sc = oracle.generate_scene()[:1].copy()   # the ground sphere
+    recs = [sc]
+    base = oracle.generate_scene()[4:5]
+    for i in range(-6, 7):
+        for j in range(-6, 7):
+            r = base.copy()
+            g = r[0, :16].view(np.float32)
+            g[:] = [float(i), 0.25, float(j), 0.25 if (i + j) % 3 else 0.5]
+            recs.append(r)
+    sc = np.concatenate(recs)
+    W, H = 40, 24
+    for cam, look in [((0.0, 0.25, -30.0), (0.0, 0.25, 0.0)), ((9.0, 3.0, -9.0), (0.0, 0.0, 0.0))]:
+        rci = oracle.render_call_info(2, W, H)
+        f = rci.view(np.float32)
+        f[8:11] = cam
+        f[12:15] = [look[k] - cam[k] for k in range(3)]
+        ra, ro, _ = oracle.render(sc, rci, W, H)
+        for accel in (BRUTE, LBVH, LBVH_OCT, LBVH_GLOBAL):
+            a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=accel, builder=builder)
+            assert_same(a, o, ra, ro)
 
 
 def test_rows_strip_map(rtvk, renderer, torch, oracle):
@@ -591,11 +621,13 @@ def test_isolated_tiles_same_image(rtvk, renderer, torch, oracle, isolate):
 
 
 
-@pytest.mark.parametrize("W,H,spp,K,form", [(320, 180, 2, 158, 0), (320, 180, 2, 158, 10), (96, 64, 3, 40, 0)])
+@pytest.mark.parametrize("W,H,spp,K,form", [(320, 180, 2, 158, 0), (320, 180, 2, 158, 8), (320, 180, 2, 158, 10),
+                                             (96, 64, 3, 40, 0), (96, 64, 3, 40, 8)])
 def test_treelet_walk_equals_brute(rtvk, renderer, torch, oracle, W, H, spp, K, form):
-    """Trees too big for LDS (device-built): the top levels staged in LDS as a treelet, subtrees
-    below the cut from L2 (ACCEL_LBVH_TOP, walk form 0) and the all-L2 walk (form 10) equal brute
-    force bit for bit, twice each (the second launch runs with the LPT order)."""
+    """Device-built scenes: the default uniform grid walked from L2 (form 0), the tree's top
+    levels staged in LDS as a treelet with subtrees below the cut from L2 (ACCEL_LBVH_TOP, form 8)
+    and the all-L2 tree walk (form 10) equal brute force bit for bit, twice each (the second
+    launch runs with the LPT order)."""
     sc = oracle.generate_scene(0.0, K)
     rci = oracle.render_call_info(spp, W, H)
     ab, ob, sb = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=BRUTE)
@@ -796,17 +828,19 @@ def test_config3_hash_full_frame(rtvk, renderer, torch, oracle):
 
 def test_config5_full_frame(rtvk, renderer, torch, oracle):
     """BASELINE config 5 on one GPU: 3840x2160, 99 860 spheres (the reference recipe with a
-    316x316 grid), 1 000 spp. The production treelet walk (LDS treelet + L2 subtrees) equals the
-    all-L2 walk bit for bit with the same segment counts, and a 4x16-pixel block at an offset
+    316x316 grid), 1 000 spp. The production walk (uniform grid from L2), the treelet walk (LDS
+    treelet + L2 subtrees) and the all-L2 tree walk agree bit for bit with the same segment counts,
+    and a 4x16-pixel block at an offset
     matches the oracle (brute force over all 99 860 spheres) at the full 1 000 spp."""
     W, H, spp, K = 3840, 2160, 1000, 158
     sc = oracle.generate_scene(0.0, K)
     rci = oracle.render_call_info(spp, W, H)
     a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH, rng_mode=HASH)
-    assert renderer.launch_info()["form"] == "lbvh-treelet"
-    a2, o2, st2 = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH_GLOBAL, rng_mode=HASH)
-    assert_same(a, o, a2, o2)
-    assert (st.segments, st.samples) == (st2.segments, st2.samples) and st.samples == W * H * spp
+    assert renderer.launch_info()["form"] == "grid-global"
+    for form in (LBVH_OCT, LBVH_GLOBAL):   # the treelet walk and the all-L2 tree walk
+        a2, o2, st2 = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=form, rng_mode=HASH)
+        assert_same(a, o, a2, o2)
+        assert (st.segments, st.samples) == (st2.segments, st2.samples) and st.samples == W * H * spp
     r = oracle.render_call_info(spp, W, H, (1800, 0))
     ra, ro, _ = oracle.render(sc, r, 4, 16, rows=np.arange(1200, 1216, dtype=np.uint32),
                               opts=oracle.options(rng_mode=HASH), threads=16)
