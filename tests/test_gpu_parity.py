@@ -21,9 +21,10 @@ BRUTE, LBVH = 1, 2
 LBVH_LDS1 = 6      # test-only alias: accel LBVH, one node copy in LDS (options.reserved[1] = 6)
 LBVH_GLOBAL = 10   # test-only alias: accel LBVH, every node from L2 (options.reserved[1] = 10)
 LBVH_OCT = 8       # test-only alias: accel LBVH, the tree's 8 octant copies in LDS (host trees) or the
-                   # treelet (device trees) instead of the default uniform grid (options.reserved[1] = 8)
-WALK_FORM = {LBVH_LDS1: 6, LBVH_GLOBAL: 10, LBVH_OCT: 8}
-FORMS = [BRUTE, LBVH, LBVH_OCT, LBVH_LDS1, LBVH_GLOBAL]
+                   # treelet (device trees) (options.reserved[1] = 8)
+GRID = 12          # test-only alias: the uniform grid (options.reserved[1] = 12)
+WALK_FORM = {LBVH_LDS1: 6, LBVH_GLOBAL: 10, LBVH_OCT: 8, GRID: 12}
+FORMS = [BRUTE, LBVH, GRID, LBVH_LDS1, LBVH_GLOBAL]
 STREAM, COUNTER, HASH = 0, 1, 2
 
 
@@ -289,7 +290,7 @@ def test_grid_lattice_axis_rays(rtvk, renderer, torch, oracle, builder):
         f[8:11] = cam
         f[12:15] = [look[k] - cam[k] for k in range(3)]
         ra, ro, _ = oracle.render(sc, rci, W, H)
-        for accel in (BRUTE, LBVH, LBVH_OCT, LBVH_GLOBAL):
+        for accel in (BRUTE, LBVH, GRID, LBVH_OCT, LBVH_GLOBAL):
             a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=accel, builder=builder)
             assert_same(a, o, ra, ro)
 
