@@ -46,6 +46,7 @@ struct rt_context {
     rt::DeviceScene scene;
     bool scene_set = false;                      // a set/refit call has succeeded (RT_ERR_NO_SCENE)
     std::vector<void*> scene_allocs;
+    std::vector<void*> grid_allocs;              // device-built grid arrays (rebuilt by every refit)
     rt::Counters* counters = nullptr;            // device
     // Every device operation of a context (scene upload / build, render) is ordered after the
     // previous one, whatever streams they are issued on: an op on a stream other than the last
@@ -168,6 +169,8 @@ void size_lds_forms(rt_context* ctx) {
 void free_scene(rt_context* ctx) {
     for (void* p : ctx->scene_allocs) (void)hipFree(p);
     ctx->scene_allocs.clear();
+    for (void* p : ctx->grid_allocs) (void)hipFree(p);
+    ctx->grid_allocs.clear();
     ctx->scene = rt::DeviceScene{};
     ctx->has_grid = false;
     ctx->grid_bytes = 0;
@@ -523,10 +526,10 @@ int set_scene_host(rt_context* ctx, const Sphere* spheres, uint32_t count, hipSt
 }
 
 template <typename T>
-int scene_alloc(rt_context* ctx, T** dst, size_t count) {
+int scene_alloc(rt_context* ctx, T** dst, size_t count, bool grid = false) {
     void* p = nullptr;
     RT_HIP(hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T) + 16));
-    ctx->scene_allocs.push_back(p);
+    (grid ? ctx->grid_allocs : ctx->scene_allocs).push_back(p);
     *dst = static_cast<T*>(p);
     return RT_OK;
 }
@@ -570,6 +573,12 @@ int set_scene_gpu(rt_context* ctx, const Sphere* d_sph, uint32_t count, hipStrea
     // from the tree's root box (the small spheres' AABB union). RT_GRID=0 disables it.
     ctx->has_grid = false;
     d.grid = rt::GridInfo{};
+    d.cell_start = d.grid_ids = nullptr;
+    d.grid_rec = nullptr;
+    // the previous build's grid (a refit rebuilds it; before, every refit leaked one): every
+    // earlier launch of the context has finished, build_scene_gpu waited for its stream
+    for (void* p : ctx->grid_allocs) (void)hipFree(p);
+    ctx->grid_allocs.clear();
     const char* ge = std::getenv("RT_GRID");
     if (!(ge && std::strcmp(ge, "0") == 0) && sm.n_small && d.small_rmax > 0.0f) {
         rt::BvhNode root;
@@ -583,11 +592,11 @@ int set_scene_gpu(rt_context* ctx, const Sphere* d_sph, uint32_t count, hipStrea
             uint32_t* cursor = nullptr;
             void* tmp = nullptr;
             const size_t tb = rt::grid_scan_bytes(gi.n_cells);
-            if (int rc = scene_alloc(ctx, &d.cell_start, size_t(gi.n_cells) + 1)) return rc;
-            if (int rc = scene_alloc(ctx, &cursor, size_t(gi.n_cells) + 1)) return rc;
-            if (int rc = scene_alloc(ctx, &d.grid_rec, size_t(bound))) return rc;
-            if (int rc = scene_alloc(ctx, &d.grid_ids, size_t(bound))) return rc;
-            if (int rc = scene_alloc(ctx, reinterpret_cast<uint8_t**>(&tmp), tb)) return rc;
+            if (int rc = scene_alloc(ctx, &d.cell_start, size_t(gi.n_cells) + 1, true)) return rc;
+            if (int rc = scene_alloc(ctx, &cursor, size_t(gi.n_cells) + 1, true)) return rc;
+            if (int rc = scene_alloc(ctx, &d.grid_rec, size_t(bound), true)) return rc;
+            if (int rc = scene_alloc(ctx, &d.grid_ids, size_t(bound), true)) return rc;
+            if (int rc = scene_alloc(ctx, reinterpret_cast<uint8_t**>(&tmp), tb, true)) return rc;
             RT_HIP(rt::build_grid_gpu(ctx->ws, d_sph, count, gi, cursor, d.cell_start, d.grid_rec, d.grid_ids, tmp,
                                       tb, st));
             gi.n_refs = 0;   // exact count left on the device: the grid is walked from L2

@@ -6,6 +6,7 @@ For each point: wave passes, mean active lanes of 64 (utilisation while the poin
 the point's share of all counted lane-slots (passes x 64), a proxy for its share of issue time
 weighted by the instructions each pass costs (the cost column is a static VALU estimate)."""
 import ctypes
+import os
 import sys
 
 sys.path.insert(0, "ray-tracing-gpu-vulkan_amd")
@@ -19,13 +20,22 @@ NAMES = {0: "node visit (LDS)", 11: "node visit (L2)", 1: "leaf test", 2: "spher
          7: "sample start", 3: "shade", 10: "shade hit", 9: "unit vector", 4: "diffuse", 5: "metal",
          6: "dielectric", 12: "node pass <=8 lanes", 13: "node pass <=16", 14: "node pass <=32"}
 r = rtvk.Renderer(0)
+
+
+def opts(rng):
+    """Walk form from RT_WALK (options.reserved[1]: 8 octant tree, 12 grid; default 0)."""
+    o = rtvk.make_options(accel=2, rng_mode=rng)
+    o.reserved[1] = int(os.environ.get("RT_WALK", "0"))
+    return o
+
+
 r.set_scene(rtvk.generateRandomScene(0.0, K))
 acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
 out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
 rci = rtvk.canonical_render_call_info(spp, W, H)
 lib = abi.load_library()
 for rng in (rtvk.HASH,):
-    r.render_device(rci, acc, out, options=rtvk.make_options(accel=2, rng_mode=rng))
+    r.render_device(rci, acc, out, options=opts(rng))
     torch.cuda.synchronize()
     u = (ctypes.c_uint64 * 32)()
     abi.check(lib.rt_debug_util(r._ctx, u))

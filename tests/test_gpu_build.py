@@ -187,6 +187,24 @@ def test_refit_moved_small_spheres(rtvk, renderer, torch, oracle):
         render_small(rtvk, renderer, torch, oracle, moved)
 
 
+def test_refit_keeps_device_memory(rtvk, renderer, torch, oracle):
+    """Every refit of a device-built scene rebuilds its uniform grid; the previous grid's arrays
+    are released (they once leaked, ~1 MB per refit here), and the image stays exact."""
+    sc = oracle.generate_scene(0.0, 40)   # 6 404 spheres: device build + grid from L2
+    with tree_builder("gpu"):
+        renderer.set_scene(sc)
+        renderer.refit_scene(sc)
+        torch.cuda.synchronize()
+        free0 = torch.cuda.mem_get_info()[0]
+        for t in (0.3, 0.6, 0.9) * 10:
+            renderer.refit_scene(oracle.generate_scene(t, 40))
+        torch.cuda.synchronize()
+        assert free0 - torch.cuda.mem_get_info()[0] < 4 << 20
+        sc = oracle.generate_scene(0.9, 40)
+        renderer.refit_scene(sc)
+        render_small(rtvk, renderer, torch, oracle, sc)
+
+
 def test_set_scene_device_input(rtvk, renderer, torch, oracle):
     sc = oracle.generate_scene(0.25, 11)
     with tree_builder("gpu"):
