@@ -744,9 +744,12 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
                                   rci->camera_pos.z * rci->camera_pos.z);
     if (o.accel == RT_ACCEL_BRUTE) {
         accel = rt::ACCEL_BRUTE;
-    } else if (ctx->has_grid && cam_r <= ctx->grid_pad_radius && (form == 12u || (form == 0u && !ctx->oct_bytes))) {
-        // the grid unless the tree fits LDS as octant copies (measured equal
-        // there); its margin covers cameras within its pad radius
+    } else if (ctx->has_grid && cam_r <= ctx->grid_pad_radius &&
+               (form == 12u || (form == 0u && (ctx->grid_bytes || !ctx->oct_bytes)))) {
+        // the grid: staged in LDS when it fits (config 3: 1 % faster than the
+        // octant tree), else the octant tree when that fits LDS (a device-built scene of ~1000
+        // spheres, whose grid would be read from L2), else the grid from L2; its margin covers
+        // cameras within its pad radius
         accel = ctx->grid_bytes ? rt::ACCEL_GRID : rt::ACCEL_GRID_GLOBAL;
         lds = ctx->grid_bytes ? ctx->grid_bytes : rt::kBigLdsBytes;
     } else if (ctx->oct_bytes && (form == 0u || form == 8u)) {
@@ -1034,7 +1037,7 @@ int rt_debug_launch_info(rt_context* ctx, uint32_t* out4) {
     if (!ctx || !out4) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     out4[0] = ctx->last_chunks;
     // the default form of the current scene for a camera within its pad radius (rt_render_device)
-    const bool grid = ctx->has_grid && !ctx->oct_bytes;
+    const bool grid = ctx->has_grid && (ctx->grid_bytes || !ctx->oct_bytes);
     out4[1] = grid ? (ctx->grid_bytes ? rt::ACCEL_GRID : rt::ACCEL_GRID_GLOBAL) : ctx->oct_bytes ? rt::ACCEL_LBVH_OCT
               : ctx->lds1_bytes ? rt::ACCEL_LBVH_LDS : ctx->gpu_tree ? rt::ACCEL_LBVH_TOP : rt::ACCEL_LBVH_GLOBAL;
     out4[2] = uint32_t(grid ? ctx->grid_bytes : ctx->oct_bytes ? ctx->oct_bytes : ctx->lds1_bytes);

@@ -151,6 +151,14 @@ __device__ __forceinline__ void test_sphere(float cx, float cy, float cz, float 
     }
 }
 
+// Both roots behind the origin (outside the sphere, moving away from it): no report in [tmin,
+// tmax], so the exact tail need not run. Exact: a >= 0 and c >= 0 give RN(a c) >= 0, so D =
+// RN(b^2 - RN(a c)) <= RN(b^2) and sqrt_cr(D) <= sqrt_cr(RN(b^2)) = b (b >= 2^-60: b^2 is normal;
+// an overflowing b^2 gives t2 = +inf, rejected by t <= best); then t1 and t2 are <= 0 < tmin.
+// Typical cases: the sphere a bounce ray leaves (origin on it, c >= 0 after rounding) and spheres
+// behind the ray whose line still crosses them.
+__device__ __forceinline__ bool behind(float b, float c) { return b >= 0x1p-60f && c >= 0.0f; }
+
 // 16-B reload of an LDS record inside a rarely run loop (volatile: not merged with the first
 // load, so the record's registers are free in between).
 typedef float f4v __attribute__((ext_vector_type(4)));
@@ -180,7 +188,7 @@ __device__ __forceinline__ void test4(const float4 s0, const float4 s1, const fl
         const float ocx = o.x - sv[k].x, ocy = o.y - sv[k].y, ocz = o.z - sv[k].z;
         const float b = __builtin_fmaf(ocz, d.z, __builtin_fmaf(ocy, d.y, ocx * d.x));
         const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - rr;
-        cand |= (__builtin_fmaf(b, b, -(a * c)) >= 0.0f ? 1u : 0u) << k;
+        cand |= (__builtin_fmaf(b, b, -(a * c)) >= 0.0f && !behind(b, c) ? 1u : 0u) << k;
     }
     while (cand) {
         UTIL(2, true);
@@ -215,7 +223,7 @@ __device__ __forceinline__ void test1(const float4 sp, const uint32_t* __restric
     const float b = __builtin_fmaf(ocz, d.z, __builtin_fmaf(ocy, d.y, ocx * d.x));
     const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - rr;
     const float D = __builtin_fmaf(b, b, -(a * c));
-    if (D >= 0.0f) {
+    if (D >= 0.0f && !behind(b, c)) {
         UTIL(2, true);
         const float sq = sqrt_cr(D);
         float t = (-b - sq) * ia;

@@ -24,7 +24,7 @@ LBVH_OCT = 8       # test-only alias: accel LBVH, the tree's 8 octant copies in 
                    # treelet (device trees) (options.reserved[1] = 8)
 GRID = 12          # test-only alias: the uniform grid (options.reserved[1] = 12)
 WALK_FORM = {LBVH_LDS1: 6, LBVH_GLOBAL: 10, LBVH_OCT: 8, GRID: 12}
-FORMS = [BRUTE, LBVH, GRID, LBVH_LDS1, LBVH_GLOBAL]
+FORMS = [BRUTE, LBVH, LBVH_OCT, LBVH_LDS1, LBVH_GLOBAL]   # LBVH: the default form (the grid for host scenes)
 STREAM, COUNTER, HASH = 0, 1, 2
 
 
