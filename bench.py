@@ -37,6 +37,11 @@ FLOP_PER_SPHERE_TEST = 23
 FLOP_PER_BOX_TEST = 20
 BYTES_PER_BOX_TEST = 32         # bytes/sample = S·(B·32 + T·16), read from LDS
 BYTES_PER_SPHERE_TEST = 16
+# Uniform-grid walk: a cell step recomputes one boundary's t, ((g + c·cs) - o)·(1/d)
+# (fma, sub, mul) and reads the cell's two offsets; the instrumented build counts cell steps where
+# the tree walk counts box tests.
+FLOP_PER_CELL_STEP = 3
+BYTES_PER_CELL_STEP = 8
 LDS_PEAK_TBPS = 256 * 256 * 2.4e9 / 1e12   # ds_read_b128: 256 B/clk/CU x 256 CU x 2.4 GHz
 
 CONFIGS = {   # BASELINE.json configs: width, height, spp, grid half extent, accel
@@ -322,7 +327,10 @@ def main() -> int:
     else:
         cs = rtvk.Stats()
     scale = spp / cnt_spp
-    flops = (cs.box_tests * FLOP_PER_BOX_TEST + cs.sphere_tests * FLOP_PER_SPHERE_TEST) * scale
+    grid_walk = info["form"].startswith("grid")
+    flop_step = FLOP_PER_CELL_STEP if grid_walk else FLOP_PER_BOX_TEST
+    bytes_step = BYTES_PER_CELL_STEP if grid_walk else BYTES_PER_BOX_TEST
+    flops = (cs.box_tests * flop_step + cs.sphere_tests * FLOP_PER_SPHERE_TEST) * scale
     achieved = flops / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
 
     result = None
@@ -330,7 +338,9 @@ def main() -> int:
         sha = lib_sha256()
         kname = {"lbvh-octant-lds": "rt_trace_lds_kernel<8 octant copies>", "lbvh-lds": "rt_trace_lds_kernel<1 copy>",
                  "lbvh-treelet": "rt_trace_top_kernel (LDS treelet + L2 subtrees)",
-                 "lbvh-global": "rt_trace_global_kernel"}.get(info["form"], info["form"])
+                 "lbvh-global": "rt_trace_global_kernel",
+                 "grid-lds": "rt_trace_grid_kernel<grid in LDS>",
+                 "grid-global": "rt_trace_grid_kernel<grid from L2>"}.get(info["form"], info["form"])
         if accel == abi.RT_ACCEL_BRUTE:
             kname = "rt_trace_brute_kernel"
         key = f"{accel_name}-{args.rng}-{W}x{H}-{spp}spp-grid{grid}-n{world}"
@@ -344,19 +354,25 @@ def main() -> int:
                               f"stream); with frames in flight a launch spans {kernel_ms_inflight:.2f} ms "
                               "including the wait for the previous frame's CUs",
                 "frac_per_step": round(flops / (elapsed / args.steps) / 1e12 / VALU_FP32_PEAK_TFLOPS, 4),
-                "flop_per_launch": int(flops), "box_tests": int(cs.box_tests * scale),
+                "flop_per_launch": int(flops),
+                ("cell_steps" if grid_walk else "box_tests"): int(cs.box_tests * scale),
                 "sphere_tests": int(cs.sphere_tests * scale),
-                "flop_model": "20/box test + 23/sphere test (SURVEY.md 8(d)); counts from the instrumented "
-                              f"build of the same kernel at {cnt_spp} spp" + (f", x{scale:g}" if scale != 1 else ""),
+                "flop_model": (f"{flop_step}/{'grid cell step' if grid_walk else 'box test'} + 23/sphere test "
+                               f"(SURVEY.md 8(d)); counts from the instrumented build of the same kernel at "
+                               f"{cnt_spp} spp" + (f", x{scale:g}" if scale != 1 else "")),
                 "lib_sha256": sha}
         roof.update({k: v for k, v in pmc.items() if k in ("valu_issue_busy", "lane_util", "pmc")})
+        if "valu_issue_busy" in pmc and "lane_util" in pmc:
+            # every executed lane-op (traversal control, shading, sampling included) against peak
+            roof["valu_lane_frac"] = round(pmc["valu_issue_busy"] * pmc["lane_util"], 4)
         if accel != abi.RT_ACCEL_BRUTE:   # the other fraction SURVEY.md 8(d) asks for: the LBVH's own bytes
-            lds_bytes = (cs.box_tests * BYTES_PER_BOX_TEST + cs.sphere_tests * BYTES_PER_SPHERE_TEST) * scale
+            lds_bytes = (cs.box_tests * bytes_step + cs.sphere_tests * BYTES_PER_SPHERE_TEST) * scale
             lds_tbps = lds_bytes / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
             roof["lds"] = {"achieved": round(lds_tbps, 3), "peak": round(LDS_PEAK_TBPS, 1), "unit": "TB/s",
                            "frac": round(lds_tbps / LDS_PEAK_TBPS, 4), "bytes_per_launch": int(lds_bytes),
-                           "model": "32 B per box test + 16 B per sphere test (node and leaf records; from L2 "
-                                    "instead of LDS below the treelet of trees too big for LDS)"}
+                           "model": (f"{bytes_step} B per {'cell step' if grid_walk else 'box test'} + 16 B per "
+                                     "sphere test (from L2 instead of LDS for walks whose structure does not fit "
+                                     "LDS)")}
         cfg_name = (f"BASELINE config {args.config}" if world == 1 or args.config not in (3, 4)
                     else f"BASELINE config {4 if world == 8 else 3} frame on {world} GPUs")
         default_shape = (W, H, spp, grid, accel_name) == CONFIGS[args.config]

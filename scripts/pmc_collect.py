@@ -23,7 +23,7 @@ SIMDS, CLOCK_HZ = 1024, 2.4e9
 
 
 def is_production(kernel_name: str) -> bool:
-    m = re.search(r"rt_trace_(lds|top|global|brute)_kernel<([^>]*)>", kernel_name)
+    m = re.search(r"rt_trace_(lds|top|grid|global|brute)_kernel<([^>]*)>", kernel_name)
     return bool(m) and m.group(2).split(",")[0].strip() == "false"
 
 
