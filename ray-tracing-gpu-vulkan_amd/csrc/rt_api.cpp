@@ -163,7 +163,7 @@ void size_lds_forms(rt_context* ctx) {
     ctx->oct_bytes = (ok && oct <= kMaxLdsBytes) ? oct : 0;
     const rt::GridInfo& g = d.grid;
     const size_t grid = (size_t(g.n_refs) + (g.n_refs + 3) / 4 + (size_t(g.n_cells) + 4) / 4) * 16 + rt::kBigLdsBytes;
-    ctx->grid_bytes = (g.n_refs && grid <= kMaxLdsBytes) ? grid : 0;
+    ctx->grid_bytes = (g.n_refs && grid + rt::kLaneSumLdsBytes <= kMaxLdsBytes) ? grid : 0;
 }
 
 void free_scene(rt_context* ctx) {

@@ -64,9 +64,18 @@ struct GridInfo {
     float cs[3];        // cell size per axis
     float inv_cs[3];    // 1 / cs (cell of the entry point)
     float margin;       // registration margin (the entry box is widened by it too)
+    float lo_m[3];      // entry box: gmin - margin, gmax + margin (one binary32 subtraction / addition,
+    float hi_m[3];      // on the host: kernel operands from SGPRs instead of loop-invariant VGPRs)
     uint32_t n[3];      // cells per axis
     uint32_t n_cells, n_refs;
 };
+
+#ifndef RT_TRACE_BLOCK
+#define RT_TRACE_BLOCK 768   // threads per block of the tree / grid kernels (rt_kernels.hip kTraceBlock)
+#endif
+// Static LDS of the grid kernels beside their dynamic LDS: per-thread 64-bit unit sums of the
+// counter-based stream (rt_kernels.hip s_lane_sum).
+constexpr unsigned kLaneSumLdsBytes = 3u * 8u * RT_TRACE_BLOCK;
 
 // Scene as resident in HBM (one allocation per context, rebuilt by rt_set_scene).
 struct DeviceScene {

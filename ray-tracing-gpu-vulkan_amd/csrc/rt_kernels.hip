@@ -57,6 +57,10 @@ struct Stamps { unsigned long long acc[8], t; uint32_t cur; };
         if (lane_id() == 0)                                                                    \
             for (int k_ = 0; k_ < 8; ++k_) atomicAdd(&P.counters->stamp[k_], stamps.acc[k_]);  \
     } while (0)
+#elif defined(RT_ASM_MARKS)   // ISA listing only: phase boundaries as comments (scripts/isa_phases.py)
+#define STAMP(k) asm volatile("; RT_PHASE " #k)
+#define STAMP_DECL [[maybe_unused]] Stamps stamps
+#define STAMP_FLUSH do {} while (0)
 #else
 #define STAMP(k) do {} while (0)
 #define STAMP_DECL [[maybe_unused]] Stamps stamps
@@ -327,15 +331,44 @@ __device__ __forceinline__ uint32_t sample_fixed(float c) {
     return uint32_t(v);
 }
 
-// Adds a lane's partial fixed-point sums to its pixel's 64-bit sums in HBM (fire-and-forget
-// relaxed atomics) and clears them; rt_resolve_fixed_kernel stores the pixel.
-__device__ __forceinline__ void flush_fixed(const rt::TraceParams& P, Path& ps) {
+// Adds fixed-point sums to a pixel's 64-bit sums in HBM (fire-and-forget relaxed atomics);
+// rt_resolve_fixed_kernel stores the pixel.
+__device__ __forceinline__ void add_fixed(const rt::TraceParams& P, const Path& ps, unsigned long long x,
+                                          unsigned long long y, unsigned long long z) {
     const uint32_t lx = ps.px & 0xffffu, ly = ps.px >> 16;
     const size_t n = size_t(P.band_w) * P.band_h, texel = size_t(ly) * P.band_w + lx;
-    __hip_atomic_fetch_add(P.fixed + texel, (unsigned long long)ps.qx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(P.fixed + n + texel, (unsigned long long)ps.qy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(P.fixed + 2 * n + texel, (unsigned long long)ps.qz, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(P.fixed + texel, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(P.fixed + n + texel, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(P.fixed + 2 * n + texel, z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Per-lane 64-bit unit sums in LDS (LSUM kernels: the grid kernels, whose LDS has room for them,
+// 24 B per thread): the 32-bit lane partial, which must be emptied every kFixedFlush samples, is
+// added here, and the unit's sum goes to HBM once when the unit ends, instead of three
+// device-scope atomics per lane every kFixedFlush samples (config 3: ~486 M atomics, 16 GB of
+// memory-side write requests per frame). Lane-private slots: no contention.
+__shared__ unsigned long long s_lane_sum[3 * RT_TRACE_BLOCK];
+// A thread's slot from the wave's first thread (wave-uniform: an SGPR) and the lane id (mbcnt),
+// so no thread-id VGPR stays live across the segment loop for it.
+__device__ __forceinline__ unsigned long long* lane_sum_slot() {
+    const uint32_t wave0 = __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
+    return s_lane_sum + wave0 + __lane_id();
+}
+static_assert(sizeof(s_lane_sum) == rt::kLaneSumLdsBytes, "rt_internal.h");
+
+// Empties a lane's 32-bit partial sums (every kFixedFlush samples and at the unit's end).
+template <bool LSUM>
+__device__ __forceinline__ void flush_fixed(const rt::TraceParams& P, Path& ps) {
+    if (LSUM) {
+        unsigned long long* s = lane_sum_slot();   // ds_add_u64 without return: no read back
+        __hip_atomic_fetch_add(s, (unsigned long long)ps.qx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_fetch_add(s + RT_TRACE_BLOCK, (unsigned long long)ps.qy, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __hip_atomic_fetch_add(s + 2 * RT_TRACE_BLOCK, (unsigned long long)ps.qz, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WAVEFRONT);
+    } else {
+        add_fixed(P, ps, ps.qx, ps.qy, ps.qz);
+    }
     ps.qx = ps.qy = ps.qz = 0u;
 }
 
@@ -491,10 +524,16 @@ __device__ __forceinline__ void store_pixel(const rt::TraceParams& P, const Path
 
 // Finished unit. STREAM: the unit is the whole pixel: store it. HASH: flush the chunk's remaining
 // partial fixed-point sum.
-template <int MODE>
+template <int MODE, bool LSUM>
 __device__ __forceinline__ void finish_unit(const rt::TraceParams& P, Path& ps) {
-    if (MODE == rt::MODE_HASH) {
-        if (ps.qx | ps.qy | ps.qz) flush_fixed(P, ps);
+    if (MODE == rt::MODE_HASH && LSUM) {   // the unit's whole sum from LDS, once
+        unsigned long long* s = lane_sum_slot();
+        const unsigned long long x = s[0] + ps.qx, y = s[RT_TRACE_BLOCK] + ps.qy, z = s[2 * RT_TRACE_BLOCK] + ps.qz;
+        if (x | y | z) add_fixed(P, ps, x, y, z);
+        s[0] = s[RT_TRACE_BLOCK] = s[2 * RT_TRACE_BLOCK] = 0ull;
+        ps.qx = ps.qy = ps.qz = 0u;
+    } else if (MODE == rt::MODE_HASH) {
+        if (ps.qx | ps.qy | ps.qz) flush_fixed<false>(P, ps);
     } else {
         store_pixel(P, ps);
     }
@@ -502,13 +541,13 @@ __device__ __forceinline__ void finish_unit(const rt::TraceParams& P, Path& ps) 
 
 // shader.rgen:56-58 + 107-115: next camera ray of the lane's unit. Returns false when the unit's
 // samples are done (empty units only: the others finish at their last sample's end).
-template <int MODE>
+template <int MODE, bool LSUM>
 __device__ __forceinline__ bool start_sample(const rt::TraceParams& P, const Camera& cam, Path& ps,
                                              V3& o, V3& d) {
     UTIL(7, true);
     const uint32_t lx = ps.px & 0xffffu, ly = ps.px >> 16;
     if (ps.s >= ps.s_end) {
-        finish_unit<MODE>(P, ps);
+        finish_unit<MODE, LSUM>(P, ps);
         return false;
     }
     const uint32_t gx = P.off_x + lx;
@@ -552,7 +591,7 @@ __device__ __forceinline__ bool start_sample(const rt::TraceParams& P, const Cam
 // shader.rchit:38-133 / shader.rmiss:13-18 + shader.rgen:77-88 for one finished trace.
 // Returns true when the path continues (o, d hold the next ray), false when the sample ended
 // (its colour has been added to the unit's sum).
-template <int MODE>
+template <int MODE, bool LSUM>
 __device__ __forceinline__ bool shade(const rt::TraceParams& P, const float4* __restrict__ geom4,
                                       const float4* __restrict__ mat4, Path& ps, uint32_t bi,
                                       float best, V3& o, V3& d) {
@@ -634,7 +673,7 @@ __device__ __forceinline__ bool shade(const rt::TraceParams& P, const float4* __
         ps.qy += sample_fixed(col.y);
         ps.qz += sample_fixed(col.z);
         // a partial never spans a multiple of kFixedFlush samples: <= kFixedFlush * 2^24 < 2^32
-        if ((ps.s & (rt::kFixedFlush - 1u)) == 0u) flush_fixed(P, ps);
+        if ((ps.s & (rt::kFixedFlush - 1u)) == 0u) flush_fixed<LSUM>(P, ps);
     } else {
         ps.sx += double(col.x);
         ps.sy += double(col.y);
@@ -665,9 +704,6 @@ __device__ __forceinline__ void record_tile_cost(const rt::TraceParams& P, const
 #define RT_TRACE_WAVES_PER_SIMD 6
 #endif
 constexpr uint32_t kBruteBlock = 256;
-#ifndef RT_TRACE_BLOCK
-#define RT_TRACE_BLOCK 768
-#endif
 constexpr uint32_t kTraceBlock = RT_TRACE_BLOCK;   // one block per CU shares one staged tree / treelet
 
 // ---------------------------------------------------------------------------------------------
@@ -688,7 +724,7 @@ __global__ __launch_bounds__(kBruteBlock, RT_BRUTE_WAVES_PER_SIMD) void rt_trace
     for (;;) {
         refill<MODE>(P, lane, st, ps, blk, stamps);
         if (st == ST_NEED_SAMPLE) {
-            if (start_sample<MODE>(P, cam, ps, o, d)) { st = ST_TRACING; n_smp++; }
+            if (start_sample<MODE, false>(P, cam, ps, o, d)) { st = ST_TRACING; n_smp++; }
             else st = ST_NEED_UNIT;
         }
         if (__ballot(st == ST_NEED_UNIT)) continue;   // refill before the next trace
@@ -702,10 +738,10 @@ __global__ __launch_bounds__(kBruteBlock, RT_BRUTE_WAVES_PER_SIMD) void rt_trace
             if (COUNT) n_sph += P.n_spheres;
             n_seg++;
             ps.segs++;
-            if (!shade<MODE>(P, reinterpret_cast<const float4*>(P.geom), reinterpret_cast<const float4*>(P.mat),
-                             ps, bi, best, o, d)) {
+            if (!shade<MODE, false>(P, reinterpret_cast<const float4*>(P.geom),
+                                    reinterpret_cast<const float4*>(P.mat), ps, bi, best, o, d)) {
                 if (ps.s >= ps.s_end) {
-                    finish_unit<MODE>(P, ps);
+                    finish_unit<MODE, false>(P, ps);
                     st = ST_NEED_UNIT;
                 } else {
                     st = ST_NEED_SAMPLE;
@@ -885,9 +921,9 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
                                           const float4* __restrict__ rec, const uint32_t* __restrict__ ids,
                                           Ray& r, uint32_t& n_cell, uint32_t& n_sph) {
     const rt::GridInfo& G = P.grid;
-    const float x0 = ((G.gmin[0] - G.margin) - r.o.x) * r.inv.x, x1 = ((G.gmax[0] + G.margin) - r.o.x) * r.inv.x;
-    const float y0 = ((G.gmin[1] - G.margin) - r.o.y) * r.inv.y, y1 = ((G.gmax[1] + G.margin) - r.o.y) * r.inv.y;
-    const float z0 = ((G.gmin[2] - G.margin) - r.o.z) * r.inv.z, z1 = ((G.gmax[2] + G.margin) - r.o.z) * r.inv.z;
+    const float x0 = (G.lo_m[0] - r.o.x) * r.inv.x, x1 = (G.hi_m[0] - r.o.x) * r.inv.x;
+    const float y0 = (G.lo_m[1] - r.o.y) * r.inv.y, y1 = (G.hi_m[1] - r.o.y) * r.inv.y;
+    const float z0 = (G.lo_m[2] - r.o.z) * r.inv.z, z1 = (G.hi_m[2] - r.o.z) * r.inv.z;
     const float tn = fmaxf(fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1)), T_MIN);
     const float tf = fminf(fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1)), r.limit);
     if (!(tn <= tf)) return;
@@ -1053,11 +1089,16 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
                                           const uint32_t* __restrict__ leaf_ids,
                                           const float4* __restrict__ geom4, const float4* __restrict__ mat4,
                                           const BigTable big) {
+    constexpr bool LSUM = MODE == rt::MODE_HASH && (LAYOUT == LAYOUT_GRID || LAYOUT == LAYOUT_GRID_L2);
     const uint32_t lane = lane_id();
     const Camera cam = load_camera(P);
     uint32_t st = ST_NEED_UNIT;
     Path ps{};
     Ray r{};
+    if (LSUM) {   // this thread's unit sums (read and written by this thread only: no barrier)
+        unsigned long long* s = lane_sum_slot();
+        s[0] = s[RT_TRACE_BLOCK] = s[2 * RT_TRACE_BLOCK] = 0ull;
+    }
     // traced segments and started samples of this wave (wave-uniform: ballot counts, no per-lane
     // registers); per-lane test counters in COUNT builds only
     uint32_t seg_w = 0, smp_w = 0, n_box = 0, n_sph = 0;
@@ -1078,7 +1119,7 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
         STAMP(4);
         bool started = false;
         if (st == ST_NEED_SAMPLE) {
-            if (start_sample<MODE>(P, cam, ps, r.o, r.d)) {
+            if (start_sample<MODE, LSUM>(P, cam, ps, r.o, r.d)) {
                 st = ST_TRACING;
                 started = true;
             } else {   // empty unit (spp = 0): stored at once
@@ -1110,12 +1151,12 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
         STAMP(3);
         if (st == ST_TRACING) {
             ps.segs++;
-            if (!shade<MODE>(P, geom4, mat4, ps, r.bi, r.best, r.o, r.d)) {
+            if (!shade<MODE, LSUM>(P, geom4, mat4, ps, r.bi, r.best, r.o, r.d)) {
                 // The sample ended. After the unit's last one, finish it here rather than at the
                 // next sample start: the lane asks for a unit at the top of the next iteration
                 // directly, instead of costing its wave one extra pass of the loop head.
                 if (ps.s >= ps.s_end) {
-                    finish_unit<MODE>(P, ps);
+                    finish_unit<MODE, LSUM>(P, ps);
                     record_tile_cost(P, ps);
                     st = ST_NEED_UNIT;
                 } else {
