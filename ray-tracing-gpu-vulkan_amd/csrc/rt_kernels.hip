@@ -539,17 +539,12 @@ __device__ __forceinline__ void finish_unit(const rt::TraceParams& P, Path& ps) 
     }
 }
 
-// shader.rgen:56-58 + 107-115: next camera ray of the lane's unit. Returns false when the unit's
-// samples are done (empty units only: the others finish at their last sample's end).
-template <int MODE, bool LSUM>
-__device__ __forceinline__ bool start_sample(const rt::TraceParams& P, const Camera& cam, Path& ps,
-                                             V3& o, V3& d) {
+// shader.rgen:56-58 + 107-115: camera ray of sample ps.s of the lane's unit: origin o and the
+// direction before normalisation, v = to - from (the caller normalises it).
+template <int MODE>
+__device__ __forceinline__ void camera_ray(const rt::TraceParams& P, const Camera& cam, Path& ps, V3& o, V3& v) {
     UTIL(7, true);
     const uint32_t lx = ps.px & 0xffffu, ly = ps.px >> 16;
-    if (ps.s >= ps.s_end) {
-        finish_unit<MODE, LSUM>(P, ps);
-        return false;
-    }
     const uint32_t gx = P.off_x + lx;
     const uint32_t gy = P.rows ? load_now(P.rows + ly) : P.off_y + ly;
     if (MODE == rt::MODE_HASH) ps.seed = sample_seed_hash(ps.pixel_seed, P.sample_base + ps.s);
@@ -582,19 +577,52 @@ __device__ __forceinline__ bool start_sample(const rt::TraceParams& P, const Cam
     const V3 from = add(cam.lf, add(scale(rx, cam.crt), scale(ry, cam.cup)));
     const V3 to = sub(add(cam.ulc, scale(ux, cam.hor)), scale(uy, cam.ver));
     o = from;
-    d = normalize(sub(to, from));
+    v = sub(to, from);
     ps.thr = v3(1.0f, 1.0f, 1.0f);
     ps.depth = 0;
+}
+
+// First camera ray of a unit just taken. Returns false when the unit has no samples (spp = 0:
+// stored at once); later samples start inside shade().
+template <int MODE, bool LSUM>
+__device__ __forceinline__ bool start_sample(const rt::TraceParams& P, const Camera& cam, Path& ps,
+                                             V3& o, V3& d) {
+    if (ps.s >= ps.s_end) {
+        finish_unit<MODE, LSUM>(P, ps);
+        return false;
+    }
+    V3 v;
+    camera_ray<MODE>(P, cam, ps, o, v);
+    d = normalize(v);
     return true;
 }
 
-// shader.rchit:38-133 / shader.rmiss:13-18 + shader.rgen:77-88 for one finished trace.
-// Returns true when the path continues (o, d hold the next ray), false when the sample ended
-// (its colour has been added to the unit's sum).
+// The sample's colour added to the unit's sum (shader.rgen:85-88, 59-60).
 template <int MODE, bool LSUM>
-__device__ __forceinline__ bool shade(const rt::TraceParams& P, const float4* __restrict__ geom4,
+__device__ __forceinline__ void sample_end(const rt::TraceParams& P, Path& ps, const V3 col) {
+    ps.s++;
+    if (MODE == rt::MODE_HASH) {
+        ps.qx += sample_fixed(col.x);
+        ps.qy += sample_fixed(col.y);
+        ps.qz += sample_fixed(col.z);
+        // a partial never spans a multiple of kFixedFlush samples: <= kFixedFlush * 2^24 < 2^32
+        if ((ps.s & (rt::kFixedFlush - 1u)) == 0u) flush_fixed<LSUM>(P, ps);
+    } else {
+        ps.sx += double(col.x);
+        ps.sy += double(col.y);
+        ps.sz += double(col.z);
+    }
+}
+
+// shader.rchit:38-133 / shader.rmiss:13-18 + shader.rgen:77-88 for one finished trace. When the
+// sample ends, its colour is added to the unit's sum and the unit's next sample starts here
+// (`fresh`): the scattered and the camera direction share one normalisation, and the loop head's
+// sample start runs only for units just taken. Returns true when the lane traces again (o, d hold
+// the next ray), false when its unit's samples are done.
+template <int MODE, bool LSUM>
+__device__ __forceinline__ bool shade(const rt::TraceParams& P, const Camera& cam, const float4* __restrict__ geom4,
                                       const float4* __restrict__ mat4, Path& ps, uint32_t bi,
-                                      float best, V3& o, V3& d) {
+                                      float best, V3& o, V3& d, bool& fresh) {
     V3 att;
     bool scatter = false;
     V3 sd = v3(0.0f, 0.0f, 0.0f);
@@ -656,31 +684,29 @@ __device__ __forceinline__ bool shade(const rt::TraceParams& P, const float4* __
         scatter = !(sd.x == 0.0f && sd.y == 0.0f && sd.z == 0.0f);  // shader.rchit:48
     }
     // shader.rgen:77-88
-    V3 col;
+    V3 col, v = sd;
+    bool more;
     if (scatter) {
         ps.thr = mul(ps.thr, att);
         o = p;
-        d = normalize(sd);
         ps.depth++;
-        if (ps.depth < P.max_depth) return true;
+        more = ps.depth < P.max_depth;
         col = mul(ps.thr, v3(0.0f, 0.0f, 0.0f));   // depth exhausted: light stays 0 (Q6)
     } else {
         col = mul(ps.thr, att);
+        more = false;
     }
-    ps.s++;
-    if (MODE == rt::MODE_HASH) {
-        ps.qx += sample_fixed(col.x);
-        ps.qy += sample_fixed(col.y);
-        ps.qz += sample_fixed(col.z);
-        // a partial never spans a multiple of kFixedFlush samples: <= kFixedFlush * 2^24 < 2^32
-        if ((ps.s & (rt::kFixedFlush - 1u)) == 0u) flush_fixed<LSUM>(P, ps);
-    } else {
-        ps.sx += double(col.x);
-        ps.sy += double(col.y);
-        ps.sz += double(col.z);
+    if (!more) {
+        sample_end<MODE, LSUM>(P, ps, col);
+        if (ps.s < ps.s_end) {   // the unit's next sample
+            camera_ray<MODE>(P, cam, ps, o, v);
+            more = fresh = true;
+        }
     }
-    return false;
+    if (more) d = normalize(v);
+    return more;
 }
+
 
 // Finished unit: its chain length (traced segments) feeds the next launch's hand-out order.
 __device__ __forceinline__ void record_tile_cost(const rt::TraceParams& P, const Path& ps) {
@@ -738,15 +764,13 @@ __global__ __launch_bounds__(kBruteBlock, RT_BRUTE_WAVES_PER_SIMD) void rt_trace
             if (COUNT) n_sph += P.n_spheres;
             n_seg++;
             ps.segs++;
-            if (!shade<MODE, false>(P, reinterpret_cast<const float4*>(P.geom),
-                                    reinterpret_cast<const float4*>(P.mat), ps, bi, best, o, d)) {
-                if (ps.s >= ps.s_end) {
-                    finish_unit<MODE, false>(P, ps);
-                    st = ST_NEED_UNIT;
-                } else {
-                    st = ST_NEED_SAMPLE;
-                }
+            bool fresh = false;
+            if (!shade<MODE, false>(P, cam, reinterpret_cast<const float4*>(P.geom),
+                                    reinterpret_cast<const float4*>(P.mat), ps, bi, best, o, d, fresh)) {
+                finish_unit<MODE, false>(P, ps);
+                st = ST_NEED_UNIT;
             }
+            if (fresh) n_smp++;
         }
     }
     atomicAdd(&P.counters->segments, (unsigned long long)n_seg);
@@ -1149,21 +1173,18 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
             if (lane == 0) wave_iters += m;
         }
         STAMP(3);
+        bool fresh = false;   // a sample started inside shade()
         if (st == ST_TRACING) {
             ps.segs++;
-            if (!shade<MODE, LSUM>(P, geom4, mat4, ps, r.bi, r.best, r.o, r.d)) {
-                // The sample ended. After the unit's last one, finish it here rather than at the
-                // next sample start: the lane asks for a unit at the top of the next iteration
-                // directly, instead of costing its wave one extra pass of the loop head.
-                if (ps.s >= ps.s_end) {
-                    finish_unit<MODE, LSUM>(P, ps);
-                    record_tile_cost(P, ps);
-                    st = ST_NEED_UNIT;
-                } else {
-                    st = ST_NEED_SAMPLE;
-                }
+            if (!shade<MODE, LSUM>(P, cam, geom4, mat4, ps, r.bi, r.best, r.o, r.d, fresh)) {
+                // The unit's last sample ended: finish it here, and the lane asks for a unit at
+                // the top of the next iteration.
+                finish_unit<MODE, LSUM>(P, ps);
+                record_tile_cost(P, ps);
+                st = ST_NEED_UNIT;
             }
         }
+        smp_w += __popcll(__ballot(fresh));
     }
     STAMP_FLUSH;
     if (lane == 0) {
