@@ -175,9 +175,11 @@ def main() -> int:
     ap.add_argument("--no-side-lines", action="store_true", help="skip the other-stream and brute-force lines")
     ap.add_argument("--profile", action="store_true", help="short run for rocprofv3 (no side legs, one frame in flight)")
     ap.add_argument("--walk", type=int, default=0, help="LBVH walk form (A/B only): 0 auto, 6 one LDS copy, 10 L2")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=1,
                     help="frames in flight: contexts + streams used round robin, so frame k+1's blocks start on "
-                         "the CUs frame k's tail leaves idle (1 = one frame at a time)")
+                         "the CUs frame k's tail leaves idle. Default 1: with sample chunks the tail is short "
+                         "and a second frame only interferes (1080p / 10 000 spp: 14 008-14 040 vs 13 822-"
+                         "13 985 Msamples/s; 1920x136: 31 626-31 750 vs 31 151-31 365; DESIGN.md §6)")
     args = ap.parse_args()
     W0, H0, spp0, grid0, accel0 = CONFIGS[args.config]
     W, H = args.width or W0, args.height or H0
