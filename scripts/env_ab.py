@@ -11,12 +11,13 @@ sys.path.insert(0, "ray-tracing-gpu-vulkan_amd")
 import torch  # noqa: E402
 import rtvk  # noqa: E402
 
-W, H = 1920, 1080
+W, H = int(os.environ.get("AB_W", 1920)), int(os.environ.get("AB_H", 1080))   # AB_W / AB_H / AB_K: frame, scene
+RNG = rtvk.HASH if os.environ.get("AB_RNG", "stream") == "hash" else rtvk.STREAM   # AB_RNG=hash
 var = sys.argv[1]
 spps = [int(x) for x in sys.argv[2].split(",")]
 settings = dict(a.split("=", 1) for a in sys.argv[3:])
 r = rtvk.Renderer(0)
-r.set_scene(rtvk.generateRandomScene())
+r.set_scene(rtvk.generateRandomScene(0.0, int(os.environ.get("AB_K", 11))))
 acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
 out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
 for spp in spps:
@@ -31,7 +32,7 @@ for spp in spps:
                 os.environ[var] = v
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            r.render_device(rci, acc, out, options=rtvk.make_options())
+            r.render_device(rci, acc, out, options=rtvk.make_options(rng_mode=RNG))
             e1.record()
             torch.cuda.synchronize()
             if rnd == 0:

@@ -13,6 +13,7 @@ import rtvk  # noqa: E402
 from rtvk import abi  # noqa: E402
 
 W, H = 1920, 1080
+RNG = rtvk.HASH if os.environ.get("AB_RNG", "stream") == "hash" else rtvk.STREAM   # AB_RNG=hash
 spp = int(sys.argv[1]) if len(sys.argv) > 1 else 100
 lib = abi.load_library()
 r = rtvk.Renderer(0)
@@ -31,7 +32,7 @@ for rep in range(3):
         for i in range(8):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            r.render_device(rci, acc, out, options=rtvk.make_options(accel=2))
+            r.render_device(rci, acc, out, options=rtvk.make_options(accel=2, rng_mode=RNG))
             e1.record()
             torch.cuda.synchronize()
             h = (ctypes.c_uint64 * 68)()
