@@ -97,7 +97,9 @@ typedef struct rt_options {
     uint32_t accumulate;  /* 0: clear the accumulator first (src/vulkan.h:1081-1086); 1: add on top */
     uint32_t sample_base; /* counter modes only: index of this launch's first sample               */
     uint32_t reserved[2]; /* 0 for production. Diagnostics / A/B only: reserved[0] bit 0 = count box
-                             and sphere tests (slower instrumented build, rt_get_stats);
+                             and sphere tests (slower instrumented build, rt_get_stats); bit 1 =
+                             recompute every segment's closest hit by the gated brute force that
+                             backs the deferred AABB gate (tests);
                              reserved[1] = LBVH walk form: 0 automatic (octant node copies in LDS
                              when they fit, else one copy in LDS, else an LDS treelet over L2
                              subtrees), 6 one LDS node copy, 8 octant copies, 10 every node from

@@ -778,6 +778,7 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     P.spp = spp;
     P.max_depth = o.max_depth ? o.max_depth : 50u;
     P.seed_local = o.seed_mode == RT_SEED_LAUNCH_LOCAL;
+    P.force_regate = (o.reserved[0] & 2u) ? 1u : 0u;   // test only: exercise regate_brute everywhere
     P.rng_counter = o.rng_mode == RT_RNG_SAMPLE_COUNTER;
     P.sample_base = o.sample_base;
     P.accumulate = o.accumulate ? 1u : 0u;
@@ -855,10 +856,13 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     // long) short, without paying a unit's start and flush too often (config 3,
     // 10 000 spp, 4 -> 25 chunks -2.0 %; config 5, 1000 spp 4K: 1 / 3 / 7 / 14 chunks 658.6 /
     // 655.3 / 666.0 / 685.9 ms). RT_SAMPLE_CHUNKS forces a count, RT_UNITS_PER_LANE /
-    // RT_UNIT_MIN_SAMPLES the targets.
+    // RT_UNIT_MIN_SAMPLES the targets. The brute-force walk's samples cost ~n/10 times a grid
+    // sample, so its floor scales down with n (488 spheres: 5 samples; config 2, 100 spp: 1 -> 20
+    // chunks).
     uint64_t chunks = 1;
     if (mode == rt::MODE_HASH && spp > 1) {
         uint64_t per_lane = 128, min_samples = 256;
+        if (accel == rt::ACCEL_BRUTE) min_samples = std::min<uint64_t>(256, std::max<uint64_t>(4, 2560 / std::max(1u, d.n_spheres)));
         if (const char* e = std::getenv("RT_UNITS_PER_LANE")) per_lane = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
         if (const char* e = std::getenv("RT_UNIT_MIN_SAMPLES")) min_samples = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
         const uint64_t pixels = uint64_t(band_width) * band_height;

@@ -175,6 +175,7 @@ struct TraceParams {
                                    // atomic per block per wave), the rest unit by unit
     uint32_t first_blocks;         // blocks [0, first_blocks) start on wave id = block (no atomic)
     uint32_t isolate_blocks;       // waves of the first LPT blocks take no further work
+    uint32_t force_regate;         // test only: every segment's winner recomputed by the gated brute force
     const uint32_t* rows;          // optional global row per band row
     const uint32_t* tile_order;    // optional: hand-out rank -> 8x8 tile index (null: row-major)
     uint32_t* tile_cost;           // optional: per 8x8 tile, traced segments of its longest unit

@@ -136,6 +136,7 @@ __device__ __forceinline__ bool aabb_hit(float cx, float cy, float cz, float r, 
 // overlaps the sphere's AABB. The roots divide by a through its reciprocal ia = 1/a, computed
 // once per segment (GLSL's division is 2.5-ulp, and AMD's Vulkan compilers emit
 // x * rcp(y) for it too).
+template <bool GATE = true>
 __device__ __forceinline__ void test_sphere(float cx, float cy, float cz, float rr,
                                             const float* __restrict__ radius, V3 o, V3 d, V3 inv,
                                             float a, float ia, uint32_t id, float& best, uint32_t& bi) {
@@ -148,7 +149,7 @@ __device__ __forceinline__ void test_sphere(float cx, float cy, float cz, float 
         const float t1 = (-b - sq) * ia;
         const float t2 = (-b + sq) * ia;
         const float t = (t1 >= T_MIN) ? t1 : t2;
-        if (t >= T_MIN && t < best && aabb_hit(cx, cy, cz, radius[id], o, inv)) {
+        if (t >= T_MIN && t < best && (!GATE || aabb_hit(cx, cy, cz, radius[id], o, inv))) {
             best = t;
             bi = id;
         }
@@ -173,9 +174,10 @@ __device__ __forceinline__ float4 lds_reload(const float4* p) {
 
 // Four spheres at once (a leaf, or a batch of big spheres): the discriminants of all four are
 // computed branch-free, then each lane loops over only ITS candidates (D >= 0). Inside the loop
-// sit the expensive exact parts (correctly rounded sqrt, the AABB gate); t2 is computed only when
-// t1 < tmin. Candidates are accepted by (t, lowest index), so the visit order of leaves does not
-// matter: the result is the brute-force closest hit. The loop reloads a candidate's record
+// sits the expensive exact part (correctly rounded sqrt); t2 is computed only when t1 < tmin. The
+// AABB gate is not tested here: only the segment's winner is gated, once (winner_gated).
+// Candidates are accepted by (t, lowest index), so the visit order of leaves does not matter: the
+// result is the brute-force closest hit. The loop reloads a candidate's record
 // (rec_of, from LDS or L2) and recomputes its b and D (the same operations, so the same bits)
 // instead of keeping four records and eight partial results live across it: this loop is where
 // the trace kernels' register pressure peaks, and 24 fewer live VGPRs there let them run at 6
@@ -209,7 +211,7 @@ __device__ __forceinline__ void test4(const float4 s0, const float4 s1, const fl
         if (!(t >= T_MIN)) t = (-b + sq) * ia;     // report t1 if t1 >= tmin, else t2
         if (t >= T_MIN && t <= best) {
             const uint32_t id = id_of(k);
-            if ((t < best || id < bi) && aabb_hit(sp.x, sp.y, sp.z, sp.w, o, inv)) {
+            if (t < best || id < bi) {   // AABB gate deferred to the segment's winner (winner_gated)
                 best = t;
                 bi = id;
                 limit = fminf(__builtin_fmaf(t, cull_rel, t + cull_abs), 10000.0f);
@@ -234,7 +236,7 @@ __device__ __forceinline__ void test1(const float4 sp, const uint32_t* __restric
         if (!(t >= T_MIN)) t = (-b + sq) * ia;     // report t1 if t1 >= tmin, else t2
         if (t >= T_MIN && t <= best) {
             const uint32_t id = *id_at;
-            if ((t < best || id < bi) && aabb_hit(sp.x, sp.y, sp.z, sp.w, o, inv)) {
+            if (t < best || id < bi) {   // AABB gate deferred to the segment's winner (winner_gated)
                 best = t;
                 bi = id;
                 limit = fminf(__builtin_fmaf(t, cull_rel, t + cull_abs), 10000.0f);
@@ -247,6 +249,7 @@ __device__ __forceinline__ void test1(const float4 sp, const uint32_t* __restric
 // comes through the scalar cache: 8 spheres (128 B) per iteration as two s_load_dwordx16 issued
 // before any of the 8 tests, feeding the VALU as SGPR operands (13 VALU per sphere, no VGPR
 // loads, no LDS). The host pads geom to a multiple of 8 with spheres that can never report.
+template <bool GATE>
 __device__ __forceinline__ void closest_brute(const rt::TraceParams& P, V3 o, V3 d, V3 inv, float a,
                                               float ia, float& best, uint32_t& bi) {
     // Constant address space: wave-uniform loads through it are emitted as s_load (the 32
@@ -260,7 +263,7 @@ __device__ __forceinline__ void closest_brute(const rt::TraceParams& P, V3 o, V3
         for (uint32_t k = 0; k < 32; ++k) b[k] = g[ib * 32u + k];
 #pragma unroll
         for (uint32_t k = 0; k < 8; ++k)
-            test_sphere(b[4 * k], b[4 * k + 1], b[4 * k + 2], b[4 * k + 3], P.radius, o, d, inv, a, ia,
+            test_sphere<GATE>(b[4 * k], b[4 * k + 1], b[4 * k + 2], b[4 * k + 3], P.radius, o, d, inv, a, ia,
                         ib * 8u + k, best, bi);
     }
 }
@@ -760,7 +763,18 @@ __global__ __launch_bounds__(kBruteBlock, RT_BRUTE_WAVES_PER_SIMD) void rt_trace
             uint32_t bi = 0xffffffffu;
             const V3 inv = v3(rcp_cr(d.x), rcp_cr(d.y), rcp_cr(d.z));
             const float a = dot(d, d);
-            closest_brute(P, o, d, inv, a, rcp_cr(a), best, bi);
+            const float ia = rcp_cr(a);
+            // AABB gate of the winner only: the ungated minimum is the
+            // gated one when it passes; otherwise the gated pass (rare, one lane's own cost)
+            closest_brute<false>(P, o, d, inv, a, ia, best, bi);
+            if (bi != 0xffffffffu) {
+                const float4 g = reinterpret_cast<const float4*>(P.geom)[bi];
+                if (!aabb_hit(g.x, g.y, g.z, P.radius[bi], o, inv)) {
+                    best = T_MAX_SUCC;
+                    bi = 0xffffffffu;
+                    closest_brute<true>(P, o, d, inv, a, ia, best, bi);
+                }
+            }
             if (COUNT) n_sph += P.n_spheres;
             n_seg++;
             ps.segs++;
@@ -1011,6 +1025,55 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
     }
 }
 
+// The AABB gate of the segment's closest hit, tested once after the walk instead of for every
+// candidate that improves the running best (in a divergent tail, each such pass cost the whole
+// wave ~30 VALU). Exact: let R be the ungated winner (smallest (t, id) among the quadratic's
+// reports the walk tested) and W the gated one (the contract's answer). If R passes the gate, R is
+// in the gated set, so W <= R; the walk stops only once the next cell / node starts beyond
+// limit(R) >= limit(W) (t_W <= t_R), and W's AABB entry lies before limit(W) (DESIGN.md §4.3
+// (iii)), so W was tested and R <= W: R = W. If R fails the gate (a rounding corner: the quadratic
+// reports a hit whose ray misses the box; ~1 segment in 7e7 on config 3), the segment's answer is
+// recomputed by the contract's rule itself: gated brute force (regate_brute).
+__device__ __forceinline__ bool winner_gated(const rt::TraceParams& P, const float4* __restrict__ geom4, const Ray& r) {
+    if (r.bi == 0xffffffffu) return true;
+    const float4 g = geom4[r.bi];
+    return aabb_hit(g.x, g.y, g.z, P.radius[r.bi], r.o, r.inv);
+}
+
+// Gated brute force for the lanes in `need` (wave-uniform), one ray at a time with the whole wave:
+// lane k tests spheres k, k + 64, ... in index order (the contract's `t < best` rule keeps the
+// lowest index on ties within a lane), then the wave takes the minimum of (t bits, id) — t >= tmin
+// > 0, so float bits order like the values and the u64 minimum is the (t, lowest id) rule. 64x
+// shorter than one lane walking the whole list (config 5: 99 860 spheres).
+template <bool COUNT>
+__device__ __forceinline__ void regate_brute(const rt::TraceParams& P, const float4* __restrict__ geom4, uint32_t lane,
+                                          unsigned long long need, Ray& r) {
+    if (COUNT && lane == 0) atomicAdd(&P.counters->util[30], (unsigned long long)__popcll(need));
+    while (need) {
+        const int L = __ffsll(need) - 1;
+        need &= need - 1ull;
+        const V3 o = v3(__shfl(r.o.x, L), __shfl(r.o.y, L), __shfl(r.o.z, L));
+        const V3 d = v3(__shfl(r.d.x, L), __shfl(r.d.y, L), __shfl(r.d.z, L));
+        const V3 inv = v3(__shfl(r.inv.x, L), __shfl(r.inv.y, L), __shfl(r.inv.z, L));
+        const float a = __shfl(r.a, L), ia = __shfl(r.ia, L);
+        float best = T_MAX_SUCC;
+        uint32_t bi = 0xffffffffu;
+        for (uint32_t i = lane; i < P.n_spheres; i += 64u) {
+            const float4 s = geom4[i];
+            test_sphere(s.x, s.y, s.z, s.w, P.radius, o, d, inv, a, ia, i, best, bi);
+        }
+        unsigned long long key = (uint64_t(__float_as_uint(best)) << 32) | bi;
+        for (int off = 32; off > 0; off >>= 1) {
+            const unsigned long long k2 = __shfl_xor(key, off);
+            key = k2 < key ? k2 : key;
+        }
+        if (int(lane) == L) {
+            r.best = __uint_as_float(uint32_t(key >> 32));
+            r.bi = uint32_t(key);
+        }
+    }
+}
+
 // The whole walk of one segment.
 template <bool COUNT, int LAYOUT>
 __device__ __forceinline__ void walk(const rt::TraceParams& P, const float4* __restrict__ nodes4,
@@ -1163,6 +1226,11 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
         if (st == ST_TRACING) setup_ray(P, big, r, n_sph);
         STAMP(2);
         if (st == ST_TRACING) walk<COUNT, LAYOUT>(P, nodes4, leaf4, leaf_ids, r, n_box, n_sph);
+        // the AABB gate of the winner only (winner_gated); the rare lanes whose winner fails it
+        // get the contract's answer by a wave-cooperative gated brute force
+        const unsigned long long regate =
+            __ballot(st == ST_TRACING && (P.force_regate || !winner_gated(P, geom4, r)));
+        if (__builtin_expect(regate != 0ull, 0)) regate_brute<COUNT>(P, geom4, lane, regate, r);
         if (COUNT && st == ST_TRACING) {   // walk-length histogram (diagnostic, COUNT builds only)
             const uint32_t len = min(n_box - box0, 63u);
             atomicAdd(&P.counters->walk_hist[r.bi != 0xffffffffu ? 1 : 0][len], 1ull);

@@ -75,9 +75,12 @@ def main():
                     torch.cuda.synchronize()
                     cs = rtvk.Stats()
                     assert lib.rt_get_stats(ctx, ctypes.byref(cs)) == 0
+                    u32 = (ctypes.c_uint64 * 32)()
+                    fb = int(u32[30]) if hasattr(lib, "rt_debug_util") and lib.rt_debug_util(ctx, u32) == 0 else None
                     print(json.dumps({"lib": Path(lp).name, "accel": accel, "walk": cth,
                                       "box_per_seg": round(cs.box_tests / max(1, cs.segments), 3),
-                                      "sphere_per_seg": round(cs.sphere_tests / max(1, cs.segments), 3)}), flush=True)
+                                      "sphere_per_seg": round(cs.sphere_tests / max(1, cs.segments), 3),
+                                      "segments": int(cs.segments), "gate_fallbacks": fb}), flush=True)
                 if r == 0:  # warm-up round doubles as the bit-exactness check
                     img = acc.cpu().numpy()
                     if accel not in ref:

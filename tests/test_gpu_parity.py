@@ -85,7 +85,7 @@ def renderer(rtvk):
 
 def gpu_render(rtvk, renderer, torch, spheres, rci_u32, band_w, band_h, rows=None, accel=LBVH,
                max_depth=50, seed_mode=0, rng_mode=0, accumulate=False, sample_base=0, accum=None,
-               count=False, builder=None):
+               count=False, builder=None, regate=False):
     with tree_builder(builder):
         renderer.set_scene(np.ascontiguousarray(spheres, np.uint8).reshape(-1, 80))
     rci = rtvk.RenderCallInfo.from_buffer_copy(np.ascontiguousarray(rci_u32).tobytes())
@@ -97,6 +97,8 @@ def gpu_render(rtvk, renderer, torch, spheres, rci_u32, band_w, band_h, rows=Non
                             accel=LBVH if accel in WALK_FORM else accel,
                             accumulate=accumulate, sample_base=sample_base, count_tests=count)
     opt.reserved[1] = WALK_FORM.get(accel, 0)
+    if regate:   # every segment's winner recomputed by the deferred AABB gate's fallback
+        opt.reserved[0] |= 2
     renderer.render_device(rci, acc, out, rows=rows_t, options=opt)
     torch.cuda.synchronize()
     st = renderer.stats()
@@ -293,6 +295,25 @@ def test_grid_lattice_axis_rays(rtvk, renderer, torch, oracle, builder):
         for accel in (BRUTE, LBVH, GRID, LBVH_OCT, LBVH_GLOBAL):
             a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=accel, builder=builder)
             assert_same(a, o, ra, ro)
+
+
+@pytest.mark.parametrize("K,builder", [(11, None), (40, "gpu")])
+@pytest.mark.parametrize("accel", [LBVH, LBVH_OCT, LBVH_GLOBAL])
+def test_forced_regate_equals_oracle(rtvk, renderer, torch, oracle, accel, K, builder):
+    """The walks test the AABB gate only for the segment's winner; a winner that fails it is
+    recomputed by a wave-cooperative gated brute force (regate_brute, ~1 segment in 7e7 on config
+    3). Forced here for every segment (options.reserved[0] bit 1): still the oracle's image bit for
+    bit, both streams, host scene (grid / octant tree in LDS) and a device-built 6 404-sphere scene
+    (grid / treelet / tree from L2)."""
+    W, H, spp = 40, 24, 2
+    sc = oracle.generate_scene(0.0, K)
+    rci = oracle.render_call_info(spp, W, H)
+    for rng in (STREAM, HASH):
+        ra, ro, rst = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=rng))
+        a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=accel, rng_mode=rng, builder=builder,
+                              regate=True)
+        assert_same(a, o, ra, ro)
+        assert (st.segments, st.samples) == rst[:2]
 
 
 def test_rows_strip_map(rtvk, renderer, torch, oracle):
