@@ -479,6 +479,7 @@ int set_scene_host(rt_context* ctx, const Sphere* spheres, uint32_t count, hipSt
         up.add(geom, &d.geom);
         up.add(radius, &d.radius);
         d.small_rmax = bvh.small_rmax;
+        d.small_rmin = bvh.small_rmin;
         up.add(mat, &d.mat);
         d.n_big = uint32_t(bvh.big_ids.size());
         up.add(bvh.big_ids, &d.big_ids);
@@ -566,6 +567,7 @@ int set_scene_gpu(rt_context* ctx, const Sphere* d_sph, uint32_t count, hipStrea
     d.n_nodes = sm.n_nodes;
     d.n_leaf = sm.n_leaf_slots;
     d.small_rmax = rt::summary_float(sm.rmax_o);
+    d.small_rmin = rt::summary_float(sm.rmin_o);
     ctx->scene_radius = rt::summary_float(sm.R_o);
     ctx->pad_radius = ctx->scene_radius * 1.01f + 100.0f;   // the build padded for this radius
     ctx->padded_for = ctx->pad_radius;
@@ -812,6 +814,26 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     // 2.75 r + 1.15e-3 t beyond its reported t.
     P.cull_abs = 3.0f * d.small_rmax + 1e-3f;
     P.cull_rel = 2e-3f;
+    // Grid walks: the r-term of the slack is there for quadratic false positives
+    // (computed D >= 0, the line passing eps_d <= 7 u |oc|^2 / r outside the sphere, u = 2^-24)
+    // whose AABB entry lies up to ~1.42 r past t. The grid registers a sphere in every cell its AABB
+    // widened by 64 u R + 1e-3 cell overlaps; the 1e-3-cell part is spare (64 u R covers the DDA's
+    // rounding), so while eps_d <= 1e-3 cell the cell holding the ray's closest approach, reached by
+    // best + 1e-3 + 2e-3 best, already references the sphere. eps_d <= 1e-3 cell holds for |oc| <= T
+    // = sqrt(1e-3 cs r_min / 7u), and t <= 0.95 T - r_max - 1e-3 cs implies |oc| <= T. The reported
+    // t lies within 9.1e-4 |oc| (sqrt of D's error, 14 u |oc|^2) of the true or closest-approach t.
+    P.cull_near_t = -1.0f;
+    P.cull_near_abs = P.cull_abs;
+    if ((accel == rt::ACCEL_GRID || accel == rt::ACCEL_GRID_GLOBAL) && d.small_rmin > 0.0f &&
+        std::isfinite(d.small_rmin)) {
+        const double m = 1e-3 * std::min<double>(d.grid.cs[0], std::min<double>(d.grid.cs[1], d.grid.cs[2]));
+        const double T = std::sqrt(m * double(d.small_rmin) / (7.0 * 0x1p-24));
+        const double tn = 0.95 * T - double(d.small_rmax) - m;
+        if (tn > 0.0 && !std::getenv("RT_GRID_FULL_SLACK")) {   // RT_GRID_FULL_SLACK: A/B only
+            P.cull_near_t = float(tn);
+            P.cull_near_abs = 1e-3f + 1e-3f * d.small_rmax;   // covers 9.1e-4 (r + eps_d) of |oc| - t
+        }
+    }
     P.accum = accum;
     P.out = reinterpret_cast<uint32_t*>(out);
     P.counters = ctx->counters;

@@ -15,6 +15,7 @@ namespace rt {
 struct BuildSummary {
     uint32_t n_big, n_small, n_nodes, n_leaf_slots;
     uint32_t rmax_o, R_o;            // order-preserving bit patterns of small_rmax and R
+    uint32_t rmin_o;                 // ... and of the smallest small radius
     uint32_t cmin_o[3], cmax_o[3];   // centroid bounds of the small spheres (Morton frame)
 };
 float summary_float(uint32_t ordered);

@@ -66,6 +66,7 @@ __global__ void k_init(BuildSummary* S, bool refit) {
         for (int k = 0; k < 3; k++) { S->cmin_o[k] = f2o(INFINITY); S->cmax_o[k] = f2o(-INFINITY); }
     }
     S->rmax_o = f2o(0.0f);
+    S->rmin_o = f2o(INFINITY);
     S->R_o = f2o(0.0f);
 }
 
@@ -130,6 +131,8 @@ __global__ void __launch_bounds__(kBlock) k_reduce(const Sphere* __restrict__ sp
     }
     const uint32_t ro = wave_max(small ? f2o(r) : f2o(0.0f));
     if (__lane_id() == 0) atomicMax(&S->rmax_o, ro);
+    const uint32_t rmo = wave_min(small ? f2o(r) : f2o(INFINITY));
+    if (__lane_id() == 0) atomicMin(&S->rmin_o, rmo);
     if (refit) return;   // the Morton frame belongs to the stored topology
 #pragma unroll
     for (int k = 0; k < 3; k++) {

@@ -295,6 +295,7 @@ void build_lbvh_host(const Sphere* sph, uint32_t n, HostBvh& out, bool sah) {
         const float c[3] = {sph[i].geometry.x, sph[i].geometry.y, sph[i].geometry.z};
         for (int k = 0; k < 3; k++) { cmin[k] = std::min(cmin[k], c[k]); cmax[k] = std::max(cmax[k], c[k]); }
         out.small_rmax = std::max(out.small_rmax, radii[i]);
+        out.small_rmin = std::min(out.small_rmin, radii[i]);   // NaN radii keep INFINITY: slack off
         prims.push_back(Prim{0, i});
     }
     if (prims.empty()) return;

@@ -15,6 +15,7 @@ struct HostBvh {
     std::vector<GeomRec> leaf_geom;   // small spheres in leaf order: center, RADIUS (4 per leaf)
     std::vector<uint32_t> leaf_ids;   // original index per leaf slot
     float small_rmax = 0.0f;          // largest radius inside the tree (traversal slack)
+    float small_rmin = INFINITY;      // smallest one (grid cull slack, rt_api.cpp)
 };
 
 // sah: binned surface-area splits (the default tree for small scenes); else the Morton radix

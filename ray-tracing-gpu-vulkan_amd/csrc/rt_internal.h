@@ -98,6 +98,7 @@ struct DeviceScene {
     float* treelet = nullptr;      // device-built trees: kTreeletCap x 8 floats (ACCEL_LBVH_TOP)
     uint32_t* treelet_count = nullptr;   // device word: nodes in the treelet
     float small_rmax = 0.0f;       // largest radius in the tree
+    float small_rmin = 0.0f;       // smallest (<= 0 or NaN: the grid keeps the full cull slack)
     GridInfo grid{};               // host-built scenes that suit a grid (n_refs = 0: none)
     uint32_t* cell_start = nullptr;
     GeomRec* grid_rec = nullptr;
@@ -198,6 +199,7 @@ struct TraceParams {
     const uint32_t* leaf_ids;
     float cull_abs;                // LBVH node-cull slack: best + cull_abs + cull_rel * best
     float cull_rel;
+    float cull_near_t, cull_near_abs;   // grid walks: best <= cull_near_t uses cull_near_abs instead
     GridInfo grid;                 // ACCEL_GRID
     const uint32_t* cell_start;
     const GeomRec* grid_rec;

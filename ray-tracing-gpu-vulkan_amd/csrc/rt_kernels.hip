@@ -172,6 +172,13 @@ __device__ __forceinline__ float4 lds_reload(const float4* p) {
     return make_float4(v.x, v.y, v.z, v.w);
 }
 
+// Cull limit of a closest-so-far t: best + cull_abs + cull_rel best, with
+// the smaller absolute slack of grid walks for t <= cull_near_t (rt_api.cpp; -1 elsewhere).
+__device__ __forceinline__ float cull_limit(const rt::TraceParams& P, float t) {
+    const float abs_slack = t <= P.cull_near_t ? P.cull_near_abs : P.cull_abs;
+    return fminf(__builtin_fmaf(t, P.cull_rel, t + abs_slack), 10000.0f);
+}
+
 // Four spheres at once (a leaf, or a batch of big spheres): the discriminants of all four are
 // computed branch-free, then each lane loops over only ITS candidates (D >= 0). Inside the loop
 // sits the expensive exact part (correctly rounded sqrt); t2 is computed only when t1 < tmin. The
@@ -185,7 +192,7 @@ __device__ __forceinline__ float4 lds_reload(const float4* p) {
 template <typename RecOf, typename IdOf>
 __device__ __forceinline__ void test4(const float4 s0, const float4 s1, const float4 s2, const float4 s3,
                                       RecOf rec_of, IdOf id_of, V3 o, V3 d, V3 inv, float a, float ia,
-                                      float& best, uint32_t& bi, float& limit, float cull_abs, float cull_rel) {
+                                      float& best, uint32_t& bi, float& limit, const rt::TraceParams& P) {
     const float4 sv[4] = {s0, s1, s2, s3};
     uint32_t cand = 0u;
 #pragma unroll
@@ -214,7 +221,7 @@ __device__ __forceinline__ void test4(const float4 s0, const float4 s1, const fl
             if (t < best || id < bi) {   // AABB gate deferred to the segment's winner (winner_gated)
                 best = t;
                 bi = id;
-                limit = fminf(__builtin_fmaf(t, cull_rel, t + cull_abs), 10000.0f);
+                limit = cull_limit(P, t);
             }
         }
     }
@@ -222,8 +229,8 @@ __device__ __forceinline__ void test4(const float4 s0, const float4 s1, const fl
 
 // One sphere (a grid cell's reference): test4's arithmetic for a single record.
 __device__ __forceinline__ void test1(const float4 sp, const uint32_t* __restrict__ id_at, V3 o, V3 d, V3 inv,
-                                      float a, float ia, float& best, uint32_t& bi, float& limit, float cull_abs,
-                                      float cull_rel) {
+                                      float a, float ia, float& best, uint32_t& bi, float& limit,
+                                      const rt::TraceParams& P) {
     const float rr = sp.w * sp.w;
     const float ocx = o.x - sp.x, ocy = o.y - sp.y, ocz = o.z - sp.z;
     const float b = __builtin_fmaf(ocz, d.z, __builtin_fmaf(ocy, d.y, ocx * d.x));
@@ -239,7 +246,7 @@ __device__ __forceinline__ void test1(const float4 sp, const uint32_t* __restric
             if (t < best || id < bi) {   // AABB gate deferred to the segment's winner (winner_gated)
                 best = t;
                 bi = id;
-                limit = fminf(__builtin_fmaf(t, cull_rel, t + cull_abs), 10000.0f);
+                limit = cull_limit(P, t);
             }
         }
     }
@@ -893,10 +900,10 @@ __device__ __forceinline__ void setup_ray(const rt::TraceParams& P, const BigTab
         float unused_limit = 0.0f;
         test4(b0, b1, b2, b3, [&](uint32_t k) { return lds_reload(big.rec + k0 + k); },
                     [&](uint32_t k) { return k == 0 ? id.x : k == 1 ? id.y : k == 2 ? id.z : id.w; },
-              r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, unused_limit, 0.0f, 0.0f);
+              r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, unused_limit, P);
     }
     n_sph += P.n_big;
-    r.limit = fminf(__builtin_fmaf(r.best, P.cull_rel, r.best + P.cull_abs), 10000.0f);
+    r.limit = cull_limit(P, r.best);
     r.walk = P.nodes != nullptr || P.cell_start != nullptr;
 }
 
@@ -914,7 +921,7 @@ __device__ __forceinline__ void leaf_test(const rt::TraceParams& P, const float4
                        return make_float4(v.x, v.y, v.z, v.w);
                    },
                     [&](uint32_t k) { return leaf_ids[first + k]; }, r.o, r.d, r.inv, r.a, r.ia, r.best,
-                    r.bi, r.limit, P.cull_abs, P.cull_rel);
+                    r.bi, r.limit, P);
     if (COUNT) n_sph += count;
 }
 
@@ -995,14 +1002,14 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
           for (; j + 1 < e; j += 2) {
             UTIL(1, true);
             const float4 s0 = rec[j], s1 = rec[j + 1];
-            test1(s0, ids + j, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P.cull_abs, P.cull_rel);
-            test1(s1, ids + j + 1, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P.cull_abs, P.cull_rel);
+            test1(s0, ids + j, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
+            test1(s1, ids + j + 1, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
             if (COUNT) n_sph += 2;
           }
         }
         for (; j < e; ++j) {   // from LDS one at a time (pairs measured 1 % slower there)
             UTIL(1, true);
-            test1(rec[j], ids + j, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P.cull_abs, P.cull_rel);
+            test1(rec[j], ids + j, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
             if (COUNT) n_sph++;
         }
         UTIL(0, true);
