@@ -820,16 +820,20 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     // widened by 64 u R + 1e-3 cell overlaps; the 1e-3-cell part is spare (64 u R covers the DDA's
     // rounding), so while eps_d <= 1e-3 cell the cell holding the ray's closest approach, reached by
     // best + 1e-3 + 2e-3 best, already references the sphere. eps_d <= 1e-3 cell holds for |oc| <= T
-    // = sqrt(1e-3 cs r_min / 7u), and t <= 0.95 T - r_max - 1e-3 cs implies |oc| <= T. The reported
+    // = sqrt(1e-3 cs r_min / 7u) (3/4 of that budget below), and t <= 0.95 T - r_max - 1e-3 cs implies
+    // |oc| <= T. The reported
     // t lies within 9.1e-4 |oc| (sqrt of D's error, 14 u |oc|^2) of the true or closest-approach t.
     P.cull_near_t = -1.0f;
     P.cull_near_abs = P.cull_abs;
     if ((accel == rt::ACCEL_GRID || accel == rt::ACCEL_GRID_GLOBAL) && d.small_rmin > 0.0f &&
         std::isfinite(d.small_rmin)) {
         const double m = 1e-3 * std::min<double>(d.grid.cs[0], std::min<double>(d.grid.cs[1], d.grid.cs[2]));
-        const double T = std::sqrt(m * double(d.small_rmin) / (7.0 * 0x1p-24));
+        // budget: 3/4 of the spare part for eps_d, 1/4 for a walk that starts (at tmin) up to
+        // 9.1e-4 |oc| ~ 9.1e-4 (r + tmin) past a closest approach just behind tmin
+        const double T = std::sqrt(0.75 * m * double(d.small_rmin) / (7.0 * 0x1p-24));
         const double tn = 0.95 * T - double(d.small_rmax) - m;
-        if (tn > 0.0 && !std::getenv("RT_GRID_FULL_SLACK")) {   // RT_GRID_FULL_SLACK: A/B only
+        const bool start_ok = 9.1e-4 * (double(d.small_rmax) + 1e-3) <= 0.25 * m;
+        if (tn > 0.0 && start_ok && !std::getenv("RT_GRID_FULL_SLACK")) {   // RT_GRID_FULL_SLACK: A/B only
             P.cull_near_t = float(tn);
             P.cull_near_abs = 1e-3f + 1e-3f * d.small_rmax;   // covers 9.1e-4 (r + eps_d) of |oc| - t
         }
