@@ -827,7 +827,7 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     P.cull_near_abs = P.cull_abs;
     if ((accel == rt::ACCEL_GRID || accel == rt::ACCEL_GRID_GLOBAL) && d.small_rmin > 0.0f &&
         std::isfinite(d.small_rmin)) {
-        const double m = 1e-3 * std::min<double>(d.grid.cs[0], std::min<double>(d.grid.cs[1], d.grid.cs[2]));
+        const double m = RT_GRID_SPARE * std::min<double>(d.grid.cs[0], std::min<double>(d.grid.cs[1], d.grid.cs[2]));
         // budget: 3/4 of the spare part for eps_d, 1/4 for a walk that starts (at tmin) up to
         // 9.1e-4 |oc| ~ 9.1e-4 (r + tmin) past a closest approach just behind tmin
         const double T = std::sqrt(0.75 * m * double(d.small_rmin) / (7.0 * 0x1p-24));

@@ -35,7 +35,7 @@ bool grid_layout(const float lo[3], const float hi[3], uint32_t m, float rmax, f
     }
     if (cells > (1u << 24)) return false;
     gi.n_cells = uint32_t(cells);
-    gi.margin = margin + 1e-3f * std::min(gi.cs[0], std::min(gi.cs[1], gi.cs[2]));
+    gi.margin = margin + float(RT_GRID_SPARE) * std::min(gi.cs[0], std::min(gi.cs[1], gi.cs[2]));
     for (int k = 0; k < 3; k++) {
         gi.lo_m[k] = gi.gmin[k] - gi.margin;
         gi.hi_m[k] = gi.gmax[k] + gi.margin;

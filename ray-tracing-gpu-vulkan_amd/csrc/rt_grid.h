@@ -29,6 +29,10 @@ bool build_grid_host(const Sphere* spheres, uint32_t n, const std::vector<uint32
 // host build and the device build, rt_build.hip build_grid_gpu). Returns false when the cell count
 // would exceed 2^24. *ref_bound = references at most (each sphere's widened AABB spans at most
 // ceil((2 rmax + 2 margin) / cs) + 1 cells per axis).
+// Spare part of the registration margin, in cells (rt_api.cpp: it bounds the near cull slack).
+#ifndef RT_GRID_SPARE
+#define RT_GRID_SPARE 4e-3
+#endif
 bool grid_layout(const float lo[3], const float hi[3], uint32_t m, float rmax, float margin, float cell_scale,
                  GridInfo& gi, uint64_t* ref_bound);
 
