@@ -505,7 +505,7 @@ int set_scene_host(rt_context* ctx, const Sphere* spheres, uint32_t count, hipSt
         // RT_GRID=0 disables it, RT_GRID_SCALE scales the cell size (A/B).
         rt::HostGrid grid;
         const char* ge = std::getenv("RT_GRID");
-        const float gscale = std::getenv("RT_GRID_SCALE") ? float(std::atof(std::getenv("RT_GRID_SCALE"))) : 2.2f;
+        const float gscale = std::getenv("RT_GRID_SCALE") ? float(std::atof(std::getenv("RT_GRID_SCALE"))) : rt::kGridCellScale;
         if (!(ge && std::strcmp(ge, "0") == 0) &&
             rt::build_grid_host(spheres, count, bvh.big_ids, 64.0f * 0x1p-24f * ctx->pad_radius, gscale, 1u << 22,
                                 grid)) {
@@ -590,7 +590,7 @@ int set_scene_gpu(rt_context* ctx, const Sphere* d_sph, uint32_t count, hipStrea
         rt::GridInfo gi;
         uint64_t bound = 0;
         if (rt::grid_layout(lo, hi, sm.n_small, d.small_rmax, 64.0f * 0x1p-24f * ctx->pad_radius,
-                            gs ? float(std::atof(gs)) : 2.2f, gi, &bound) && bound <= (1u << 26)) {
+                            gs ? float(std::atof(gs)) : rt::kGridCellScale, gi, &bound) && bound <= (1u << 26)) {
             uint32_t* cursor = nullptr;
             void* tmp = nullptr;
             const size_t tb = rt::grid_scan_bytes(gi.n_cells);

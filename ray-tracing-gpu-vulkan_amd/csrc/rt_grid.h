@@ -29,6 +29,11 @@ bool build_grid_host(const Sphere* spheres, uint32_t n, const std::vector<uint32
 // host build and the device build, rt_build.hip build_grid_gpu). Returns false when the cell count
 // would exceed 2^24. *ref_bound = references at most (each sphere's widened AABB spans at most
 // ceil((2 rmax + 2 margin) / cs) + 1 cells per axis).
+// Cells sized for about kGridCellScale^3 small spheres per cell volume. Measured at config 3 / 5
+// (scripts/scale_ab.py, images bit-identical): 1.5 / 1.7 / 1.9 / 2.2 / 2.6 / 3.0 ->
+// 138.4 / 137.8 / 138.4 / 139.3 / 141.9 / 147.0 ms and 15.31 / 15.17 / 15.28 / 15.39 / 15.49 / 15.88 ms.
+constexpr float kGridCellScale = 1.7f;
+
 // Spare part of the registration margin, in cells (rt_api.cpp: it bounds the near cull slack).
 #ifndef RT_GRID_SPARE
 #define RT_GRID_SPARE 4e-3
