@@ -270,6 +270,36 @@ def test_empty_and_single_sphere(rtvk, renderer, torch, oracle):
 
 
 @pytest.mark.parametrize("builder", [None, "gpu"])
+def test_grid_near_cull_slack_mixed_radii(rtvk, renderer, torch, oracle, builder):
+    """The grid walks' small cull slack depends on the smallest and largest small
+    radius: a scene of 300 spheres with radii 0.06-0.45 (the grid's 8:1 limit), cameras inside and
+    far outside it. The default slack, the full slack (RT_GRID_FULL_SLACK=1) and the oracle agree
+    bit for bit, both streams, host (LDS) and device (L2) grids."""
+    rng = np.random.default_rng(7)
+    base = oracle.generate_scene()[4:5]
+    recs = [oracle.generate_scene()[:1].copy()]   # the ground sphere
+    for _ in range(300):
+        r = base.copy()
+        rad = float(rng.uniform(0.06, 0.45))
+        r[0, :16].view(np.float32)[:] = [rng.uniform(-6, 6), rad, rng.uniform(-6, 6), rad]
+        recs.append(r)
+    sc = np.concatenate(recs)
+    W, H = 48, 32
+    for cam, look in [((2.0, 0.6, -3.0), (0.0, 0.3, 0.0)), ((25.0, 9.0, -25.0), (0.0, 0.0, 0.0))]:
+        rci = oracle.render_call_info(3, W, H)
+        f = rci.view(np.float32)
+        f[8:11] = cam
+        f[12:15] = [look[k] - cam[k] for k in range(3)]
+        for rng_mode in (STREAM, HASH):
+            ra, ro, _ = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=rng_mode))
+            for full in (None, "1"):
+                with env(RT_GRID_FULL_SLACK=full):
+                    a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH, rng_mode=rng_mode,
+                                         builder=builder)
+                assert_same(a, o, ra, ro)
+
+
+@pytest.mark.parametrize("builder", [None, "gpu"])
 def test_grid_lattice_axis_rays(rtvk, renderer, torch, oracle, builder):
     """Uniform-grid stress: spheres on an integer lattice (centers, AABB faces and cell boundaries
     coincide or nearly so), camera looking exactly along +z through the lattice (zero direction
