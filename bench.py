@@ -14,8 +14,15 @@ per-sample LCG starts, fixed-point sums, samples of a pixel split into chunks ov
 "stream" (the reference's per-pixel LCG stream). Both are bit-exact against the CPU oracle; the
 N = 1 line also times the other stream on the same frame (`reference_stream`).
 
-Launch: python bench.py [--gpus 1 --steps 3 --warmup 1]
-        python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+Launch modes (the line's config.path names the one that ran):
+  python bench.py [--gpus 1 --steps 3 --warmup 1]         single: one Renderer on one GPU
+  python bench.py --gpus N                                 multi: rt_multi over N GPUs in ONE process
+        (the C-ABI path behind the reference's ray_trace(gpu_count): ncclCommInitAll, strips, RCCL
+        gather to GPU 0); exits non-zero when fewer than N GPUs are visible
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+                                                           per-process: one rank per GPU, RCCL gather
+        to rank 0 (rtvk.dist); exits non-zero when WORLD_SIZE != --gpus
+At N > 1 the line carries n1_check: the gathered frame against the same frame rendered on one GPU.
 Rank 0 prints one JSON line (DESIGN.md §6 explains every field).
 """
 from __future__ import annotations
@@ -156,6 +163,50 @@ def pmc_record(key: str, sha: str) -> dict:
     return {k: rec[k] for k in ("valu_issue_busy", "lane_util", "hbm_bytes_per_launch", "kernel_ms") if k in rec}
 
 
+WALK_NAMES = {   # rt_debug_launch_info form -> (kernel, walk)
+    "lbvh-octant-lds": ("rt_trace_lds_kernel<8 octant copies>", "LBVH, 8 octant node copies staged in LDS"),
+    "lbvh-lds": ("rt_trace_lds_kernel<1 copy>", "LBVH, one node copy staged in LDS"),
+    "lbvh-treelet": ("rt_trace_top_kernel", "LBVH, LDS treelet over L2 subtrees"),
+    "lbvh-global": ("rt_trace_global_kernel", "LBVH, every node from L2"),
+    "grid-lds": ("rt_trace_grid_kernel<grid in LDS>", "uniform grid (3D DDA), staged in LDS"),
+    "grid-global": ("rt_trace_grid_kernel<grid from L2>", "uniform grid (3D DDA), from L2"),
+}
+
+
+def roofline_block(cs, scale, form: str, kernel_ms: float, step_ms: float, n_gpus: int, sha: str, pmc: dict,
+                   basis: str) -> dict:
+    """VALU FP32 roofline of the dominant (trace) kernel: algorithmic FLOP of one launch (counts
+    of the instrumented build x scale) / the launch's duration measured inside the timed region."""
+    grid_walk = form.startswith("grid")
+    flop_step = FLOP_PER_CELL_STEP if grid_walk else FLOP_PER_BOX_TEST
+    bytes_step = BYTES_PER_CELL_STEP if grid_walk else BYTES_PER_BOX_TEST
+    flops = (cs.box_tests * flop_step + cs.sphere_tests * FLOP_PER_SPHERE_TEST) * scale
+    peak = VALU_FP32_PEAK_TFLOPS * n_gpus
+    achieved = flops / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
+    roof = {"bound": "valu-fp32", "achieved": round(achieved, 3), "peak": round(peak, 1), "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": pmc.get("hbm_bytes_per_launch"),
+            "kernel": WALK_NAMES.get(form, (form,))[0], "kernel_ms": round(kernel_ms, 4), "frac_basis": basis,
+            "frac_per_step": round(flops / (step_ms * 1e-3) / 1e12 / peak, 4),
+            "flop_per_launch": int(flops),
+            ("cell_steps" if grid_walk else "box_tests"): int(cs.box_tests * scale),
+            "sphere_tests": int(cs.sphere_tests * scale),
+            "flop_model": (f"{flop_step}/{'grid cell step' if grid_walk else 'box test'} + 23/sphere test "
+                           f"(SURVEY.md 8(d)); counts from the instrumented build of the same kernel"
+                           + (f", x{scale:g} to the frame's spp" if scale != 1 else "")),
+            "lib_sha256": sha}
+    roof.update({k: v for k, v in pmc.items() if k in ("valu_issue_busy", "lane_util", "pmc")})
+    if "valu_issue_busy" in pmc and "lane_util" in pmc:
+        # every executed lane-op (traversal control, shading, sampling included) against peak
+        roof["valu_lane_frac"] = round(pmc["valu_issue_busy"] * pmc["lane_util"], 4)
+    lds_bytes = (cs.box_tests * bytes_step + cs.sphere_tests * BYTES_PER_SPHERE_TEST) * scale
+    lds_tbps = lds_bytes / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
+    roof["lds"] = {"achieved": round(lds_tbps, 3), "peak": round(LDS_PEAK_TBPS * n_gpus, 1), "unit": "TB/s",
+                   "frac": round(lds_tbps / (LDS_PEAK_TBPS * n_gpus), 4), "bytes_per_launch": int(lds_bytes),
+                   "model": (f"{bytes_step} B per {'cell step' if grid_walk else 'box test'} + 16 B per sphere test "
+                             "(from L2 instead of LDS for walks whose structure does not fit LDS)")}
+    return roof
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -166,20 +217,27 @@ def main() -> int:
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--grid", type=int, default=None, help="scene grid half extent (11: 488 spheres)")
-    ap.add_argument("--accel", choices=["lbvh", "brute"], default=None)
+    ap.add_argument("--accel", choices=["lbvh", "brute"], default=None,
+                    help="lbvh: the accelerated walk the library picks (uniform grid when it fits, else "
+                         "LBVH; --walk forces one); brute: every sphere per segment")
     ap.add_argument("--rng", choices=["hash", "stream"], default="hash")
+    ap.add_argument("--path", choices=["auto", "single", "multi"], default="auto",
+                    help="without a torch.distributed launcher: 'single' = one Renderer (one GPU), 'multi' = "
+                         "rt_multi over --gpus GPUs in this process (the C-ABI path behind ray_trace(gpu_count)); "
+                         "auto = single at --gpus 1, multi above")
     ap.add_argument("--count-spp", type=int, default=100,
                     help="spp of the instrumented (test-counting) launch; its counts are scaled to the frame's "
                          "spp (per-sample statistics are stationary: same scene, same streams)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-side-lines", action="store_true", help="skip the other-stream and brute-force lines")
+    ap.add_argument("--no-side-lines", action="store_true",
+                    help="skip the other-stream, LBVH-walk and brute-force lines")
     ap.add_argument("--profile", action="store_true", help="short run for rocprofv3 (no side legs, one frame in flight)")
-    ap.add_argument("--walk", type=int, default=0, help="LBVH walk form (A/B only): 0 auto, 6 one LDS copy, 10 L2")
+    ap.add_argument("--walk", type=int, default=0,
+                    help="walk form (A/B only): 0 auto, 6 one LDS LBVH copy, 8 octant LBVH copies, 10 LBVH from L2, "
+                         "12 grid")
     ap.add_argument("--inflight", type=int, default=1,
-                    help="frames in flight: contexts + streams used round robin, so frame k+1's blocks start on "
-                         "the CUs frame k's tail leaves idle. Default 1: with sample chunks the tail is short "
-                         "and a second frame only interferes (1080p / 10 000 spp: 14 008-14 040 vs 13 822-"
-                         "13 985 Msamples/s; 1920x136: 31 626-31 750 vs 31 151-31 365; DESIGN.md §6)")
+                    help="frames in flight (single path): contexts + streams used round robin. Default 1: with "
+                         "sample chunks the tail is short and a second frame only interferes (DESIGN.md §6)")
     args = ap.parse_args()
     W0, H0, spp0, grid0, accel0 = CONFIGS[args.config]
     W, H = args.width or W0, args.height or H0
@@ -197,19 +255,36 @@ def main() -> int:
     from rtvk import abi
     from rtvk.dist import DistributedRenderer, hip_assembler, hip_band_renderer
 
+    launched = "WORLD_SIZE" in os.environ
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if launched and world != args.gpus:
+        print(f"error: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        return 2
+    if launched and world > 1:
+        mode = "per-process"
+    elif args.path == "multi" or (args.path == "auto" and args.gpus > 1):
+        mode = "multi"
+    else:
+        mode = "single"
+    n_vis = torch.cuda.device_count()
+    if mode != "per-process" and args.gpus > max(1, n_vis):
+        print(f"error: --gpus {args.gpus} but only {n_vis} GPU(s) visible; refusing to report a smaller run",
+              file=sys.stderr)
+        return 2
+    if mode == "single" and args.gpus != 1:
+        print("error: --path single renders on one GPU; use --gpus 1", file=sys.stderr)
+        return 2
+    n_gpus = args.gpus
     # RCCL (backend "nccl"); RT_BENCH_BACKEND=gloo rehearses N ranks sharing the visible GPUs
     # (bands staged through host memory): a test of the N > 1 code path, never a reported number.
     backend = os.environ.get("RT_BENCH_BACKEND", "nccl")
     if backend != "nccl":
-        local = local % max(1, torch.cuda.device_count())
+        local = local % max(1, n_vis)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if mode == "per-process":
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -221,172 +296,197 @@ def main() -> int:
     rci = rtvk.canonical_render_call_info(spp, W, H)
     opts = rtvk.make_options(accel=accel, rng_mode=rng_mode)
     opts.reserved[1] = args.walk
-    ev = []
+    cnt_opts = rtvk.make_options(accel=accel, rng_mode=rng_mode, count_tests=True)
+    cnt_opts.reserved[1] = args.walk
+    cnt_spp = max(1, min(spp, args.count_spp))
+    cnt_rci = rtvk.canonical_render_call_info(cnt_spp, W, H)
+    scale = spp / cnt_spp
 
-    def timed(fn):
-        """fn(*a) bracketed by HIP events on the stream it is launched on (the slot's)."""
-        def run(*a):
-            st = torch.cuda.current_stream()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(st)
-            fn(*a)
-            e1.record(st)
-            ev.append((e0, e1))
-        return run
-
-    class Slot:
-        """One frame in flight: its own context (scene blob, counters, LPT history), stream and
-        frame buffers; frames go to the slots round robin."""
-        def __init__(self):
-            self.renderer = rtvk.Renderer(local)
-            self.stream = torch.cuda.Stream(device=dev)
-            with torch.cuda.stream(self.stream):
-                self.dr = DistributedRenderer(W, H, dev, timed(hip_band_renderer(self.renderer, rci, opts)),
-                                              hip_assembler(self.renderer))
-
-        def frame(self):
-            # The reference rebuilds its acceleration structure every frame (src/vulkan.h:1020-1059)
-            # and SURVEY.md 8(d) counts the build in the wall clock: rebuild, then render + gather.
-            # The host build runs while earlier frames render (its upload is queued behind them).
-            with torch.cuda.stream(self.stream):
-                self.renderer.set_scene(scene, stream=self.stream)
-                return self.dr.step()
-
-    slots = [Slot() for _ in range(max(1, args.inflight))]
-    renderer, dr = slots[0].renderer, slots[0].dr
-    torch.cuda.synchronize()
-    t_scene = time.perf_counter()
-    renderer.set_scene(scene)
-    torch.cuda.synchronize()
-    t_scene = time.perf_counter() - t_scene
+    def sync_all():
+        for d in range(n_gpus if mode == "multi" else 1):
+            torch.cuda.synchronize(d if mode == "multi" else dev)
 
     def barrier():
-        torch.cuda.synchronize()
-        if world > 1:
+        sync_all()
+        if mode == "per-process":
             dist.barrier()
-        torch.cuda.synchronize()
+        sync_all()
 
-    n_frames = 0
+    multi_info = None
+    if mode == "multi":
+        # One process drives every GPU through the C-ABI (rt_multi: ncclCommInitAll, 8-row strips
+        # dealt round robin, grouped ncclSend / ncclRecv of every strip to GPU 0, reorder there):
+        # the code the reference's ray_trace(gpu_count) binds (src/ray_trace.cpp:42-105, :922-972).
+        mr = rtvk.MultiRenderer(n_gpus)
+        if mr.device_count != n_gpus:
+            print(f"error: rt_multi opened {mr.device_count} devices, asked for {n_gpus}", file=sys.stderr)
+            return 2
+        acc0 = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda:0")
+        out0 = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda:0")
+        t_scene = time.perf_counter()
+        mr.set_scene(scene)
+        sync_all()
+        t_scene = time.perf_counter() - t_scene
 
-    def frame():
-        nonlocal n_frames
-        r = slots[n_frames % len(slots)].frame()
-        n_frames += 1
-        return r
+        def frame():
+            # per-frame rebuild as the reference does (src/vulkan.h:1020-1059), then render + gather
+            mr.set_scene(scene)
+            mr.render(rci, acc0, out0, options=opts)
+            return acc0, out0
+    else:
+        ev_slots = []
 
-    for _ in range(max(args.warmup, len(slots))):   # every slot has rendered once (LPT order)
+        class Slot:
+            """One frame in flight: its own context (scene blob, counters, LPT history), stream and
+            frame buffers; frames go to the slots round robin."""
+            def __init__(self):
+                self.renderer = rtvk.Renderer(local)
+                self.stream = torch.cuda.Stream(device=dev)
+                with torch.cuda.stream(self.stream):
+                    self.dr = DistributedRenderer(W, H, dev, hip_band_renderer(self.renderer, rci, opts),
+                                                  hip_assembler(self.renderer))
+                self.launches = 0
+
+            def frame(self):
+                # The reference rebuilds its acceleration structure every frame (src/vulkan.h:1020-1059)
+                # and SURVEY.md 8(d) counts the build in the wall clock: rebuild, then render (+ gather).
+                with torch.cuda.stream(self.stream):
+                    self.renderer.set_scene(scene, stream=self.stream)
+                    self.launches += 1
+                    return self.dr.step()
+
+        slots = [Slot() for _ in range(max(1, args.inflight if mode == "single" else 1))]
+        renderer, dr = slots[0].renderer, slots[0].dr
+        sync_all()
+        t_scene = time.perf_counter()
+        renderer.set_scene(scene)
+        sync_all()
+        t_scene = time.perf_counter() - t_scene
+        n_frames = 0
+
+        def frame():
+            nonlocal n_frames
+            r = slots[n_frames % len(slots)].frame()
+            n_frames += 1
+            return r
+
+    for _ in range(max(args.warmup, 1 if mode == "multi" else len(slots))):   # LPT order, occupancy
         frame()
     barrier()
-    ev.clear()
+    if mode != "multi":
+        for sl in slots:
+            sl.launches = 0
     t0 = time.perf_counter()
     last = None
     for _ in range(args.steps):
         last = frame()
     barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    # trace-kernel durations inside the timed region (HIP events the library records around the
+    # kernel on its launch stream; rt_debug_kernel_times)
+    if mode == "multi":
+        per_dev = mr.kernel_times()   # last frame, each device
+        kernel_ms = max(per_dev) if per_dev else 0.0
+        k_basis = (f"last timed frame, slowest of {len(per_dev)} devices' trace kernels (HIP events on each "
+                   f"launch stream): {', '.join(f'{v:.2f}' for v in per_dev)} ms")
+    else:
+        ks = []
+        for sl in slots:
+            if sl.launches and sl.dr.n:
+                ks += sl.renderer.kernel_times(min(64, sl.launches))
+        kernel_ms = sum(ks) / max(1, len(ks))
+        k_basis = (f"mean trace-kernel duration of the {len(ks)} launches of the timed region (HIP events "
+                   f"recorded by the library around the kernel on its launch stream)")
+    if mode == "per-process":
+        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    kernel_ms_inflight = sum(a.elapsed_time(b) for a, b in ev) / max(1, len(ev))
-    # Kernel duration for the roofline: with frames in flight a launch's events also span the wait
-    # for the CUs the previous frame still holds, so this rank's band is timed alone, back to
-    # back, right after the timed region (same slot, same LPT order).
-    ev.clear()
-    sl0 = slots[0]
-    n_iso = max(2, min(args.steps, 3))
-    for _ in range(n_iso):
-        with torch.cuda.stream(sl0.stream):
-            sl0.dr.render_band(sl0.dr.rows, sl0.dr.accum[: sl0.dr.n], sl0.dr.out[: sl0.dr.n])
-        torch.cuda.synchronize()
-    kernel_ms = sum(a.elapsed_time(b) for a, b in ev) / max(1, len(ev))
-    # the per-frame rebuild alone (host build + upload), outside the timed region
-    torch.cuda.synchronize()
-    tb = time.perf_counter()
-    renderer.set_scene(scene)
-    torch.cuda.synchronize()
-    build_ms = (time.perf_counter() - tb) * 1e3
-    st = renderer.stats()   # this rank's last band
-    info = renderer.launch_info()
+        elapsed, kernel_ms = float(t[0].item()), float(t[1].item())
+        k_basis += f"; max over {world} ranks"
+    step_ms = elapsed / args.steps * 1e3
+
+    # Algorithmic work of one frame, counted by the instrumented build of the same kernel
+    # (identical image, same traversal; outside the timed region).
+    if mode == "multi":
+        st = mr.stats()
+        info = None
+        ca = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda:0")
+        co = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda:0")
+        mr.render(cnt_rci, ca, co, options=cnt_opts)
+        sync_all()
+        cs = mr.stats()
+        del ca, co
+        multi_info = mr.info()
+        # the walk form of device 0's context (every device renders the same scene the same way)
+        probe = rtvk.Renderer(0)
+        probe.set_scene(scene)
+        pa = torch.zeros((8, W, 4), dtype=torch.float32, device="cuda:0")
+        po = torch.zeros((8, W, 4), dtype=torch.uint8, device="cuda:0")
+        probe.render_device(rtvk.canonical_render_call_info(1, W, H), pa, po, options=opts)
+        sync_all()
+        info = probe.launch_info()
+        info["chunks"] = None   # per device, chosen for its own band
+        device_built = probe.scene_array(8)["device_built"]
+    else:
+        st = renderer.stats()   # this rank's last band
+        info = renderer.launch_info()
+        device_built = renderer.scene_array(8)["device_built"]
+        if dr.n:
+            acc = torch.zeros((dr.n, W, 4), dtype=torch.float32, device=dev)
+            out = torch.zeros((dr.n, W, 4), dtype=torch.uint8, device=dev)
+            renderer.render_device(cnt_rci, acc, out, rows=dr.rows, options=cnt_opts)
+            sync_all()
+            cs = renderer.stats()
+            del acc, out
+        else:
+            cs = rtvk.Stats()
+        if mode == "per-process":   # whole-frame counts: sum over the ranks
+            t = torch.tensor([cs.box_tests, cs.sphere_tests, st.segments, st.samples], dtype=torch.float64,
+                             device=dev)
+            dist.all_reduce(t)
+            cs = rtvk.Stats(segments=0, samples=0, box_tests=int(t[0].item()), sphere_tests=int(t[1].item()))
+            st = rtvk.Stats(segments=int(t[2].item()), samples=int(t[3].item()), box_tests=0, sphere_tests=0)
+    form = "brute" if accel == abi.RT_ACCEL_BRUTE else info["form"]
 
     samples_per_step = W * H * spp
     value = samples_per_step * args.steps / elapsed / 1e6
-
-    # Algorithmic work of one launch on this rank, counted by the instrumented build of the same
-    # kernel (identical image, same traversal; outside the timed region).
-    local_rows = dr.n
-    cnt_opts = rtvk.make_options(accel=accel, rng_mode=rng_mode, count_tests=True)
-    cnt_opts.reserved[1] = args.walk
-    cnt_spp = max(1, min(spp, args.count_spp))
-    if local_rows:
-        acc = torch.zeros((local_rows, W, 4), dtype=torch.float32, device=dev)
-        out = torch.zeros((local_rows, W, 4), dtype=torch.uint8, device=dev)
-        renderer.render_device(rtvk.canonical_render_call_info(cnt_spp, W, H), acc, out, rows=dr.rows,
-                               options=cnt_opts)
-        torch.cuda.synchronize()
-        cs = renderer.stats()
-        del acc, out
-    else:
-        cs = rtvk.Stats()
-    scale = spp / cnt_spp
-    grid_walk = info["form"].startswith("grid")
-    flop_step = FLOP_PER_CELL_STEP if grid_walk else FLOP_PER_BOX_TEST
-    bytes_step = BYTES_PER_CELL_STEP if grid_walk else BYTES_PER_BOX_TEST
-    flops = (cs.box_tests * flop_step + cs.sphere_tests * FLOP_PER_SPHERE_TEST) * scale
-    achieved = flops / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
-
     result = None
+    frame_np = None
     if rank == 0:
         sha = lib_sha256()
-        kname = {"lbvh-octant-lds": "rt_trace_lds_kernel<8 octant copies>", "lbvh-lds": "rt_trace_lds_kernel<1 copy>",
-                 "lbvh-treelet": "rt_trace_top_kernel (LDS treelet + L2 subtrees)",
-                 "lbvh-global": "rt_trace_global_kernel",
-                 "grid-lds": "rt_trace_grid_kernel<grid in LDS>",
-                 "grid-global": "rt_trace_grid_kernel<grid from L2>"}.get(info["form"], info["form"])
-        if accel == abi.RT_ACCEL_BRUTE:
-            kname = "rt_trace_brute_kernel"
-        key = f"{accel_name}-{args.rng}-{W}x{H}-{spp}spp-grid{grid}-n{world}"
+        key = f"{accel_name}-{args.rng}-{W}x{H}-{spp}spp-grid{grid}-n{n_gpus}"
         pmc = pmc_record(key, sha)
-        roof = {"bound": "valu-fp32", "achieved": round(achieved, 3), "peak": VALU_FP32_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / VALU_FP32_PEAK_TFLOPS, 4),
-                "traffic": pmc.get("hbm_bytes_per_launch"),
-                "kernel": kname, "kernel_ms": round(kernel_ms, 4),
-                "frac_basis": f"per isolated launch: algorithmic FLOP of this rank's band / its launch time, "
-                              f"{n_iso} launches timed alone after the timed region (HIP events on the launch "
-                              f"stream); with frames in flight a launch spans {kernel_ms_inflight:.2f} ms "
-                              "including the wait for the previous frame's CUs",
-                "frac_per_step": round(flops / (elapsed / args.steps) / 1e12 / VALU_FP32_PEAK_TFLOPS, 4),
-                "flop_per_launch": int(flops),
-                ("cell_steps" if grid_walk else "box_tests"): int(cs.box_tests * scale),
-                "sphere_tests": int(cs.sphere_tests * scale),
-                "flop_model": (f"{flop_step}/{'grid cell step' if grid_walk else 'box test'} + 23/sphere test "
-                               f"(SURVEY.md 8(d)); counts from the instrumented build of the same kernel at "
-                               f"{cnt_spp} spp" + (f", x{scale:g}" if scale != 1 else "")),
-                "lib_sha256": sha}
-        roof.update({k: v for k, v in pmc.items() if k in ("valu_issue_busy", "lane_util", "pmc")})
-        if "valu_issue_busy" in pmc and "lane_util" in pmc:
-            # every executed lane-op (traversal control, shading, sampling included) against peak
-            roof["valu_lane_frac"] = round(pmc["valu_issue_busy"] * pmc["lane_util"], 4)
-        if accel != abi.RT_ACCEL_BRUTE:   # the other fraction SURVEY.md 8(d) asks for: the LBVH's own bytes
-            lds_bytes = (cs.box_tests * bytes_step + cs.sphere_tests * BYTES_PER_SPHERE_TEST) * scale
-            lds_tbps = lds_bytes / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
-            roof["lds"] = {"achieved": round(lds_tbps, 3), "peak": round(LDS_PEAK_TBPS, 1), "unit": "TB/s",
-                           "frac": round(lds_tbps / LDS_PEAK_TBPS, 4), "bytes_per_launch": int(lds_bytes),
-                           "model": (f"{bytes_step} B per {'cell step' if grid_walk else 'box test'} + 16 B per "
-                                     "sphere test (from L2 instead of LDS for walks whose structure does not fit "
-                                     "LDS)")}
-        cfg_name = (f"BASELINE config {args.config}" if world == 1 or args.config not in (3, 4)
-                    else f"BASELINE config {4 if world == 8 else 3} frame on {world} GPUs")
+        if accel == abi.RT_ACCEL_BRUTE:
+            flops = st.segments * len(scene) * FLOP_PER_SPHERE_TEST
+            peak = VALU_FP32_PEAK_TFLOPS * n_gpus
+            ach = flops / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
+            roof = {"bound": "valu-fp32", "achieved": round(ach, 3), "peak": round(peak, 1), "unit": "TFLOP/s",
+                    "frac": round(ach / peak, 4), "traffic": pmc.get("hbm_bytes_per_launch"),
+                    "kernel": "rt_trace_brute_kernel", "kernel_ms": round(kernel_ms, 4), "frac_basis": k_basis,
+                    "frac_per_step": round(flops / (step_ms * 1e-3) / 1e12 / peak, 4), "lib_sha256": sha}
+        else:
+            roof = roofline_block(cs, scale, form, kernel_ms, step_ms, n_gpus, sha, pmc, k_basis)
+        cfg_name = (f"BASELINE config {args.config}" if n_gpus == 1 or args.config not in (3, 4)
+                    else f"BASELINE config {4 if n_gpus == 8 else 3} frame on {n_gpus} GPUs")
         default_shape = (W, H, spp, grid, accel_name) == CONFIGS[args.config]
+        walk = "brute-force sphere list (scalar cache)" if form == "brute" else WALK_NAMES.get(form, (form, form))[1]
+        if mode == "multi":
+            par = (f"rt_multi (C-ABI, one process): {multi_info['devices']} GPUs, {multi_info['strip_rows']}-row "
+                   f"strips dealt round robin, RCCL grouped ncclSend/ncclRecv gather of every strip to GPU 0 "
+                   f"(ncclCommInitAll communicator of {multi_info['rccl_ranks']} ranks) + device reorder")
+        elif mode == "per-process":
+            par = (f"torch.distributed ({backend}): {world} processes, one per GPU, 8-row strips round robin + "
+                   f"gather to rank 0 + device reorder")
+        else:
+            par = "1 GPU"
         result = {
             "metric": "Msamples/s (1920x1080 RTIOW scene, depth 50)" if (W, H) == (1920, 1080)
                       else f"Msamples/s ({W}x{H} RTIOW scene, depth 50)",
             "value": round(value, 2),
             "unit": "Msamples/s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step": round(step_ms, 4),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -394,30 +494,46 @@ def main() -> int:
             "data": f"synthetic: canonical scene generateRandomScene(t=0), grid {2 * grid}x{2 * grid} "
                     f"({len(scene)} spheres), camera (13,11,-3) -> origin, global per-pixel seeds "
                     f"TEA(TEA(x,y),0), {'counter-based per-sample streams (RT_RNG_SAMPLE_HASH)' if args.rng == 'hash' else 'the reference per-pixel LCG stream'}",
-            "config": {"workload": f"rtiow-{W}x{H}-{spp}spp-depth50-{accel_name}"
-                                   + (f" ({cfg_name})" if default_shape else " (custom)"),
+            "config": {"workload": f"rtiow-{W}x{H}-{spp}spp-depth50"
+                                   + (f" ({cfg_name} workload)" if default_shape else " (custom)"),
                        "width": W, "height": H, "spp": spp, "depth": 50, "spheres": len(scene),
-                       "accel": accel_name, "rng": args.rng, "sample_chunks": info["chunks"],
-                       "parallelism": f"8-row strips x{world} + rccl gather to rank 0",
-                       "frames_in_flight": len(slots)},
+                       "accel": form, "walk": walk,
+                       "structure_build": ("device (Morton + radix sort + Karras LBVH, device grid)" if device_built
+                                           else "host (binned-SAH LBVH + uniform grid), uploaded per frame"),
+                       "rng": args.rng, "sample_chunks": info["chunks"],
+                       "path": mode, "parallelism": par,
+                       "frames_in_flight": 1 if mode == "multi" else len(slots)},
             "segments_per_sample": round(st.segments / max(1, st.samples), 4),
             "scene_setup_ms": round(t_scene * 1e3, 2),
-            "scene_build_ms": round(build_ms, 3),
-            "tree": "device-lbvh" if renderer.scene_array(8)["device_built"] else "host-sah",
             "msegments_per_s": round(st.segments / max(1, st.samples) * value, 2),
             "roofline": roof,
-            **({"rehearsal": f"{backend} backend, {world} ranks sharing {torch.cuda.device_count()} GPU(s): "
-                               "code-path test, not a measurement"} if backend != "nccl" else {}),
+            "build": abi.build_info(),
+            **({"rehearsal": f"{backend} backend, {world} ranks sharing {n_vis} GPU(s): "
+                               "code-path test, not a measurement"} if backend != "nccl" and mode == "per-process" else {}),
             "context": {"reference_rx6800xt_vulkan_rt_msamples": 1658.9,
                         "source": "README.md:57,61 via BASELINE.md (different GPU, HW RT cores)"},
         }
-    frame_np = None
-    if rank == 0 and world == 1:
         fa, fo = last
-        frame_np = (fa.cpu().numpy(), fo.cpu().numpy())
-    # Side lines (N = 1): the same frame with the other random stream, and BASELINE config 2 as
-    # specified (100 spp, brute force).
-    if world == 1 and not args.no_side_lines and not args.profile:
+        if n_gpus > 1:
+            # N > 1 verifies itself: the gathered frame against this frame rendered on ONE GPU
+            r1 = rtvk.Renderer(local)
+            r1.set_scene(scene)
+            a1 = torch.zeros((H, W, 4), dtype=torch.float32, device=dev)
+            o1 = torch.zeros((H, W, 4), dtype=torch.uint8, device=dev)
+            r1.render_device(rci, a1, o1, options=opts)
+            torch.cuda.synchronize(dev)
+            fa_d, fo_d = fa.to(dev), fo.to(dev)
+            result["n1_check"] = {
+                "pixels": W * H, "accum_bit_equal": bool(torch.equal(fa_d, a1)),
+                "rgba8_equal": bool(torch.equal(fo_d, o1)),
+                "what": "gathered N-GPU frame vs the same frame rendered by one GPU (same seeds, same stream)"}
+            result["rccl_ranks"] = multi_info["rccl_ranks"] if mode == "multi" else world
+            r1.close()
+        if n_gpus == 1:
+            frame_np = (fa.cpu().numpy(), fo.cpu().numpy())
+    # Side lines (single GPU): the same frame with the other random stream and with the LBVH walk
+    # (BASELINE config 3 names LBVH traversal), and BASELINE config 2 as specified.
+    if mode == "single" and not args.no_side_lines and not args.profile:
         def time_frames(o, w, h, s, n):
             a = torch.zeros((h, w, 4), dtype=torch.float32, device=dev)
             b = torch.zeros((h, w, 4), dtype=torch.uint8, device=dev)
@@ -441,6 +557,28 @@ def main() -> int:
                 "kernel_ms": round(oms, 3), "rng": "stream" if other == abi.RT_RNG_PIXEL_STREAM else "hash",
                 "psnr_vs_headline_frame_db": "inf" if mse == 0 else round(10 * np.log10(255 ** 2 / mse), 2),
                 "note": "same frame, other random stream (two independent Monte-Carlo estimates of one picture)"}
+            if form.startswith("grid"):
+                lo = rtvk.make_options(accel=accel, rng_mode=rng_mode)
+                lo.reserved[1] = 8   # octant LBVH copies in LDS
+                lms, la, lb = time_frames(lo, W, H, spp, 1)
+                linfo = renderer.launch_info()
+                lcnt = rtvk.make_options(accel=accel, rng_mode=rng_mode, count_tests=True)
+                lcnt.reserved[1] = 8
+                a_ = torch.zeros((H, W, 4), dtype=torch.float32, device=dev)
+                b_ = torch.zeros((H, W, 4), dtype=torch.uint8, device=dev)
+                renderer.render_device(cnt_rci, a_, b_, options=lcnt)
+                torch.cuda.synchronize()
+                lcs = renderer.stats()
+                lroof = roofline_block(lcs, scale, linfo["form"], lms, lms, 1, result["roofline"]["lib_sha256"], {},
+                                       "one frame timed alone (HIP events)")
+                result["lbvh_walk"] = {
+                    "workload": f"BASELINE config {args.config} frame, LBVH walk (octant node copies in LDS)",
+                    "accel": linfo["form"], "value": round(samples_per_step / (lms * 1e-3) / 1e6, 2),
+                    "unit": "Msamples/s", "kernel_ms": round(lms, 3),
+                    "image_bit_equal_to_headline": bool(np.array_equal(la.cpu().numpy(), frame_np[0])
+                                                        and np.array_equal(lb.cpu().numpy(), frame_np[1])),
+                    "roofline": {k: lroof[k] for k in ("bound", "achieved", "peak", "unit", "frac", "kernel",
+                                                       "box_tests", "sphere_tests", "flop_per_launch")}}
         if grid == 11:
             bw_, bh_, bspp = CONFIGS[2][:3]
             bms, _, _ = time_frames(rtvk.make_options(accel=abi.RT_ACCEL_BRUTE, rng_mode=rng_mode), bw_, bh_, bspp, 2)
@@ -453,13 +591,16 @@ def main() -> int:
                 "roofline": {"bound": "valu-fp32", "achieved": round(bflops / (bms * 1e-3) / 1e12, 3),
                              "peak": VALU_FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                              "frac": round(bflops / (bms * 1e-3) / 1e12 / VALU_FP32_PEAK_TFLOPS, 4)}}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.profile:
+    if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline and not args.profile:
         result["cpu_baseline"] = cpu_baseline(W, H, spp, grid, rng_mode, frame_np[0], frame_np[1])
     if rank == 0:
         print(json.dumps(result), flush=True)
-    for sl in slots:
-        sl.renderer.close()
-    if world > 1:
+    if mode == "multi":
+        mr.close()
+    else:
+        for sl in slots:
+            sl.renderer.close()
+    if mode == "per-process":
         dist.destroy_process_group()
     return 0
 

@@ -79,7 +79,15 @@ typedef enum rt_rng_mode {
                                   lowbias32(pixel_seed + 0x9E3779B9 * s) and per-sample colours are summed in
                                   8.24 fixed point, so the library splits a pixel's samples into chunks run
                                   by any lanes in any order with bit-identical results;
-                                  samplesPerRenderCall <= 2^19                                                */
+                                  samplesPerRenderCall <= 2^19. The fixed point holds a sample colour
+                                  channel in [0, 1] (a NaN channel counts 0): every sample colour is a
+                                  product of sphere colours and the sky (0.7, 0.8, 1), so it lies in
+                                  [0, 1] exactly when every colour a sphere can return does (colors[0],
+                                  and colors[1] of checkered spheres). rt_render_device refuses a scene
+                                  with a colour channel outside [0, 1] in this mode
+                                  (RT_ERR_INVALID_ARGUMENT) instead of clipping it; the reference sums
+                                  unclamped (shader.rgen:55-59): render such scenes with
+                                  RT_RNG_PIXEL_STREAM.                                                      */
 } rt_rng_mode;
 
 /* Closest-hit search structure (the reference uses the driver's BVH, src/vulkan.h:395-554). */
@@ -202,6 +210,12 @@ int rt_multi_render(rt_multi* m, const RenderCallInfo* rci, const rt_options* op
                     float* accum_rgba32f, uint8_t* out_rgba8, void* stream);
 /* Sum over the devices of the last frame's statistics (synchronises). */
 int rt_multi_stats(rt_multi* m, rt_stats* out);
+/* {devices, ranks of the RCCL communicator (ncclCommCount), rows per strip, devices that rendered
+ * rows in the last frame}. */
+int rt_multi_info(const rt_multi* m, uint32_t* out4);
+/* Trace-kernel duration (ms, HIP events on the launch stream) of the last frame on each device
+ * that rendered rows, in device order; *count = devices written (synchronises). */
+int rt_multi_kernel_times(rt_multi* m, float* out_ms, uint32_t capacity, uint32_t* count);
 
 /* ---- host-pointer convenience ------------------------------------------------------ */
 /*
@@ -227,6 +241,14 @@ int rt_debug_math(int device, int op, const float* in_pairs, float* out, uint32_
  * binary32 inputs (mismatches3[0], [1]; NaN == NaN), and the camera's float(double(x) * (1 /
  * double(b))) vs x / b for every binary32 x in [0, 65536) and eleven image sizes b (mismatches3[2]). */
 int rt_debug_exact_exhaustive(int device, uint64_t* mismatches3);
+/* Durations (ms) of the trace kernel of ctx's most recent launches (at most 64 are kept), oldest
+ * first, from HIP events recorded on the launch stream around the kernel itself (not the resolve):
+ * a caller times K launches inside its own timed region and reads them afterwards. *count =
+ * min(capacity, launches kept). Synchronises on those events. */
+int rt_debug_kernel_times(rt_context* ctx, float* out_ms, uint32_t capacity, uint32_t* count);
+/* Build provenance of this library: "sources_sha256=<16 hex of the sources it was compiled
+ * from>;arch=gfx950;flags=...". Static string. */
+const char* rt_build_info(void);
 /* Diagnostic: of ctx's last launch, {sample chunks per pixel, staged kernel form of the scene
  * (rt_internal.h ACCEL_*), its LDS bytes, CU count}. */
 int rt_debug_launch_info(rt_context* ctx, uint32_t* out4);
@@ -255,9 +277,11 @@ int rt_debug_tile_cost(rt_context* ctx, uint32_t* out, uint64_t capacity, uint64
 int rt_debug_scene(rt_context* ctx, uint32_t what, void* out, uint64_t capacity, uint64_t* bytes);
 
 /* src/ray_trace.h:9-15 — identical symbol and parameter list. Renders the canonical scene once
- * (t = 0) on min(gpu_count, visible) GPUs through rt_multi (8-row strips, RCCL gather; the
- * reference's per-pixel LCG stream with global seeds, so the image does not depend on gpu_count),
- * prints the frame time, stores `render.ppm` when storeRenderResult, and returns. */
+ * (t = 0) on min(gpu_count, visible) GPUs through rt_multi (8-row strips, RCCL gather, global
+ * seeds, so the image does not depend on gpu_count), prints the frame time, stores `render.ppm`
+ * when storeRenderResult, and returns. Random stream: the reference's per-pixel LCG stream, or
+ * RT_RNG_SAMPLE_HASH when the environment holds RT_RNG=hash (the signature has no parameter for
+ * it; any other RT_RNG value than "stream" / "hash" is reported and nothing renders). */
 void ray_trace(uint32_t samples, bool storeRenderResult, uint32_t width, uint32_t height,
                uint32_t gpu_count);
 

@@ -101,9 +101,16 @@ def render_call_info(spp: int, width: int, height: int, offset=(0, 0), number: i
     return r
 
 
-def options(max_depth=50, seed_mode=0, rng_mode=0, accel=0, accumulate=0, sample_base=0) -> np.ndarray:
+# Arithmetic forms of the oracle (rt_oracle.cpp LIT_*): the shipped contract (what the kernels
+# implement), shader.rint read as written, and every dot / normalize read as written too.
+LIT_CONTRACT, LIT_RINT, LIT_ALL = 0, 1, 2
+
+
+def options(max_depth=50, seed_mode=0, rng_mode=0, accel=0, accumulate=0, sample_base=0,
+            lit=LIT_CONTRACT) -> np.ndarray:
     o = np.zeros(8, np.uint32)
     o[:6] = [max_depth, seed_mode, rng_mode, accel, accumulate, sample_base]
+    o[7] = lit
     return o
 
 

@@ -93,9 +93,25 @@ inline V3 sub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
 inline V3 mul(V3 a, V3 b) { return v3(a.x * b.x, a.y * b.y, a.z * b.z); }
 inline V3 scale(float s, V3 a) { return v3(s * a.x, s * a.y, s * a.z); }
 inline V3 neg(V3 a) { return v3(-a.x, -a.y, -a.z); }
-inline float dot(V3 a, V3 b) { return std::fma(a.z, b.z, std::fma(a.y, b.y, a.x * b.x)); }
+// Arithmetic forms (orc_render's opt->reserved[1]): L = LIT_CONTRACT is the shipped
+// contract that the HIP kernels implement; LIT_RINT reads shader.rint:33-55 as
+// written (D = b*b - a*c unfused, roots divided by a, hit point o + t*d unfused); LIT_ALL also
+// takes every dot() unfused left to right and normalize(v) = v / length(v) (GLSL 4.60 §8.5)
+// everywhere. The two literal forms exist to MEASURE the contract's distance from the GLSL as
+// written; the kernels never implement them.
+enum { LIT_CONTRACT = 0, LIT_RINT = 1, LIT_ALL = 2 };
+template <int L = LIT_CONTRACT>
+inline float dot(V3 a, V3 b) {
+    if (L == LIT_ALL) {
+        float xx = a.x * b.x, yy = a.y * b.y, zz = a.z * b.z;
+        return (xx + yy) + zz;
+    }
+    return std::fma(a.z, b.z, std::fma(a.y, b.y, a.x * b.x));
+}
+template <int L = LIT_CONTRACT>
 inline V3 normalize(V3 v) {
-    float len = std::sqrt(dot(v, v));
+    float len = std::sqrt(dot<L>(v, v));
+    if (L == LIT_ALL) return v3(v.x / len, v.y / len, v.z / len);
     float inv = 1.0f / len;
     return v3(v.x * inv, v.y * inv, v.z * inv);
 }
@@ -104,13 +120,15 @@ inline V3 cross(V3 a, V3 b) {
     return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
 // GLSL reflect(I, N) = I - 2.0 * dot(N, I) * N
+template <int L = LIT_CONTRACT>
 inline V3 reflect(V3 i, V3 n) {
-    float k = 2.0f * dot(n, i);
+    float k = 2.0f * dot<L>(n, i);
     return sub(i, scale(k, n));
 }
 // GLSL refract(I, N, eta)
+template <int L = LIT_CONTRACT>
 inline V3 refract(V3 i, V3 n, float eta) {
-    float d = dot(n, i);
+    float d = dot<L>(n, i);
     float k = 1.0f - eta * eta * (1.0f - d * d);
     if (k < 0.0f) return v3(0.0f, 0.0f, 0.0f);
     float s = eta * d + std::sqrt(k);
@@ -125,7 +143,8 @@ inline V3 random_vector(uint32_t& seed, float mn, float mx) {
     return v3(x, y, z);
 }
 // random.glsl:32-34
-inline V3 random_unit_vector(uint32_t& seed) { return normalize(random_vector(seed, -1.0f, 1.0f)); }
+template <int L = LIT_CONTRACT>
+inline V3 random_unit_vector(uint32_t& seed) { return normalize<L>(random_vector(seed, -1.0f, 1.0f)); }
 
 // ------------------------------------------------------------------------------------
 // sin for the checker texture (shader.rchit:59). Deterministic: only +,-,*,fma, rint.
@@ -192,6 +211,7 @@ struct Viewport {
     float aperture;
 };
 
+template <int L = LIT_CONTRACT>
 Viewport make_viewport(const RenderCallInfo& rci) {
     // shader.rgen:29 Camera(25.0f, 0.0f, 10.0f, ...), up = (0,1,0); lookFrom/lookAt from rci.
     const float fov = 25.0f, aperture = 0.0f, focus = 10.0f;
@@ -205,9 +225,9 @@ Viewport make_viewport(const RenderCallInfo& rci) {
     float th = float(std::tan(double(half)));  // tan(), rounded once to float
     float vh = th * 2.0f;
     float vw = aspect * vh;
-    V3 fwd = normalize(sub(look_at, look_from));
-    V3 right = normalize(cross(up, fwd));
-    V3 cup = normalize(cross(fwd, right));
+    V3 fwd = normalize<L>(sub(look_at, look_from));
+    V3 right = normalize<L>(cross(up, fwd));
+    V3 cup = normalize<L>(cross(fwd, right));
     Viewport vp;
     // viewportWidth * cameraRight * focusDistance, evaluated left to right
     vp.horizontal = v3(vw * right.x * focus, vw * right.y * focus, vw * right.z * focus);
@@ -248,8 +268,9 @@ inline bool aabb_hit(const rt_vec4& g, V3 o, V3 inv) {
 // overlaps its AABB and the quadratic reports t (t1 if t1 >= tmin, else t2) inside
 // [tmin, tmax]; the closest candidate wins, the lowest index on ties.
 // A report at exactly tMax is accepted (reportIntersectionEXT), hence '<' against succ(T_MAX).
+template <int L>
 Hit closest_hit(const Sphere* sph, uint32_t n, V3 o, V3 d, uint64_t* tests) {
-    float a = dot(d, d);
+    float a = dot<L>(d, d);
     float ia = 1.0f / a;
     V3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     float best = std::nextafter(T_MAX, std::numeric_limits<float>::infinity());
@@ -257,14 +278,20 @@ Hit closest_hit(const Sphere* sph, uint32_t n, V3 o, V3 d, uint64_t* tests) {
     for (uint32_t i = 0; i < n; i++) {
         const rt_vec4& g = sph[i].geometry;
         V3 oc = sub(o, v3(g.x, g.y, g.z));
-        float b = dot(oc, d);
+        float b = dot<L>(oc, d);
         float rr = g.w * g.w;
-        float c = dot(oc, oc) - rr;
-        float D = std::fma(b, b, -(a * c));
+        float c = dot<L>(oc, oc) - rr;
+        float D;
+        if (L == LIT_CONTRACT) {
+            D = std::fma(b, b, -(a * c));
+        } else {   // shader.rint:50 as written
+            float bb = b * b, ac = a * c;
+            D = bb - ac;
+        }
         if (D >= 0.0f) {
             float sq = std::sqrt(D);
-            float t1 = (-b - sq) * ia;
-            float t2 = (-b + sq) * ia;
+            float t1 = L == LIT_CONTRACT ? (-b - sq) * ia : (-b - sq) / a;   // shader.rint:55-56 as written: / a
+            float t2 = L == LIT_CONTRACT ? (-b + sq) * ia : (-b + sq) / a;
             float t = (t1 >= T_MIN) ? t1 : t2;   // rint:32-39 (t1 > tMax implies t2 > tMax)
             if (t >= T_MIN && t < best && aabb_hit(g, o, inv)) { best = t; bi = int(i); }
         }
@@ -296,25 +323,26 @@ inline bool near_zero(V3 v) {  // rchit:120-123
 }
 
 // shader.rchit:38-49 + 66-133
+template <int L>
 void closest_hit_shader(const Sphere& s, V3 p, V3 dir, uint32_t& seed, Payload& pl) {
     V3 center = v3(s.geometry.x, s.geometry.y, s.geometry.z);
-    V3 outward = normalize(sub(p, center));
-    bool front = dot(dir, outward) < 0.0f;
+    V3 outward = normalize<L>(sub(p, center));
+    bool front = dot<L>(dir, outward) < 0.0f;
     V3 n = front ? outward : neg(outward);
     pl.attenuation = texture_color(s, p);
     V3 sd;
     if (s.materialType == RT_DIFFUSE) {                      // rchit:68-76
-        sd = add(n, random_unit_vector(seed));
+        sd = add(n, random_unit_vector<L>(seed));
         if (near_zero(sd)) sd = n;
     } else if (s.materialType == RT_METAL) {                 // rchit:78-89
-        V3 refl = reflect(dir, n);
-        V3 fuzz = scale(s.materialSpecificAttribute, random_unit_vector(seed));
-        V3 sc = normalize(add(refl, fuzz));
-        sd = (dot(sc, n) > 0.0f) ? sc : v3(0.0f, 0.0f, 0.0f);
+        V3 refl = reflect<L>(dir, n);
+        V3 fuzz = scale(s.materialSpecificAttribute, random_unit_vector<L>(seed));
+        V3 sc = normalize<L>(add(refl, fuzz));
+        sd = (dot<L>(sc, n) > 0.0f) ? sc : v3(0.0f, 0.0f, 0.0f);
     } else if (s.materialType == RT_REFRACTIVE) {            // rchit:91-100, 125-133
         float attr = s.materialSpecificAttribute;
         float eta = front ? (1.0f / attr) : attr;
-        float cos_t = dot(neg(dir), n);
+        float cos_t = dot<L>(neg(dir), n);
         bool can_refract = eta * std::sqrt(1.0f - cos_t * cos_t) <= 1.0f;
         bool refracts = false;
         if (can_refract) {  // && short-circuit: the draw happens only here
@@ -323,7 +351,7 @@ void closest_hit_shader(const Sphere& s, V3 p, V3 dir, uint32_t& seed, Payload& 
             float refl = r + (1.0f - r) * pow5_glsl(1.0f - cos_t);
             refracts = refl < random_float(seed);
         }
-        sd = refracts ? refract(dir, n, eta) : reflect(dir, n);
+        sd = refracts ? refract<L>(dir, n, eta) : reflect<L>(dir, n);
     } else {
         sd = v3(0.0f, 0.0f, 0.0f);
     }
@@ -335,17 +363,20 @@ void closest_hit_shader(const Sphere& s, V3 p, V3 dir, uint32_t& seed, Payload& 
 struct Counters { uint64_t segments = 0, samples = 0, sphere_tests = 0; };
 
 // shader.rgen:70-89 calculateRayColor
+template <int L>
 V3 ray_color(const Sphere* sph, uint32_t n, V3 o, V3 d, uint32_t& seed, uint32_t max_depth,
              Counters& cnt) {
     V3 reflected = v3(1.0f, 1.0f, 1.0f);
     V3 light = v3(0.0f, 0.0f, 0.0f);
     for (uint32_t depth = 0; depth < max_depth; depth++) {
-        Hit h = closest_hit(sph, n, o, d, &cnt.sphere_tests);
+        Hit h = closest_hit<L>(sph, n, o, d, &cnt.sphere_tests);
         cnt.segments++;
         Payload pl;
         if (h.idx >= 0) {
-            V3 p = v3(std::fma(h.t, d.x, o.x), std::fma(h.t, d.y, o.y), std::fma(h.t, d.z, o.z));
-            closest_hit_shader(sph[h.idx], p, d, seed, pl);
+            V3 p = L == LIT_CONTRACT
+                       ? v3(std::fma(h.t, d.x, o.x), std::fma(h.t, d.y, o.y), std::fma(h.t, d.z, o.z))
+                       : add(o, scale(h.t, d));   // shader.rint:33/37 as written
+            closest_hit_shader<L>(sph[h.idx], p, d, seed, pl);
         } else {  // shader.rmiss:13-18
             pl.does_scatter = false;
             pl.attenuation = v3(0.7f, 0.8f, 1.0f);
@@ -353,7 +384,7 @@ V3 ray_color(const Sphere* sph, uint32_t n, V3 o, V3 d, uint32_t& seed, uint32_t
         if (pl.does_scatter) {
             reflected = mul(reflected, pl.attenuation);
             o = pl.point;
-            d = normalize(pl.scatter_dir);
+            d = normalize<L>(pl.scatter_dir);
         } else {
             light = pl.attenuation;
             break;
@@ -381,6 +412,7 @@ struct RenderJob {
 };
 
 // shader.rgen:39-67 main() for one launch-id pixel (lx, ly).
+template <int L>
 void render_pixel(const RenderJob& job, uint32_t lx, uint32_t ly, Counters& cnt) {
     const RenderCallInfo& rci = *job.rci;
     uint32_t gx = rci.offset.x + lx;
@@ -412,16 +444,16 @@ void render_pixel(const RenderJob& job, uint32_t lx, uint32_t ly, Counters& cnt)
         // shader.rgen:107-115 getCameraRay
         float lx_ = random_in_interval(seed, -1.0f, 1.0f);
         float ly_ = random_in_interval(seed, -1.0f, 1.0f);
-        float l2 = std::sqrt(std::fma(ly_, ly_, lx_ * lx_));
+        float l2 = L == LIT_ALL ? std::sqrt(lx_ * lx_ + ly_ * ly_) : std::sqrt(std::fma(ly_, ly_, lx_ * lx_));
         float il = 1.0f / l2;
         float half_ap = vp.aperture / 2.0f;
         float rx = half_ap * (lx_ * il), ry = half_ap * (ly_ * il);
         V3 off = add(scale(rx, vp.cam_right), scale(ry, vp.cam_up));
         V3 from = add(vp.look_from, off);
         V3 to = sub(add(vp.upper_left, scale(ux, vp.horizontal)), scale(uy, vp.vertical));
-        V3 dir = normalize(sub(to, from));
+        V3 dir = normalize<L>(sub(to, from));
         cnt.samples++;
-        V3 c = ray_color(job.sph, job.n, from, dir, seed, max_depth, cnt);
+        V3 c = ray_color<L>(job.sph, job.n, from, dir, seed, max_depth, cnt);
         if (hash) {
             q[0] += sample_fixed(c.x);
             q[1] += sample_fixed(c.y);
@@ -496,7 +528,7 @@ uint32_t orc_sample_seed_hash(uint32_t pixel_seed, uint32_t s) { return sample_s
 uint64_t orc_sample_fixed(float c) { return sample_fixed(c); }
 
 void orc_viewport(const RenderCallInfo* rci, float* out18) {
-    Viewport vp = make_viewport(*rci);
+    Viewport vp = make_viewport<LIT_CONTRACT>(*rci);
     const V3* vs[6] = {&vp.look_from, &vp.horizontal, &vp.vertical, &vp.upper_left, &vp.cam_up,
                        &vp.cam_right};
     for (int i = 0; i < 6; i++) { out18[3 * i] = vs[i]->x; out18[3 * i + 1] = vs[i]->y; out18[3 * i + 2] = vs[i]->z; }
@@ -558,7 +590,9 @@ int orc_render(const Sphere* spheres, uint32_t n, const RenderCallInfo* rci, con
     job.band_w = band_w; job.band_h = band_h;
     std::memset(&job.opt, 0, sizeof(job.opt));
     if (opt) job.opt = *opt;
-    job.vp = make_viewport(*rci);
+    const uint32_t lit = job.opt.reserved[1];   // arithmetic form (LIT_*), oracle only
+    if (lit > LIT_ALL) return -1;
+    job.vp = lit == LIT_ALL ? make_viewport<LIT_ALL>(*rci) : make_viewport<LIT_CONTRACT>(*rci);
     job.accum = accum; job.out = out;
     if (!job.opt.accumulate) std::memset(accum, 0, size_t(band_w) * band_h * 4 * sizeof(float));
     unsigned nt = threads > 0 ? unsigned(threads) : std::max(1u, std::thread::hardware_concurrency());
@@ -568,7 +602,11 @@ int orc_render(const Sphere* spheres, uint32_t n, const RenderCallInfo* rci, con
         for (;;) {
             uint32_t y = next_row.fetch_add(1);
             if (y >= band_h) break;
-            for (uint32_t x = 0; x < band_w; x++) render_pixel(job, x, y, cnts[tid]);
+            for (uint32_t x = 0; x < band_w; x++) {
+                if (lit == LIT_CONTRACT) render_pixel<LIT_CONTRACT>(job, x, y, cnts[tid]);
+                else if (lit == LIT_RINT) render_pixel<LIT_RINT>(job, x, y, cnts[tid]);
+                else render_pixel<LIT_ALL>(job, x, y, cnts[tid]);
+            }
         }
     };
     std::vector<std::thread> pool;

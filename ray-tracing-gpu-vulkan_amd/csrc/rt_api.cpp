@@ -89,6 +89,13 @@ struct rt_context {
     unsigned long long* fixed = nullptr;
     uint64_t fixed_cap = 0;                      // texels
     uint32_t last_chunks = 1;
+    // every colour the shaders can return lies in [0, 1] (RT_RNG_SAMPLE_HASH's fixed point needs it)
+    bool colours_unit = true;
+    // HIP events bracketing the trace kernel of the last kKernelEvents launches (ring; timing
+    // inside a caller's timed region without a host sync per launch, rt_debug_kernel_times)
+    static constexpr uint32_t kKernelEvents = 64;
+    hipEvent_t kev[kKernelEvents][2] = {};
+    uint64_t kev_count = 0;                      // launches recorded so far
 };
 
 namespace {
@@ -435,6 +442,9 @@ int rt_context_destroy(rt_context* ctx) {
         if (ctx->stage_ev[k]) (void)hipEventDestroy(ctx->stage_ev[k]);
     }
     if (ctx->ev_last) (void)hipEventDestroy(ctx->ev_last);
+    for (auto& pr : ctx->kev)
+        for (hipEvent_t e : pr)
+            if (e) (void)hipEventDestroy(e);
     if (ctx->d_spheres) (void)hipFree(ctx->d_spheres);
     if (ctx->fixed) (void)hipFree(ctx->fixed);
     if (ctx->counters) (void)hipFree(ctx->counters);
@@ -461,8 +471,10 @@ int set_scene_host(rt_context* ctx, const Sphere* spheres, uint32_t count, hipSt
         std::vector<rt::GeomRec> geom(count);
         std::vector<float> radius(count);
         std::vector<rt::MatRec> mat(count);
+        ctx->colours_unit = true;
         for (uint32_t i = 0; i < count; i++) {
             const Sphere& s = spheres[i];
+            if (!rt::colours_in_unit(s)) ctx->colours_unit = false;
             const float r = s.geometry.w;
             geom[i] = rt::GeomRec{s.geometry.x, s.geometry.y, s.geometry.z, r * r};
             radius[i] = r;
@@ -563,6 +575,7 @@ int set_scene_gpu(rt_context* ctx, const Sphere* d_sph, uint32_t count, hipStrea
                     std::string("device LBVH build: ") + hipGetErrorString(e));
     }
     d.n_spheres = count;
+    ctx->colours_unit = sm.colour_out_of_range == 0u;
     d.n_big = sm.n_big;
     d.n_nodes = sm.n_nodes;
     d.n_leaf = sm.n_leaf_slots;
@@ -733,6 +746,13 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     const uint32_t spp = rci->samplesPerRenderCall;
     if (mode == rt::MODE_HASH && spp > rt::kHashMaxSpp)
         return fail(RT_ERR_INVALID_ARGUMENT, "RT_RNG_SAMPLE_HASH: samplesPerRenderCall above 2^19");
+    // The fixed-point sums of RT_RNG_SAMPLE_HASH hold per-sample colours in [0, 1]: the reference
+    // sums unclamped (shader.rgen:55-59), so a scene whose colours can leave [0, 1] is refused
+    // rather than silently clipped (use RT_RNG_PIXEL_STREAM for it).
+    if (mode == rt::MODE_HASH && !ctx->colours_unit)
+        return fail(RT_ERR_INVALID_ARGUMENT,
+                    "RT_RNG_SAMPLE_HASH needs every sphere colour channel in [0, 1] (colors[0], and colors[1] of "
+                    "checkered spheres); this scene has one outside: render it with RT_RNG_PIXEL_STREAM");
     const uint64_t tiles_x = (band_width + 7u) / 8u, tiles_y = (band_height + 7u) / 8u;
     const uint64_t n_tiles = tiles_x * tiles_y;
     // reserved[1] (internal, A/B only): LBVH walk form, 0 = automatic (octant node copies in LDS
@@ -962,7 +982,13 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
         RT_HIP(rt::build_treelet(d.nodes, d.n_nodes, d.treelet, d.treelet_count, st));
         ctx->treelet_stale = false;
     }
+    hipEvent_t* kev = ctx->kev[ctx->kev_count % rt_context::kKernelEvents];
+    for (int k = 0; k < 2; k++)
+        if (!kev[k]) RT_HIP(hipEventCreate(&kev[k]));
+    RT_HIP(hipEventRecord(kev[0], st));
     RT_HIP(rt::launch_trace(P, accel, count, mode, grid, lds, st));
+    RT_HIP(hipEventRecord(kev[1], st));
+    ctx->kev_count++;
     if (mode == rt::MODE_HASH)
         RT_HIP(rt::launch_resolve_fixed(ctx->fixed, texels, P.accumulate, spp, accum, out, st));
     if (P.tile_cost) {
@@ -1066,6 +1092,24 @@ int rt_debug_walk_hist(rt_context* ctx, uint64_t* out128) {
     RT_HIP(hipMemcpy(&c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
     std::memcpy(out128, c.walk_hist, sizeof(c.walk_hist));
     return RT_OK;
+}
+
+int rt_debug_kernel_times(rt_context* ctx, float* out_ms, uint32_t capacity, uint32_t* count) {
+    if (!ctx || !count || (!out_ms && capacity)) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    DeviceGuard g(ctx->device);
+    const uint64_t have = std::min<uint64_t>(ctx->kev_count, rt_context::kKernelEvents);
+    const uint32_t n = uint32_t(std::min<uint64_t>(have, capacity));
+    for (uint32_t i = 0; i < n; i++) {   // the n most recent launches, oldest first
+        hipEvent_t* e = ctx->kev[(ctx->kev_count - n + i) % rt_context::kKernelEvents];
+        RT_HIP(hipEventSynchronize(e[1]));
+        RT_HIP(hipEventElapsedTime(&out_ms[i], e[0], e[1]));
+    }
+    *count = n;
+    return RT_OK;
+}
+
+const char* rt_build_info(void) {
+    return "sources_sha256=" RT_SOURCES_SHA256 ";arch=gfx950;flags=-O3 -ffp-contract=off -fno-slp-vectorize";
 }
 
 int rt_debug_launch_info(rt_context* ctx, uint32_t* out4) {

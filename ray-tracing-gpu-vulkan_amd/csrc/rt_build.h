@@ -17,6 +17,7 @@ struct BuildSummary {
     uint32_t rmax_o, R_o;            // order-preserving bit patterns of small_rmax and R
     uint32_t rmin_o;                 // ... and of the smallest small radius
     uint32_t cmin_o[3], cmax_o[3];   // centroid bounds of the small spheres (Morton frame)
+    uint32_t colour_out_of_range;    // != 0: some sphere colour leaves [0, 1] (colours_in_unit)
 };
 float summary_float(uint32_t ordered);
 

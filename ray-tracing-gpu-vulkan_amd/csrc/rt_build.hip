@@ -67,6 +67,7 @@ __global__ void k_init(BuildSummary* S, bool refit) {
     }
     S->rmax_o = f2o(0.0f);
     S->rmin_o = f2o(INFINITY);
+    S->colour_out_of_range = 0u;
     S->R_o = f2o(0.0f);
 }
 
@@ -84,6 +85,7 @@ __global__ void __launch_bounds__(kBlock) k_prep(const Sphere* __restrict__ sph,
         mat[i] = make_mat(s.colors[0].x, s.colors[0].y, s.colors[0].z, s.materialSpecificAttribute,
                           s.colors[1].x, s.colors[1].y, s.colors[1].z, s.materialType, s.textureType);
         if (rkeys) { rkeys[i] = r; ids[i] = i; }
+        if (!colours_in_unit(s)) atomicOr(&S->colour_out_of_range, 1u);
         Ro = f2o(__builtin_sqrtf(x * x + y * y + z * z) + __builtin_fabsf(r));
     } else if (i < n_geom) {   // brute-force pad record: never hit (rt_api.cpp)
         geom[i] = GeomRec{0.0f, 1e19f, 0.0f, -1e38f};

@@ -4,6 +4,8 @@
 
 #include <stdint.h>
 
+#include "../../include/rt_abi.h"
+
 namespace rt {
 
 // Per-sphere geometry record read by the closest-hit search (shader.rint:28-30):
@@ -23,6 +25,19 @@ struct alignas(16) MatRec {
 // constants of shader.rchit:94 and :131 (eta = 1/ior on a front face, ior on a back face;
 // r0 = ((1 - eta) / (1 + eta))^2, Q7), computed with the kernel's own binary32 operations.
 constexpr uint32_t kMatDielConst = 1u << 16;
+
+// Every colour a sphere can return as attenuation (shader.rchit:53-64: colors[0], and colors[1]
+// of a checkered texture) lies in [0, 1] (NaN fails): then every sample colour does too, which
+// RT_RNG_SAMPLE_HASH's 8.24 fixed-point sums require (rt_render_device refuses other scenes).
+#if defined(__HIPCC__)
+__host__ __device__
+#endif
+inline bool colours_in_unit(const Sphere& s) {
+    auto in = [](float v) { return v >= 0.0f && v <= 1.0f; };
+    bool ok = in(s.colors[0].x) && in(s.colors[0].y) && in(s.colors[0].z);
+    if (s.textureType == 1u) ok = ok && in(s.colors[1].x) && in(s.colors[1].y) && in(s.colors[1].z);
+    return ok;
+}
 
 // Fills a material record (host and device builds alike).
 #if defined(__HIPCC__)

@@ -4,12 +4,15 @@
 // but a flag missing its value is an error here (the reference reads past argv, :33-46).
 //
 //   --help  --store  --samples <spp>  --width <w>  --height <h>  --gpus <n>
-//   --frames <n> [--animate] [--rng stream|hash]: the reference's benchmark frame loop
-//   (src/ray_trace.cpp:567-748): n frames back to back, each rebuilding the scene
-//   (generateRandomScene(t), t = seconds since start with --animate, else 0) and rendering the
-//   image tiled over the GPUs with an RCCL gather to GPU 0 (rt_multi), two frames in flight (the
-//   reference keeps one per swapchain image); prints duration_per_frame like the reference
-//   (:740-744). --rng hash selects the counter-based stream (RT_RNG_SAMPLE_HASH).
+//   --frames <n> [--animate]: the reference's benchmark frame loop (src/ray_trace.cpp:567-748):
+//   n frames back to back, each rebuilding the scene (generateRandomScene(t), t = seconds since
+//   start with --animate, else 0) and rendering the image tiled over the GPUs with an RCCL gather
+//   to GPU 0 (rt_multi); prints duration_per_frame like the reference (:740-744). Frames are
+//   queued asynchronously on ONE rt_multi (one communicator, its streams keep the gathers of
+//   successive frames in one order on every device), so the host builds frame k+1's scene while
+//   frame k renders.
+//   --rng stream|hash: the reference's per-pixel LCG stream (default) or the counter-based
+//   RT_RNG_SAMPLE_HASH stream, for --frames and for the single ray_trace() frame alike.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -17,6 +20,7 @@
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -47,40 +51,34 @@ static bool parse_u32(const char* s, uint32_t& out) {
 
 namespace {
 
-struct Slot {   // one frame in flight: a multi-device renderer and its device-0 frame buffers
+int run_frames(uint32_t samples, uint32_t width, uint32_t height, uint32_t gpu_count, uint32_t frames,
+               bool animate, bool store, uint32_t rng_mode) {
+    // One multi-device renderer: two rt_multi over the same devices would be two RCCL
+    // communicators whose grouped gathers could run in different orders on different devices.
     rt_multi* m = nullptr;
     hipStream_t stream = nullptr;   // device 0
     float* accum = nullptr;
     uint8_t* rgba8 = nullptr;
-};
-
-int run_frames(uint32_t samples, uint32_t width, uint32_t height, uint32_t gpu_count, uint32_t frames,
-               bool animate, bool store, uint32_t rng_mode) {
-    constexpr int kInFlight = 2;
-    std::vector<Slot> slots(kInFlight);
     uint32_t n = 1;
     CLI_HIP(hipSetDevice(0));
-    for (Slot& s : slots) {
-        CLI_RT(rt_multi_create(gpu_count, &s.m));
-        CLI_RT(rt_multi_device_count(s.m, &n));
-        CLI_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-        CLI_HIP(hipMalloc(&s.accum, size_t(width) * height * 16));
-        CLI_HIP(hipMalloc(&s.rgba8, size_t(width) * height * 4));
-    }
+    CLI_RT(rt_multi_create(gpu_count, &m));
+    CLI_RT(rt_multi_device_count(m, &n));
+    CLI_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    CLI_HIP(hipMalloc(&accum, size_t(width) * height * 16));
+    CLI_HIP(hipMalloc(&rgba8, size_t(width) * height * 4));
     rt_options opt;
     std::memset(&opt, 0, sizeof(opt));
     opt.rng_mode = rng_mode;
     std::vector<Sphere> scene(488);
     uint32_t cnt = 0;
     const auto t_start = std::chrono::steady_clock::now();
-    auto frame = [&](uint32_t f) -> int {
+    auto frame = [&]() -> int {
         const float t = animate ? std::chrono::duration<float>(std::chrono::steady_clock::now() - t_start).count() : 0.0f;
         CLI_RT(rt_generate_scene(t, 11, scene.data(), uint32_t(scene.size()), &cnt));   // scene.h:79
-        Slot& s = slots[f % kInFlight];
         RenderCallInfo rci;
         CLI_RT(rt_canonical_render_call_info(samples, width, height, &rci));
-        CLI_RT(rt_multi_set_scene(s.m, scene.data(), cnt));
-        CLI_RT(rt_multi_render(s.m, &rci, &opt, s.accum, s.rgba8, s.stream));
+        CLI_RT(rt_multi_set_scene(m, scene.data(), cnt));
+        CLI_RT(rt_multi_render(m, &rci, &opt, accum, rgba8, stream));
         return 0;
     };
     auto sync_all = [&]() -> int {
@@ -91,8 +89,7 @@ int run_frames(uint32_t samples, uint32_t width, uint32_t height, uint32_t gpu_c
         CLI_HIP(hipSetDevice(0));
         return 0;
     };
-    for (uint32_t f = 0; f < kInFlight; f++)   // warm-up: every context has its LPT order
-        if (int rc = frame(f)) return rc;
+    if (int rc = frame()) return rc;   // warm-up: every context has its LPT order
     if (int rc = sync_all()) return rc;
     // Report about once a second, like the reference's ~4 s benchmark windows (:740-748).
     uint32_t done = 0;
@@ -100,7 +97,7 @@ int run_frames(uint32_t samples, uint32_t width, uint32_t height, uint32_t gpu_c
         const auto b = std::chrono::steady_clock::now();
         uint32_t k = 0;
         for (;;) {
-            if (int rc = frame(kInFlight + done + k)) return rc;
+            if (int rc = frame()) return rc;
             ++k;
             if (done + k >= frames) break;
             if (std::chrono::steady_clock::now() - b > std::chrono::milliseconds(1000)) break;
@@ -113,16 +110,13 @@ int run_frames(uint32_t samples, uint32_t width, uint32_t height, uint32_t gpu_c
     }
     if (store) {   // the last frame
         std::vector<uint8_t> img(size_t(width) * height * 4);
-        const uint32_t last = kInFlight + frames - 1;
-        CLI_HIP(hipMemcpy(img.data(), slots[last % kInFlight].rgba8, img.size(), hipMemcpyDeviceToHost));
+        CLI_HIP(hipMemcpy(img.data(), rgba8, img.size(), hipMemcpyDeviceToHost));
         CLI_RT(rt_store_ppm("render.ppm", img.data(), width, height));
     }
-    for (Slot& s : slots) {
-        rt_multi_destroy(s.m);
-        (void)hipStreamDestroy(s.stream);
-        (void)hipFree(s.accum);
-        (void)hipFree(s.rgba8);
-    }
+    rt_multi_destroy(m);
+    (void)hipStreamDestroy(stream);
+    (void)hipFree(accum);
+    (void)hipFree(rgba8);
     return 0;
 }
 
@@ -142,7 +136,7 @@ int main(int argc, const char** argv) {
             std::puts("--gpus <count>                    # Max used GPUs count");
             std::puts("--frames <count>                  # Benchmark loop: render count frames, print duration_per_frame");
             std::puts("--animate                         # With --frames: scene time t = seconds since start");
-            std::puts("--rng <stream|hash>               # With --frames: reference LCG stream or counter-based stream");
+            std::puts("--rng <stream|hash>               # Reference per-pixel LCG stream (default) or counter-based stream");
             return 0;
         } else if (a == "--store") {
             store = true;
@@ -176,6 +170,8 @@ int main(int argc, const char** argv) {
         return 1;
     }
     if (frames > 0) return run_frames(samples, width, height, gpu_count, frames, animate, store, rng_mode);
+    // ray_trace() keeps the reference's signature; its stream is selected through RT_RNG
+    if (rng_mode == RT_RNG_SAMPLE_HASH) setenv("RT_RNG", "hash", 1);
     ray_trace(samples, store, width, height, gpu_count);
     return 0;
 }

@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <memory>
@@ -199,8 +200,14 @@ int rt_multi_create(uint32_t gpu_count, rt_multi** out) {
     *out = nullptr;
     int nd = 0;
     if (int rc = rt::current_device_count(&nd)) return rc;
+    rt_multi* m = nullptr;
     try {
-        std::unique_ptr<rt_multi> m(new rt_multi());
+        m = new rt_multi();
+    } catch (const std::exception& e) {
+        return fail(RT_ERR_OUT_OF_MEMORY, e.what());
+    }
+    // every failure below releases what was created so far (streams, events, comms)
+    auto body = [&]() -> int {
         m->n = std::max(1u, std::min(gpu_count, uint32_t(nd)));
         m->stream.assign(m->n, nullptr);
         m->comm.assign(m->n, nullptr);
@@ -216,11 +223,22 @@ int rt_multi_create(uint32_t gpu_count, rt_multi** out) {
         std::vector<int> devs(m->n);
         for (uint32_t d = 0; d < m->n; d++) devs[d] = int(d);
         RT_NCCL(ncclCommInitAll(m->comm.data(), int(m->n), devs.data()));
-        *out = m.release();
         return RT_OK;
+    };
+    int rc;
+    try {
+        rc = body();
     } catch (const std::exception& e) {
-        return fail(RT_ERR_OUT_OF_MEMORY, e.what());
+        rc = fail(RT_ERR_OUT_OF_MEMORY, e.what());
     }
+    if (rc != RT_OK) {
+        const std::string msg = rt::g_last_error;   // destroy must not overwrite the cause
+        rt_multi_destroy(m);
+        rt::g_last_error = msg;
+        return rc;
+    }
+    *out = m;
+    return RT_OK;
 }
 
 int rt_multi_destroy(rt_multi* m) {
@@ -229,8 +247,8 @@ int rt_multi_destroy(rt_multi* m) {
     for (uint32_t d = 0; d < m->n; d++) {
         DeviceGuard g(static_cast<int>(d));
         (void)hipDeviceSynchronize();
-        if (m->comm[d]) (void)ncclCommDestroy(m->comm[d]);
-        if (m->stream[d]) (void)hipStreamDestroy(m->stream[d]);
+        if (d < m->comm.size() && m->comm[d]) (void)ncclCommDestroy(m->comm[d]);
+        if (d < m->stream.size() && m->stream[d]) (void)hipStreamDestroy(m->stream[d]);
     }
     {
         DeviceGuard g(0);
@@ -284,6 +302,34 @@ int rt_multi_render(rt_multi* m, const RenderCallInfo* rci, const rt_options* op
     DeviceGuard g0(0);
     RT_HIP(hipEventRecord(m->ev_out, m->stream[0]));   // the caller's later work waits for it
     RT_HIP(hipStreamWaitEvent(st, m->ev_out, 0));
+    return RT_OK;
+}
+
+int rt_multi_info(const rt_multi* m, uint32_t* out4) {
+    if (!m || !out4) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    int ranks = 0;
+    RT_NCCL(ncclCommCount(m->comm[0], &ranks));
+    uint32_t launches = 0;
+    for (const Launch& l : m->launches) launches += l.rows.empty() ? 0u : 1u;
+    out4[0] = m->n;
+    out4[1] = uint32_t(ranks);
+    out4[2] = kStrip;
+    out4[3] = launches;
+    return RT_OK;
+}
+
+int rt_multi_kernel_times(rt_multi* m, float* out_ms, uint32_t capacity, uint32_t* count) {
+    if (!m || !count || (!out_ms && capacity)) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    uint32_t k = 0;
+    for (Launch& l : m->launches) {
+        if (l.rows.empty()) continue;
+        if (k >= capacity) break;
+        uint32_t got = 0;
+        if (int rc = rt_debug_kernel_times(l.ctx, out_ms + k, 1, &got)) return rc;
+        if (got == 0) out_ms[k] = 0.0f;
+        k++;
+    }
+    *count = k;
     return RT_OK;
 }
 
@@ -373,7 +419,10 @@ int rt_render(const Sphere* spheres, uint32_t sphere_count, const RenderCallInfo
 }
 
 // src/ray_trace.h:9-15. Headless: one frame of the canonical scene (t = 0) tiled over
-// min(gpu_count, visible) GPUs (rt_multi), the reference's per-pixel LCG stream.
+// min(gpu_count, visible) GPUs (rt_multi). Random stream: the reference's per-pixel LCG stream, or
+// with RT_RNG=hash in the environment the counter-based RT_RNG_SAMPLE_HASH stream, whose samples
+// split into chunks so that every GPU stays throughput-bound (the reference signature has no
+// parameter for it, so the selection travels out of band).
 void ray_trace(uint32_t samples, bool storeRenderResult, uint32_t width, uint32_t height, uint32_t gpu_count) {
     auto report = [](const char* what) { std::fprintf(stderr, "ray_trace: %s: %s\n", what, rt::g_last_error.c_str()); };
     try {
@@ -386,6 +435,16 @@ void ray_trace(uint32_t samples, bool storeRenderResult, uint32_t width, uint32_
         if (rt_multi_set_scene(m, scene.data(), cnt)) return report("rt_multi_set_scene");
         RenderCallInfo rci;
         rt_canonical_render_call_info(samples, width, height, &rci);
+        rt_options opt;
+        std::memset(&opt, 0, sizeof(opt));
+        opt.rng_mode = RT_RNG_PIXEL_STREAM;
+        if (const char* e = std::getenv("RT_RNG")) {
+            if (std::strcmp(e, "hash") == 0) opt.rng_mode = RT_RNG_SAMPLE_HASH;
+            else if (std::strcmp(e, "stream") != 0) {
+                std::fprintf(stderr, "ray_trace: RT_RNG must be 'stream' or 'hash', got '%s'\n", e);
+                return;
+            }
+        }
         DeviceGuard g0(0);
         float* dacc = nullptr;
         uint8_t* dout = nullptr;
@@ -397,7 +456,7 @@ void ray_trace(uint32_t samples, bool storeRenderResult, uint32_t width, uint32_
         }
         (void)hipDeviceSynchronize();
         const auto t0 = std::chrono::steady_clock::now();
-        int rc = rt_multi_render(m, &rci, nullptr, dacc, dout, nullptr);
+        int rc = rt_multi_render(m, &rci, &opt, dacc, dout, nullptr);
         if (rc == RT_OK) rc = hipDeviceSynchronize() == hipSuccess ? RT_OK : RT_ERR_DEVICE;
         const auto t1 = std::chrono::steady_clock::now();
         rt_stats st;
@@ -410,8 +469,9 @@ void ray_trace(uint32_t samples, bool storeRenderResult, uint32_t width, uint32_
         (void)hipFree(dout);
         if (rc != RT_OK) return report("render");
         const double sec = std::chrono::duration<double>(t1 - t0).count();
-        std::printf("duration_per_frame: %.3f ms (%u GPU, %llu samples, %.1f Msamples/s incl. first-launch setup)\n",
-                    sec * 1e3, m->n, (unsigned long long)st.samples, double(st.samples) / sec / 1e6);
+        std::printf("duration_per_frame: %.3f ms (%u GPU, %s stream, %llu samples, %.1f Msamples/s incl. first-launch setup)\n",
+                    sec * 1e3, m->n, opt.rng_mode == RT_RNG_SAMPLE_HASH ? "hash" : "reference",
+                    (unsigned long long)st.samples, double(st.samples) / sec / 1e6);
         if (storeRenderResult && rt_store_ppm("render.ppm", img.data(), width, height)) report("store");
     } catch (const std::exception& e) {
         std::fprintf(stderr, "ray_trace: %s\n", e.what());

@@ -70,10 +70,12 @@ def make_options(max_depth: int = MAX_DEPTH, seed_mode: int = abi.RT_SEED_GLOBAL
     return o
 
 
-def _stream_ptr(stream) -> Optional[int]:
+def _stream_ptr(stream, device: int) -> Optional[int]:
+    """hipStream_t of `stream`, or of torch's current stream ON `device` when None (torch's
+    current device may be another GPU)."""
     if stream is None:
         import torch
-        return torch.cuda.current_stream().cuda_stream
+        return torch.cuda.current_stream(device).cuda_stream
     return getattr(stream, "cuda_stream", stream)
 
 
@@ -122,7 +124,7 @@ class Renderer:
         buf = spheres if not isinstance(spheres, np.ndarray) else np.ascontiguousarray(spheres, np.uint8)
         n = len(spheres)
         ptr = ctypes.addressof(buf) if not isinstance(buf, np.ndarray) else buf.ctypes.data
-        st = _stream_ptr(stream)
+        st = _stream_ptr(stream, self.device)
         check(self._lib.rt_set_scene(self._ctx, ptr if n else None, n, st))
         self.sphere_count = n
 
@@ -131,7 +133,7 @@ class Renderer:
         buf = spheres if not isinstance(spheres, np.ndarray) else np.ascontiguousarray(spheres, np.uint8)
         n = len(spheres)
         ptr = ctypes.addressof(buf) if not isinstance(buf, np.ndarray) else buf.ctypes.data
-        st = _stream_ptr(stream)
+        st = _stream_ptr(stream, self.device)
         check(self._lib.rt_refit_scene(self._ctx, ptr if n else None, n, st))
         self.sphere_count = n
 
@@ -142,7 +144,7 @@ class Renderer:
                 or spheres_dev.shape[1] != 80 or not spheres_dev.is_contiguous():
             raise ValueError("spheres_dev must be a contiguous uint8 cuda tensor [n, 80]")
         n = int(spheres_dev.shape[0])
-        st = _stream_ptr(stream if stream is not None else torch.cuda.current_stream())
+        st = _stream_ptr(stream, self.device)
         fn = self._lib.rt_refit_scene_device if refit else self._lib.rt_set_scene_device
         check(fn(self._ctx, spheres_dev.data_ptr() if n else None, n, st))
         self.sphere_count = n
@@ -197,7 +199,7 @@ class Renderer:
         check(self._lib.rt_render_device(self._ctx, ctypes.byref(rci), rows_ptr, bw, bh,
                                          accum.data_ptr(), out.data_ptr(),
                                          ctypes.byref(options) if options is not None else None,
-                                         _stream_ptr(stream)))
+                                         _stream_ptr(stream, self.device)))
 
     def stats(self) -> Stats:
         st = Stats()
@@ -229,7 +231,7 @@ class Renderer:
         check(self._lib.rt_scatter_rows(self._ctx, src_accum.data_ptr() if src_accum is not None else None,
                                         src_rgba8.data_ptr(), rows.data_ptr(), n, w, dh,
                                         dst_accum.data_ptr() if dst_accum is not None else None,
-                                        dst_rgba8.data_ptr(), _stream_ptr(stream)))
+                                        dst_rgba8.data_ptr(), _stream_ptr(stream, self.device)))
 
     def resolve_rgba8(self, accum, spp: int, out, stream=None) -> None:
         """out = rgba8 tonemap of the summed float4 accumulator `accum` (device tensors), exactly
@@ -237,7 +239,16 @@ class Renderer:
         n = accum.numel() // 4
         if out.numel() != 4 * n:
             raise ValueError("out must hold 4 bytes per accumulator texel")
-        check(self._lib.rt_resolve_rgba8(self._ctx, accum.data_ptr(), n, spp, out.data_ptr(), _stream_ptr(stream)))
+        check(self._lib.rt_resolve_rgba8(self._ctx, accum.data_ptr(), n, spp, out.data_ptr(),
+                                         _stream_ptr(stream, self.device)))
+
+    def kernel_times(self, n: int = 64) -> list:
+        """Trace-kernel durations (ms) of the last `n` launches (at most 64 kept), oldest first:
+        HIP events recorded around the kernel on its launch stream (rt_debug_kernel_times)."""
+        buf = (ctypes.c_float * max(1, n))()
+        got = ctypes.c_uint32(0)
+        check(self._lib.rt_debug_kernel_times(self._ctx, buf, n, ctypes.byref(got)))
+        return [float(buf[i]) for i in range(got.value)]
 
 
 class MultiRenderer:
@@ -281,9 +292,25 @@ class MultiRenderer:
         W, H = rci.image_size.x, rci.image_size.y
         _check_dev_tensor(accum, "torch.float32", (H, W, 4))
         _check_dev_tensor(out, "torch.uint8", (H, W, 4))
+        if accum.device.index != 0 or out.device.index != 0:
+            raise ValueError("MultiRenderer.render gathers to device 0: accum and out must live on cuda:0")
         check(self._lib.rt_multi_render(self._m, ctypes.byref(rci),
                                         ctypes.byref(options) if options is not None else None,
-                                        accum.data_ptr(), out.data_ptr(), _stream_ptr(stream)))
+                                        accum.data_ptr(), out.data_ptr(), _stream_ptr(stream, 0)))
+
+    def info(self) -> dict:
+        """{devices, rccl_ranks (ncclCommCount of the communicator), strip_rows, launches of the
+        last frame} (rt_multi_info)."""
+        v = (ctypes.c_uint32 * 4)()
+        check(self._lib.rt_multi_info(self._m, v))
+        return {"devices": int(v[0]), "rccl_ranks": int(v[1]), "strip_rows": int(v[2]), "launches": int(v[3])}
+
+    def kernel_times(self) -> list:
+        """Trace-kernel ms of the last frame on each device that rendered rows (device order)."""
+        buf = (ctypes.c_float * max(1, self.device_count))()
+        got = ctypes.c_uint32(0)
+        check(self._lib.rt_multi_kernel_times(self._m, buf, self.device_count, ctypes.byref(got)))
+        return [float(buf[i]) for i in range(got.value)]
 
     def stats(self) -> Stats:
         st = Stats()

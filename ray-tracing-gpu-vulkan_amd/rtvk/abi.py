@@ -117,6 +117,8 @@ EXPORTS = {
     "rt_multi_set_scene": (_I, [_P, _P, _U32]),
     "rt_multi_render": (_I, [_P, ctypes.POINTER(RenderCallInfo), ctypes.POINTER(Options), _P, _P, _P]),
     "rt_multi_stats": (_I, [_P, ctypes.POINTER(Stats)]),
+    "rt_multi_info": (_I, [_P, _P]),
+    "rt_multi_kernel_times": (_I, [_P, _P, _U32, ctypes.POINTER(_U32)]),
     "rt_render": (_I, [_P, _U32, _P, _U32, _P, _P, ctypes.POINTER(Options), ctypes.POINTER(Stats)]),
     "rt_store_ppm": (_I, [ctypes.c_char_p, _P, _U32, _U32]),
     "rt_debug_math": (_I, [_I, _I, _P, _P, _U32]),
@@ -124,6 +126,8 @@ EXPORTS = {
     "rt_debug_util": (_I, [_P, _P]),
     "rt_debug_exact_exhaustive": (_I, [ctypes.c_int, _P]),
     "rt_debug_launch_info": (_I, [_P, _P]),
+    "rt_debug_kernel_times": (_I, [_P, _P, _U32, ctypes.POINTER(_U32)]),
+    "rt_build_info": (ctypes.c_char_p, []),
     "rt_debug_walk_hist": (_I, [_P, _P]),
     "rt_debug_lane_hist": (_I, [_P, _P]),
     "rt_debug_tile_cost": (_I, [_P, _P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
@@ -167,6 +171,32 @@ def load_library(path: os.PathLike | str | None = None) -> ctypes.CDLL:
     if path is None:
         _lib = lib
     return lib
+
+
+def source_files() -> list[Path]:
+    """The library's sources in the order the Makefile hashes them (SRC_FILES)."""
+    csrc, inc = PKG_ROOT / "csrc", PKG_ROOT.parent / "include"
+    return (sorted([*csrc.glob("*.hip"), *csrc.glob("*.cpp"), *csrc.glob("*.h")], key=str)
+            + sorted(inc.glob("*.h"), key=str))
+
+
+def sources_sha256() -> str:
+    """sha256 (16 hex) of the library sources in this tree: equals the sources_sha256 of
+    rt_build_info() when the loaded .so was built from them."""
+    import hashlib
+    h = hashlib.sha256()
+    for p in source_files():
+        h.update(p.read_bytes())
+    return h.hexdigest()[:16]
+
+
+def build_info() -> dict:
+    """rt_build_info() of the loaded library, parsed, plus whether it matches this tree."""
+    raw = load_library().rt_build_info().decode()
+    info = dict(kv.split("=", 1) for kv in raw.split(";") if "=" in kv)
+    info["tree_sources_sha256"] = sources_sha256()
+    info["built_from_tree"] = info.get("sources_sha256") == info["tree_sources_sha256"]
+    return info
 
 
 def check(rc: int) -> None:

@@ -1,0 +1,97 @@
+#!/usr/bin/env python3
+"""Contract drift: how far the shipped arithmetic contract (what the HIP kernels
+implement bit for bit) sits from the reference's GLSL read literally.
+
+The oracle renders the same pixels three ways (oracle/rt_oracle.cpp LIT_*):
+  contract  the shipped contract (fma dot, D = fma(b, b, -a c), roots times 1/a, fma hit point)
+  rint      shader.rint:33-55 as written: D = b*b - a*c, roots / a, hit point o + t*d
+  all       also every dot() unfused left to right and normalize(v) = v / length(v)
+and reports, for contract vs each literal form: the fraction of bit-identical accumulator
+texels, of identical rgba8 pixels, and the PSNR of the rgba8 image.
+
+Workloads: (1) blocks of the BASELINE config 3 frame (1920x1080, 10 000 spp, counter-based
+stream, the bench's pixels), (2) a 320x180 frame at 64 spp in both streams.
+Usage: python scripts/contract_drift.py [--blocks 8 --rows 8 --width 24] [--threads N]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+from oracle import oracle  # noqa: E402  (test / measurement infrastructure)
+
+
+def compare(a_acc, a_px, b_acc, b_px) -> dict:
+    same_acc = np.all(a_acc[..., :3] == b_acc[..., :3], axis=-1)
+    same_px = np.all(a_px[..., :3] == b_px[..., :3], axis=-1)
+    mse = float(np.mean((a_px[..., :3].astype(np.float64) - b_px[..., :3]) ** 2))
+    rel = np.abs(a_acc[..., :3].astype(np.float64) - b_acc[..., :3]) / np.maximum(1e-30, np.abs(b_acc[..., :3]))
+    mean_a, mean_b = float(a_acc[..., :3].astype(np.float64).mean()), float(b_acc[..., :3].astype(np.float64).mean())
+    return {"texels": int(same_acc.size), "accum_bit_identical": round(float(same_acc.mean()), 6),
+            "image_mean_rel_diff": (mean_a - mean_b) / mean_b,
+            "rgba8_identical": round(float(same_px.mean()), 6),
+            "psnr_db": "inf" if mse == 0 else round(10 * np.log10(255 ** 2 / mse), 2),
+            "accum_max_rel_diff": float(rel.max())}
+
+
+def render3(sc, rci, w, h, rows, rng, threads):
+    out = {}
+    for name, lit in (("contract", oracle.LIT_CONTRACT), ("rint", oracle.LIT_RINT), ("all", oracle.LIT_ALL)):
+        t0 = time.perf_counter()
+        acc, px, st = oracle.render(sc, rci, w, h, rows=rows, opts=oracle.options(rng_mode=rng, lit=lit),
+                                    threads=threads)
+        out[name] = (acc, px, st, time.perf_counter() - t0)
+    return out
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--blocks", type=int, default=8)
+    ap.add_argument("--rows", type=int, default=8)
+    ap.add_argument("--width", type=int, default=24)
+    ap.add_argument("--spp", type=int, default=10000)
+    ap.add_argument("--threads", type=int, default=os.cpu_count() or 1)
+    args = ap.parse_args()
+    oracle.build()
+    sc = oracle.generate_scene(0.0)
+    res = {}
+    # (1) config 3 blocks, counter-based stream (the bench's stream), spread like bench.py's cpu_baseline
+    W, H = 1920, 1080
+    ys = np.linspace(0, H - args.rows, args.blocks).round().astype(int)
+    xs = np.linspace(0, W - args.width, args.blocks).round().astype(int)[::-1]
+    parts = {k: [] for k in ("contract", "rint", "all")}
+    secs = 0.0
+    for y, x in zip(ys, xs):
+        rows = np.arange(y, y + args.rows, dtype=np.uint32)
+        r = render3(sc, oracle.render_call_info(args.spp, W, H, (int(x), 0)), args.width, args.rows, rows,
+                    2, args.threads)
+        for k in parts:
+            parts[k].append(r[k][:2])
+        secs += sum(v[3] for v in r.values())
+    cat = {k: (np.concatenate([p[0] for p in v]), np.concatenate([p[1] for p in v])) for k, v in parts.items()}
+    res["config3_blocks"] = {
+        "pixels": f"{args.blocks} blocks of {args.rows} rows x {args.width} px of 1920x1080 at {args.spp} spp, hash stream",
+        "rint_literal": compare(*cat["rint"], *cat["contract"]),
+        "all_literal": compare(*cat["all"], *cat["contract"]),
+        "cpu_s": round(secs, 1)}
+    # (2) 320x180 at 64 spp, both streams
+    for rng, name in ((0, "stream"), (2, "hash")):
+        r = render3(sc, oracle.render_call_info(64, 320, 180), 320, 180, None, rng, args.threads)
+        res[f"320x180_64spp_{name}"] = {
+            "rint_literal": compare(*r["rint"][:2], *r["contract"][:2]),
+            "all_literal": compare(*r["all"][:2], *r["contract"][:2]),
+            "segments": {k: v[2][0] for k, v in r.items()}}
+    print(json.dumps(res, indent=1))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

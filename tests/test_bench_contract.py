@@ -36,3 +36,43 @@ def test_bench_json_line_contract():
     assert d["config"]["rng"] == "hash" and "reference_stream" in d and "brute_force" in d
     assert d["roofline"]["lib_sha256"] and "frac_basis" in d["roofline"]
     assert cb["parity"]["accum_bit_exact"] and cb["parity"]["rgba8_equal"] and cb["parity"]["psnr_db"] == "inf"
+    # honest labels: the accel named in config is the walk that ran (the roofline's kernel)
+    assert d["config"]["path"] == "single" and d["config"]["accel"] in ("grid-lds", "lbvh-octant-lds")
+    assert ("grid" in d["roofline"]["kernel"]) == d["config"]["accel"].startswith("grid")
+    # the kernel is timed inside the timed region: it cannot outlast the step
+    assert 0 < roof["kernel_ms"] <= d["ms_per_step"]
+    assert d["build"]["built_from_tree"], d["build"]
+    if d["config"]["accel"].startswith("grid"):
+        assert d["lbvh_walk"]["image_bit_equal_to_headline"] and d["lbvh_walk"]["accel"] == "lbvh-octant-lds"
+
+
+@pytest.mark.gpu
+def test_bench_multi_path_one_gpu():
+    """--path multi: the C-ABI rt_multi path (one process, ncclCommInitAll, strips + RCCL gather)
+    on the box's one GPU; labelled as such, with the communicator's rank count."""
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--width", "96", "--height", "64", "--spp", "2",
+                        "--steps", "2", "--warmup", "1", "--path", "multi", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["config"]["path"] == "multi" and "rt_multi" in d["config"]["parallelism"]
+    assert "communicator of 1 ranks" in d["config"]["parallelism"]
+    assert d["n_gpus"] == 1 and d["value"] > 0 and 0 < d["roofline"]["kernel_ms"] <= d["ms_per_step"]
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """--gpus N without a launcher drives rt_multi over N GPUs; with fewer visible it fails instead
+    of silently benching fewer."""
+    import torch
+    n = torch.cuda.device_count()
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(max(1, n) + 1), "--steps", "1"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 2 and "visible" in r.stderr
+
+
+def test_bench_refuses_launcher_mismatch():
+    import os
+    e = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "1", "--steps", "1"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=e)
+    assert r.returncode == 2 and "WORLD_SIZE" in r.stderr

@@ -8,8 +8,8 @@ import pytest
 CLI = Path(__file__).resolve().parent.parent / "ray-tracing-gpu-vulkan_amd" / "bin" / "rt_mi355x_cli"
 
 
-def run(*args, cwd=None):
-    return subprocess.run([str(CLI), *args], capture_output=True, text=True, cwd=cwd, timeout=300)
+def run(*args, cwd=None, env=None):
+    return subprocess.run([str(CLI), *args], capture_output=True, text=True, cwd=cwd, timeout=300, env=env)
 
 
 def test_help_lists_reference_flags():
@@ -58,9 +58,9 @@ def test_frames_no_device_fails_loudly():
 @pytest.mark.gpu
 @pytest.mark.parametrize("rng", ["stream", "hash"])
 def test_frame_loop_matches_oracle(tmp_path, oracle, rng):
-    """--frames: the benchmark loop (two frames in flight, per-frame scene rebuild, the image tiled
-    over the GPUs with an RCCL gather) prints duration_per_frame like the reference and its last
-    frame equals the oracle's, in both random stream modes."""
+    """--frames: the benchmark loop (one rt_multi, frames queued asynchronously, per-frame scene
+    rebuild, the image tiled over the GPUs with an RCCL gather) prints duration_per_frame like the
+    reference and its last frame equals the oracle's, in both random stream modes."""
     r = run("--frames", "5", "--store", "--samples", "2", "--width", "72", "--height", "40", "--rng", rng,
             cwd=tmp_path)
     assert r.returncode == 0, r.stderr
@@ -72,3 +72,39 @@ def test_frame_loop_matches_oracle(tmp_path, oracle, rng):
     _, ref, _ = oracle.render(oracle.generate_scene(), oracle.render_call_info(2, 72, 40), 72, 40,
                               opts=oracle.options(rng_mode=2 if rng == "hash" else 0))
     np.testing.assert_array_equal(img, ref[..., :3])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("how", ["env", "flag"])
+def test_ray_trace_hash_stream_matches_oracle(tmp_path, oracle, how):
+    """The drop-in entry point's scalable mode: ray_trace() in the counter-based stream, selected by
+    RT_RNG=hash in the environment (the reference signature has no parameter for it) or by the
+    CLI's --rng hash, renders the oracle's hash-stream image (1 device here; any device count
+    renders the same image)."""
+    import os
+    e = dict(os.environ)
+    args = ["--store", "--samples", "5", "--width", "64", "--height", "36"]
+    if how == "env":
+        e["RT_RNG"] = "hash"
+    else:
+        args += ["--rng", "hash"]
+    r = run(*args, cwd=tmp_path, env=e)
+    assert r.returncode == 0, r.stderr
+    assert "hash stream" in r.stdout
+    data = (tmp_path / "render.ppm").read_bytes()
+    hdr = b"P6\n64 36\n255\n"
+    img = np.frombuffer(data[len(hdr):], np.uint8).reshape(36, 64, 3)
+    _, ref, _ = oracle.render(oracle.generate_scene(), oracle.render_call_info(5, 64, 36), 64, 36,
+                              opts=oracle.options(rng_mode=2))
+    np.testing.assert_array_equal(img, ref[..., :3])
+    _, ref_stream, _ = oracle.render(oracle.generate_scene(), oracle.render_call_info(5, 64, 36), 64, 36)
+    assert not np.array_equal(img, ref_stream[..., :3])
+
+
+@pytest.mark.gpu
+def test_ray_trace_rejects_unknown_rng(tmp_path):
+    import os
+    e = dict(os.environ, RT_RNG="philox")
+    r = run("--store", "--samples", "1", "--width", "16", "--height", "8", cwd=tmp_path, env=e)
+    assert "RT_RNG must be" in r.stderr
+    assert not (tmp_path / "render.ppm").exists()

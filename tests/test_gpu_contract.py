@@ -1,0 +1,132 @@
+"""GPU checks of the boundary's contract beyond pixel parity: the full headline frame across
+walks, the kernel's distance from a literal reading of the GLSL, the hash stream's colour range,
+in-region kernel timing and build provenance, and what the multi-device path reports."""
+import numpy as np
+import pytest
+
+from test_gpu_parity import GRID, HASH, LBVH, LBVH_OCT, STREAM, assert_same, gpu_render  # noqa: F401
+from test_gpu_parity import renderer, rtvk, torch  # noqa: F401  (module fixtures)
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("rng_mode", [HASH, STREAM])
+def test_config3_full_frame_grid_equals_lbvh(rtvk, renderer, torch, oracle, rng_mode):
+    """BASELINE config 3 in full (1920x1080, 10 000 spp): the default walk (uniform grid in LDS)
+    and the octant LBVH walk the baseline names give the same frame, every accumulator float and
+    every rgba8 byte of all 2 073 600 pixels, with equal segment counts, in both streams."""
+    W, H, spp = 1920, 1080, 10000
+    sc = oracle.generate_scene()
+    rci = oracle.render_call_info(spp, W, H)
+    a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH, rng_mode=rng_mode)
+    assert renderer.launch_info()["form"] == "grid-lds"
+    a2, o2, st2 = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH_OCT, rng_mode=rng_mode)
+    assert renderer.launch_info()["form"] == "lbvh-octant-lds"
+    assert_same(a, o, a2, o2)
+    assert (st.segments, st.samples) == (st2.segments, st2.samples) and st.samples == W * H * spp
+
+
+@pytest.mark.parametrize("rng_mode,min_psnr", [(HASH, 50.0), (STREAM, 40.0)])
+def test_kernel_vs_literal_glsl(rtvk, renderer, torch, oracle, rng_mode, min_psnr):
+    """Contract drift: the kernel is bit-exact to the shipped contract; against
+    the oracle's literal readings of the GLSL (shader.rint:46-55 with unfused D and a true / a;
+    then every dot / normalize as written) it differs only where rounding flips a branch. At
+    320x180, 64 spp the rgba8 PSNR stays above the floor (hash stream: a flipped branch changes
+    one sample; reference stream: it changes the rest of the pixel's chain)."""
+    W, H, spp = 320, 180, 64
+    sc = oracle.generate_scene()
+    rci = oracle.render_call_info(spp, W, H)
+    a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH, rng_mode=rng_mode)
+    ca, co, _ = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=rng_mode), threads=16)
+    assert_same(a, o, ca, co)
+    for lit in (oracle.LIT_RINT, oracle.LIT_ALL):
+        la, lo, _ = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=rng_mode, lit=lit), threads=16)
+        same = np.all(a[..., :3] == la[..., :3], axis=-1).mean()
+        mse = np.mean((o[..., :3].astype(np.float64) - lo[..., :3]) ** 2)
+        psnr = 10 * np.log10(255 ** 2 / mse)
+        print(f"rng {rng_mode} lit {lit}: {same:.4f} of accumulator texels bit-identical, rgba8 PSNR {psnr:.2f} dB")
+        assert psnr >= min_psnr and same > 0.7
+
+
+def _bright_scene(oracle):
+    sc = oracle.generate_scene().copy()
+    col = sc[:, 32:48].copy().view(np.float32)   # colors[0]
+    col[1, :3] = [1.6, 0.9, 0.4]                  # the big diffuse sphere: albedo above 1
+    sc[:, 32:48] = col.view(np.uint8)
+    return sc
+
+
+@pytest.mark.parametrize("builder", [None, "gpu"])
+def test_hash_stream_refuses_colours_outside_unit(rtvk, renderer, torch, oracle, builder):
+    """RT_RNG_SAMPLE_HASH sums per-sample colours in 8.24 fixed point (channels in [0, 1]); the
+    reference sums unclamped (shader.rgen:55-59). A scene with a colour channel above 1 is refused
+    in hash mode (host- and device-built scenes alike), and renders bit-exactly (unclamped) in the
+    reference stream."""
+    sc = _bright_scene(oracle)
+    W, H, spp = 48, 32, 3
+    rci = oracle.render_call_info(spp, W, H)
+    with pytest.raises(rtvk.RtError, match="RT_RNG_SAMPLE_HASH needs every sphere colour"):
+        gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH, rng_mode=HASH, builder=builder)
+    a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH, rng_mode=STREAM, builder=builder)
+    ra, ro, rs = oracle.render(sc, rci, W, H)
+    assert_same(a, o, ra, ro)
+    assert (a[..., :3] / spp > 1.0).any()   # some pixel really is brighter than 1 per sample
+    # back to a [0, 1] scene: hash mode renders again
+    a, o, _ = gpu_render(rtvk, renderer, torch, oracle.generate_scene(), rci, W, H, accel=LBVH, rng_mode=HASH,
+                         builder=builder)
+    ra, ro, _ = oracle.render(oracle.generate_scene(), rci, W, H, opts=oracle.options(rng_mode=HASH))
+    assert_same(a, o, ra, ro)
+
+
+def test_kernel_times_inside_the_timed_region(rtvk, torch, oracle):
+    """rt_debug_kernel_times: the trace kernel's own duration for each of the last launches,
+    recorded on the launch stream with no host sync in between, each within the wall time of the
+    whole sequence."""
+    import time
+    sc = oracle.generate_scene()
+    renderer = rtvk.Renderer(0)
+    renderer.set_scene(sc)
+    W, H = 640, 360
+    rci = rtvk.canonical_render_call_info(64, W, H)
+    acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+    out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+    opt = rtvk.make_options(rng_mode=HASH)
+    renderer.render_device(rci, acc, out, options=opt)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(5):
+        renderer.render_device(rci, acc, out, options=opt)
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) * 1e3
+    ks = renderer.kernel_times(5)
+    assert len(ks) == 5 and all(k > 0 for k in ks) and sum(ks) <= wall
+    assert len(renderer.kernel_times(1000)) == 6
+    renderer.close()
+
+
+def test_build_provenance(rtvk):
+    """The loaded library says which sources it was built from, and they are this tree's."""
+    from rtvk import abi
+    info = abi.build_info()
+    assert info["arch"] == "gfx950" and info["built_from_tree"], info
+
+
+def test_multi_renderer_reports_communicator(rtvk, torch, oracle):
+    """rt_multi_info: the RCCL communicator's own rank count (ncclCommCount) equals the devices
+    rt_multi opened, and the last frame's launches / per-device kernel times are reported."""
+    n = torch.cuda.device_count()
+    with rtvk.MultiRenderer(n) as m:
+        m.set_scene(oracle.generate_scene())
+        W, H = 64, 40
+        acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda:0")
+        out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda:0")
+        m.render(rtvk.canonical_render_call_info(2, W, H), acc, out, options=rtvk.make_options(rng_mode=HASH))
+        torch.cuda.synchronize()
+        info = m.info()
+        assert info["devices"] == n and info["rccl_ranks"] == n and info["strip_rows"] == 8
+        assert info["launches"] == min(n, (H + 7) // 8)
+        kt = m.kernel_times()
+        assert len(kt) == info["launches"] and all(k > 0 for k in kt)
+        with pytest.raises((TypeError, ValueError)):
+            bad = torch.zeros((H, W, 4), dtype=torch.float32, device="cpu")
+            m.render(rtvk.canonical_render_call_info(2, W, H), bad, out)

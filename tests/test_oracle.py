@@ -241,3 +241,31 @@ def test_sky_matches_reference_render(oracle):
     sky_ours = out[0, 0, :3].astype(np.float32)
     assert sky_ours.tolist() == [213.0, 228.0, 255.0]
     np.testing.assert_allclose(sky_ref, sky_ours, atol=0.5)
+
+
+@pytest.mark.parametrize("rng,min_psnr", [(0, 35.0), (2, 45.0)])
+def test_literal_glsl_forms_near_contract(oracle, rng, min_psnr):
+    """The contract drift measure: the oracle's literal readings of the GLSL
+    (LIT_RINT: shader.rint:33-55 as written, unfused D and / a; LIT_ALL: also every dot() and
+    normalize() as written) against the shipped contract the kernels implement. They differ (in
+    some pixels, through rounding-flipped branches) but stay close: at 96x54, 16 spp the image
+    PSNR stays above the stated floor and the mean brightness within 1 %."""
+    sc = oracle.generate_scene()
+    rci = oracle.render_call_info(16, 96, 54)
+    acc0, px0, st0 = oracle.render(sc, rci, 96, 54, opts=oracle.options(rng_mode=rng))
+    for lit in (oracle.LIT_RINT, oracle.LIT_ALL):
+        acc, px, st = oracle.render(sc, rci, 96, 54, opts=oracle.options(rng_mode=rng, lit=lit))
+        assert not np.array_equal(acc, acc0)   # the forms really differ
+        mse = np.mean((px[..., :3].astype(np.float64) - px0[..., :3]) ** 2)
+        assert 10 * np.log10(255 ** 2 / mse) >= min_psnr
+        assert abs(acc[..., :3].mean() / acc0[..., :3].mean() - 1) < 0.01
+        assert abs(st[0] / st0[0] - 1) < 0.01
+
+
+def test_literal_form_contract_unchanged(oracle):
+    """Selecting the contract explicitly is the default render (the literal forms are opt-in)."""
+    sc = oracle.generate_scene()
+    rci = oracle.render_call_info(2, 40, 24)
+    a0, p0, _ = oracle.render(sc, rci, 40, 24)
+    a1, p1, _ = oracle.render(sc, rci, 40, 24, opts=oracle.options(lit=oracle.LIT_CONTRACT))
+    assert np.array_equal(a0, a1) and np.array_equal(p0, p1)
