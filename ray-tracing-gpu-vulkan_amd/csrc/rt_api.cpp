@@ -89,6 +89,8 @@ struct rt_context {
     unsigned long long* fixed = nullptr;
     uint64_t fixed_cap = 0;                      // texels
     uint32_t last_chunks = 1;
+    uint32_t last_accel = 0;                     // kernel form (rt::ACCEL_*) of the last launch, 0 = none yet
+    size_t last_lds = 0;                         // its dynamic LDS bytes
     // every colour the shaders can return lies in [0, 1] (RT_RNG_SAMPLE_HASH's fixed point needs it)
     bool colours_unit = true;
     // HIP events bracketing the trace kernel of the last kKernelEvents launches (ring; timing
@@ -673,6 +675,7 @@ int scene_op(rt_context* ctx, hipStream_t st, F&& body) {
         return rc;
     }
     ctx->scene_set = true;
+    ctx->last_accel = 0;   // launch info reports the new scene's default form until it renders
     return mark_issued(ctx, st);
 }
 
@@ -920,6 +923,8 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     if (n_tiles * chunks * 64u >= (1ull << 32)) return fail(RT_ERR_INVALID_ARGUMENT, "band too large");
     P.chunks = uint32_t(chunks);
     ctx->last_chunks = P.chunks;
+    ctx->last_accel = accel;
+    ctx->last_lds = lds;
     P.n_units = uint32_t(n_tiles * chunks * 64u);
     const uint64_t texels = uint64_t(band_width) * band_height;
     if (mode == rt::MODE_HASH) {
@@ -1115,11 +1120,15 @@ const char* rt_build_info(void) {
 int rt_debug_launch_info(rt_context* ctx, uint32_t* out4) {
     if (!ctx || !out4) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     out4[0] = ctx->last_chunks;
-    // the default form of the current scene for a camera within its pad radius (rt_render_device)
-    const bool grid = ctx->has_grid && (ctx->grid_bytes || !ctx->oct_bytes);
-    out4[1] = grid ? (ctx->grid_bytes ? rt::ACCEL_GRID : rt::ACCEL_GRID_GLOBAL) : ctx->oct_bytes ? rt::ACCEL_LBVH_OCT
-              : ctx->lds1_bytes ? rt::ACCEL_LBVH_LDS : ctx->gpu_tree ? rt::ACCEL_LBVH_TOP : rt::ACCEL_LBVH_GLOBAL;
-    out4[2] = uint32_t(grid ? ctx->grid_bytes : ctx->oct_bytes ? ctx->oct_bytes : ctx->lds1_bytes);
+    if (ctx->last_accel) {   // the kernel form the last launch actually ran
+        out4[1] = ctx->last_accel;
+        out4[2] = uint32_t(ctx->last_lds);
+    } else {   // no launch yet: the default form of the current scene (camera within its pad radius)
+        const bool grid = ctx->has_grid && (ctx->grid_bytes || !ctx->oct_bytes);
+        out4[1] = grid ? (ctx->grid_bytes ? rt::ACCEL_GRID : rt::ACCEL_GRID_GLOBAL) : ctx->oct_bytes ? rt::ACCEL_LBVH_OCT
+                  : ctx->lds1_bytes ? rt::ACCEL_LBVH_LDS : ctx->gpu_tree ? rt::ACCEL_LBVH_TOP : rt::ACCEL_LBVH_GLOBAL;
+        out4[2] = uint32_t(grid ? ctx->grid_bytes : ctx->oct_bytes ? ctx->oct_bytes : ctx->lds1_bytes);
+    }
     out4[3] = uint32_t(ctx->cu_count);
     return RT_OK;
 }
