@@ -170,6 +170,8 @@ WALK_NAMES = {   # rt_debug_launch_info form -> (kernel, walk)
     "lbvh-global": ("rt_trace_global_kernel", "LBVH, every node from L2"),
     "grid-lds": ("rt_trace_grid_kernel<grid in LDS>", "uniform grid (3D DDA), staged in LDS"),
     "grid-global": ("rt_trace_grid_kernel<grid from L2>", "uniform grid (3D DDA), from L2"),
+    "grid-lds-coop": ("rt_trace_grid_kernel<grid in LDS, wave-cooperative>",
+                      "uniform grid (3D DDA) staged in LDS, reference tests spread over the wave's lanes"),
 }
 
 

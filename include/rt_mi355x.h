@@ -111,7 +111,8 @@ typedef struct rt_options {
                              reserved[1] = LBVH walk form: 0 automatic (octant node copies in LDS
                              when they fit, else one copy in LDS, else an LDS treelet over L2
                              subtrees), 6 one LDS node copy, 8 octant copies, 10 every node from
-                             L2 */
+                             L2, 12 the uniform grid, 14 the uniform grid in LDS with the
+                             wave-cooperative walk */
 } rt_options;
 
 /* Statistics of the last rt_render_device() on a context (valid after its stream completes). */

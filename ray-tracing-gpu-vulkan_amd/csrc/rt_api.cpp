@@ -770,13 +770,18 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     if (o.accel == RT_ACCEL_BRUTE) {
         accel = rt::ACCEL_BRUTE;
     } else if (ctx->has_grid && cam_r <= ctx->grid_pad_radius &&
-               (form == 12u || (form == 0u && (ctx->grid_bytes || !ctx->oct_bytes)))) {
+               (form == 12u || form == 14u || (form == 0u && (ctx->grid_bytes || !ctx->oct_bytes)))) {
         // the grid: staged in LDS when it fits (config 3: 1 % faster than the
         // octant tree), else the octant tree when that fits LDS (a device-built scene of ~1000
         // spheres, whose grid would be read from L2), else the grid from L2; its margin covers
         // cameras within its pad radius
         accel = ctx->grid_bytes ? rt::ACCEL_GRID : rt::ACCEL_GRID_GLOBAL;
         lds = ctx->grid_bytes ? ctx->grid_bytes : rt::kBigLdsBytes;
+        // the wave-cooperative walk of the LDS grid: form 14, or RT_GRID_COOP=1
+        const char* ce = std::getenv("RT_GRID_COOP");
+        if (accel == rt::ACCEL_GRID && (form == 14u || (form == 0u && ce && std::strcmp(ce, "1") == 0)) &&
+            ctx->grid_bytes + rt::kLaneSumLdsBytes + rt::kCoopLdsBytes <= kMaxLdsBytes)
+            accel = rt::ACCEL_GRID_COOP;
     } else if (ctx->oct_bytes && (form == 0u || form == 8u)) {
         accel = rt::ACCEL_LBVH_OCT;
         lds = ctx->oct_bytes;
@@ -824,7 +829,8 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     P.nodes_oct = d.nodes_oct;
     P.treelet = d.treelet;
     P.treelet_count = d.treelet_count;
-    if (accel == rt::ACCEL_GRID || accel == rt::ACCEL_GRID_GLOBAL) {   // (cell_start also marks a walk)
+    const bool grid_walk = accel == rt::ACCEL_GRID || accel == rt::ACCEL_GRID_GLOBAL || accel == rt::ACCEL_GRID_COOP;
+    if (grid_walk) {   // (cell_start also marks a walk)
         P.grid = d.grid;
         P.cell_start = d.cell_start;
         P.grid_rec = d.grid_rec;
@@ -848,7 +854,7 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     // t lies within 9.1e-4 |oc| (sqrt of D's error, 14 u |oc|^2) of the true or closest-approach t.
     P.cull_near_t = -1.0f;
     P.cull_near_abs = P.cull_abs;
-    if ((accel == rt::ACCEL_GRID || accel == rt::ACCEL_GRID_GLOBAL) && d.small_rmin > 0.0f &&
+    if (grid_walk && d.small_rmin > 0.0f &&
         std::isfinite(d.small_rmin)) {
         const double m = RT_GRID_SPARE * std::min<double>(d.grid.cs[0], std::min<double>(d.grid.cs[1], d.grid.cs[2]));
         // budget: 3/4 of the spare part for eps_d, 1/4 for a walk that starts (at tmin) up to

@@ -91,6 +91,9 @@ struct GridInfo {
 // Static LDS of the grid kernels beside their dynamic LDS: per-thread 64-bit unit sums of the
 // counter-based stream (rt_kernels.hip s_lane_sum).
 constexpr unsigned kLaneSumLdsBytes = 3u * 8u * RT_TRACE_BLOCK;
+// Wave-cooperative grid walk (ACCEL_GRID_COOP): per thread a ray (2 float4), a key (u64) and a
+// pass marker (u32) in LDS.
+constexpr unsigned kCoopLdsBytes = (2u * 16u + 8u + 4u) * RT_TRACE_BLOCK;
 
 // Scene as resident in HBM (one allocation per context, rebuilt by rt_set_scene).
 struct DeviceScene {
@@ -125,7 +128,7 @@ struct DeviceScene {
 // scene records in LDS), TOP (bigger trees: LDS treelet + L2 subtrees). GLOBAL (every node from
 // L2) is the A/B reference of TOP (options.reserved[1] = 10).
 enum : uint32_t { ACCEL_BRUTE = 1, ACCEL_LBVH_GLOBAL = 2, ACCEL_LBVH_LDS = 3, ACCEL_LBVH_OCT = 4,
-                  ACCEL_LBVH_TOP = 5, ACCEL_GRID = 6, ACCEL_GRID_GLOBAL = 7, ACCEL_COUNT = 8 };
+                  ACCEL_LBVH_TOP = 5, ACCEL_GRID = 6, ACCEL_GRID_GLOBAL = 7, ACCEL_GRID_COOP = 8, ACCEL_COUNT = 9 };
 
 // Random stream layout of a launch (template parameter of the trace kernels).
 //   STREAM: the reference's per-pixel LCG stream (random.glsl), or with rng_counter the TEA

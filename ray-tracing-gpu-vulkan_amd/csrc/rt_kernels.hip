@@ -815,7 +815,8 @@ constexpr uint32_t END = 0xffffffffu;
 // Walk forms (template LAYOUT): GLOBAL = escape-link BvhNode pairs from L2 (A/B reference of TOP),
 // LDS1 = one node copy in LDS (AB layout), OCT = 8 octant-specialised copies in LDS, TOP = LDS
 // treelet over L2 subtrees.
-enum : int { LAYOUT_GLOBAL = 0, LAYOUT_LDS1 = 1, LAYOUT_OCT = 2, LAYOUT_TOP = 3, LAYOUT_GRID = 4, LAYOUT_GRID_L2 = 5 };
+enum : int { LAYOUT_GLOBAL = 0, LAYOUT_LDS1 = 1, LAYOUT_OCT = 2, LAYOUT_TOP = 3, LAYOUT_GRID = 4, LAYOUT_GRID_L2 = 5,
+             LAYOUT_GRID_COOP = 6 };
 
 // Node slab test: one fma per plane, t = fma(plane, inv, -o * inv) (a sub-then-mul form is exact
 // in the gate's own arithmetic but costs twice the issue cycles: packed f32 ops take 4 cycles on
@@ -892,7 +893,10 @@ __device__ __forceinline__ void setup_ray(const rt::TraceParams& P, const BigTab
     r.a = dot(r.d, r.d);
     r.ia = rcp_cr(r.a);
     r.inv = v3(rcp_cr(r.d.x), rcp_cr(r.d.y), rcp_cr(r.d.z));
-    r.best = T_MAX_SUCC;
+    // closest so far: none, with t <= tMax (shader.rint:32-39 reports t <= tMax). The walks accept
+    // (t <= best, lowest id on ties), so best = 10000 exactly accepts a report at tMax and nothing
+    // beyond it, and the (t bits, id) keys of the cooperative walk order the same way.
+    r.best = 10000.0f;
     r.bi = 0xffffffffu;
     for (uint32_t k0 = 0; k0 < P.n_big; k0 += 4) {   // wave-uniform: LDS broadcast reads
         const float4 b0 = big.rec[k0], b1 = big.rec[k0 + 1], b2 = big.rec[k0 + 2], b3 = big.rec[k0 + 3];
@@ -1029,6 +1033,174 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
         tx = mx ? tnew : tx;
         ty = my ? tnew : ty;
         tz = mz ? tnew : tz;
+    }
+}
+
+// ---- wave-cooperative grid walk (LAYOUT_GRID_COOP) ---------------------------
+// Wave64 inclusive scans through DPP: row_shr 1/2/4/8 inside each 16-lane row (zero fill), then
+// row_bcast:15 (lane 15 of rows 0 / 2 into rows 1 / 3) and row_bcast:31 (lane 31 into rows 2, 3).
+// Every lane of the wave must be active (exec full): DPP reads disabled lanes as the fill value.
+__device__ __forceinline__ uint32_t wave_scan_add(uint32_t v) {
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x111, 0xf, 0xf, false));
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x112, 0xf, 0xf, false));
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x114, 0xf, 0xf, false));
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x118, 0xf, 0xf, false));
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x142, 0xa, 0xf, false));
+    v += uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x143, 0xc, 0xf, false));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_scan_max(uint32_t v) {
+    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x111, 0xf, 0xf, false)));
+    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x112, 0xf, 0xf, false)));
+    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x114, 0xf, 0xf, false)));
+    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x118, 0xf, 0xf, false)));
+    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x142, 0xa, 0xf, false)));
+    v = max(v, uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x143, 0xc, 0xf, false)));
+    return v;
+}
+
+// Per wave (64 slots of its block's arrays): the rays of the segment (o, a | d, 1/a), the closest
+// hit so far as a (t bits, sphere id) key, and the slot markers of one pass.
+__shared__ float4 s_coop_ray[2 * RT_TRACE_BLOCK];
+__shared__ unsigned long long s_coop_key[RT_TRACE_BLOCK];
+__shared__ uint32_t s_coop_mark[RT_TRACE_BLOCK];
+static_assert(sizeof(s_coop_ray) + sizeof(s_coop_key) + sizeof(s_coop_mark) == rt::kCoopLdsBytes, "rt_internal.h");
+
+// Compiler-only ordering of LDS accesses made by different lanes of one wave: the LDS executes a
+// wave's instructions in issue order, so no wait or barrier is needed, only no reordering.
+__device__ __forceinline__ void lane_order() { asm volatile("" ::: "memory"); }
+
+// The grid walk of grid_walk with the reference tests of a wave's rays spread over all 64 lanes.
+// Rounds: every walking lane takes its current cell's n references; an exclusive scan of n gives
+// each ray its run [start, start + n) of the round's `total` (ray, reference) pairs, which the
+// wave tests in ceil(total / 64) passes with every lane busy instead of max-over-lanes passes at
+// one reference per lane. A pass finds each slot's ray by a max-scan of the runs' start markers;
+// a candidate lowers its ray's key by an LDS 64-bit atomic minimum. t >= tmin > 0, so the float
+// bits order like the values and the u64 minimum of (t bits << 32 | id) is exactly the walks'
+// (t, lowest id) rule: the order of tests cannot change the result. After the passes each ray
+// reads its key, updates its cull limit and takes its DDA step, as grid_walk does after a cell:
+// the cells visited, the references tested and the closest hit are grid_walk's. Called with every
+// lane of the wave (tracing or not), never inside divergent control flow.
+template <bool COUNT>
+__device__ __forceinline__ void grid_walk_coop(const rt::TraceParams& P, const uint32_t* __restrict__ cstart,
+                                               const float4* __restrict__ rec, const uint32_t* __restrict__ ids,
+                                               Ray& r, bool tracing, uint32_t& n_cell, uint32_t& n_sph) {
+    const rt::GridInfo& G = P.grid;
+    const uint32_t lane = lane_id();
+    const uint32_t wave0 = __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
+    float4* const rayA = s_coop_ray + wave0;
+    float4* const rayB = s_coop_ray + RT_TRACE_BLOCK + wave0;
+    unsigned long long* const key = s_coop_key + wave0;
+    uint32_t* const mark = s_coop_mark + wave0;
+    bool walking = tracing && r.walk;
+    int cx = 0, cy = 0, cz = 0, sx = 0, sy = 0, sz = 0;
+    float tx = 0.0f, ty = 0.0f, tz = 0.0f;
+    uint32_t cell = 0;
+    if (walking) {   // entry cell and DDA state: grid_walk's arithmetic
+        const float x0 = (G.lo_m[0] - r.o.x) * r.inv.x, x1 = (G.hi_m[0] - r.o.x) * r.inv.x;
+        const float y0 = (G.lo_m[1] - r.o.y) * r.inv.y, y1 = (G.hi_m[1] - r.o.y) * r.inv.y;
+        const float z0 = (G.lo_m[2] - r.o.z) * r.inv.z, z1 = (G.hi_m[2] - r.o.z) * r.inv.z;
+        const float tn = fmaxf(fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1)), T_MIN);
+        const float tf = fminf(fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1)), r.limit);
+        walking = tn <= tf;
+        if (walking) {
+            auto cell_of = [&](float p, int k) {
+                const int c = int(floorf((p - G.gmin[k]) * G.inv_cs[k]));
+                return min(max(c, 0), int(G.n[k]) - 1);
+            };
+            cx = cell_of(__builtin_fmaf(tn, r.d.x, r.o.x), 0);
+            cy = cell_of(__builtin_fmaf(tn, r.d.y, r.o.y), 1);
+            cz = cell_of(__builtin_fmaf(tn, r.d.z, r.o.z), 2);
+            sx = r.d.x > 0.0f ? 1 : (r.d.x < 0.0f ? -1 : 0);
+            sy = r.d.y > 0.0f ? 1 : (r.d.y < 0.0f ? -1 : 0);
+            sz = r.d.z > 0.0f ? 1 : (r.d.z < 0.0f ? -1 : 0);
+            auto bound_t = [&](int c, int s, int k, float o, float inv) {
+                const float plane = __builtin_fmaf(float(c + (s > 0 ? 1 : 0)), G.cs[k], G.gmin[k]);
+                return s == 0 ? __builtin_inff() : (plane - o) * inv;
+            };
+            tx = bound_t(cx, sx, 0, r.o.x, r.inv.x);
+            ty = bound_t(cy, sy, 1, r.o.y, r.inv.y);
+            tz = bound_t(cz, sz, 2, r.o.z, r.inv.z);
+            cell = (uint32_t(cz) * G.n[1] + uint32_t(cy)) * G.n[0] + uint32_t(cx);
+            rayA[lane] = make_float4(r.o.x, r.o.y, r.o.z, r.a);
+            rayB[lane] = make_float4(r.d.x, r.d.y, r.d.z, r.ia);
+            key[lane] = (static_cast<unsigned long long>(__float_as_uint(r.best)) << 32) | r.bi;
+        }
+    }
+    while (__ballot(walking)) {
+        uint32_t b = 0u, n = 0u;
+        if (walking) {
+            b = cstart[cell];
+            n = cstart[cell + 1] - b;
+            if (COUNT) { n_cell++; n_sph += n; }
+        }
+        const uint32_t incl = wave_scan_add(n);
+        const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+        const uint32_t start = incl - n;
+        const uint32_t off = b - start;   // reference of slot s of this ray: s + off
+        uint32_t carry = 0u;              // marker (owner + 1) of the last slot of the previous pass
+        for (uint32_t base = 0; base < total; base += 64u) {
+            mark[lane] = 0u;
+            lane_order();
+            if (n != 0u && start - base < 64u) mark[start - base] = lane + 1u;
+            lane_order();
+            const uint32_t m = max(wave_scan_max(mark[lane]), carry);
+            carry = __builtin_amdgcn_readlane(m, 63);
+            const uint32_t L = (m - 1u) & 63u;   // the slot's ray
+            const uint32_t offL = __shfl(off, int(L));
+            const uint32_t s = base + lane;
+            UTIL(1, s < total);
+            if (s < total) {
+                const uint32_t j = s + offL;
+                const float4 A = rayA[L], B = rayB[L], sp = rec[j];
+                const float rr = sp.w * sp.w;
+                const float ocx = A.x - sp.x, ocy = A.y - sp.y, ocz = A.z - sp.z;
+                const float bb = __builtin_fmaf(ocz, B.z, __builtin_fmaf(ocy, B.y, ocx * B.x));
+                const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - rr;
+                const float D = __builtin_fmaf(bb, bb, -(A.w * c));
+                if (D >= 0.0f && !behind(bb, c)) {
+                    UTIL(2, true);
+                    const float sq = sqrt_cr(D);
+                    float t = (-bb - sq) * B.w;
+                    if (!(t >= T_MIN)) t = (-bb + sq) * B.w;   // report t1 if t1 >= tmin, else t2
+                    if (t >= T_MIN) {
+                        const unsigned long long k = (static_cast<unsigned long long>(__float_as_uint(t)) << 32) | ids[j];
+                        __hip_atomic_fetch_min(&key[L], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                    }
+                }
+            }
+            lane_order();
+        }
+        if (walking) {
+            const unsigned long long k = key[lane];
+            r.best = __uint_as_float(uint32_t(k >> 32));
+            r.bi = uint32_t(k);
+            r.limit = cull_limit(P, r.best);
+            UTIL(0, true);
+            // DDA step (grid_walk): the axis whose boundary comes first, x before y before z on ties
+            const float tm = fminf(fminf(tx, ty), tz);
+            if (!(tm <= r.limit)) {
+                walking = false;   // the next cell starts beyond every closer candidate
+            } else {
+                const bool mx = tx == tm, my = !mx && ty == tm, mz = !mx && !my;
+                cx += mx ? sx : 0;
+                cy += my ? sy : 0;
+                cz += mz ? sz : 0;
+                if (uint32_t(cx) >= G.n[0] || uint32_t(cy) >= G.n[1] || uint32_t(cz) >= G.n[2]) {
+                    walking = false;
+                } else {
+                    cell += mx ? sx : my ? sy * int(G.n[0]) : sz * int(G.n[0] * G.n[1]);
+                    const int c = mx ? cx : my ? cy : cz, sg = mx ? sx : my ? sy : sz;
+                    const float csk = mx ? G.cs[0] : my ? G.cs[1] : G.cs[2];
+                    const float g0 = mx ? G.gmin[0] : my ? G.gmin[1] : G.gmin[2];
+                    const float ok = mx ? r.o.x : my ? r.o.y : r.o.z, ik = mx ? r.inv.x : my ? r.inv.y : r.inv.z;
+                    const float tnew = (__builtin_fmaf(float(c + (sg > 0 ? 1 : 0)), csk, g0) - ok) * ik;
+                    tx = mx ? tnew : tx;
+                    ty = my ? tnew : ty;
+                    tz = mz ? tnew : tz;
+                }
+            }
+        }
     }
 }
 
@@ -1183,7 +1355,8 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
                                           const uint32_t* __restrict__ leaf_ids,
                                           const float4* __restrict__ geom4, const float4* __restrict__ mat4,
                                           const BigTable big) {
-    constexpr bool LSUM = MODE == rt::MODE_HASH && (LAYOUT == LAYOUT_GRID || LAYOUT == LAYOUT_GRID_L2);
+    constexpr bool LSUM = MODE == rt::MODE_HASH &&
+                          (LAYOUT == LAYOUT_GRID || LAYOUT == LAYOUT_GRID_L2 || LAYOUT == LAYOUT_GRID_COOP);
     const uint32_t lane = lane_id();
     const Camera cam = load_camera(P);
     uint32_t st = ST_NEED_UNIT;
@@ -1232,7 +1405,12 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
         const uint32_t box0 = n_box;
         if (st == ST_TRACING) setup_ray(P, big, r, n_sph);
         STAMP(2);
-        if (st == ST_TRACING) walk<COUNT, LAYOUT>(P, nodes4, leaf4, leaf_ids, r, n_box, n_sph);
+        if constexpr (LAYOUT == LAYOUT_GRID_COOP) {   // every lane of the wave takes part (tracing or not)
+            grid_walk_coop<COUNT>(P, reinterpret_cast<const uint32_t*>(nodes4), leaf4, leaf_ids, r, st == ST_TRACING,
+                                  n_box, n_sph);
+        } else {
+            if (st == ST_TRACING) walk<COUNT, LAYOUT>(P, nodes4, leaf4, leaf_ids, r, n_box, n_sph);
+        }
         // the AABB gate of the winner only (winner_gated); the rare lanes whose winner fails it
         // get the contract's answer by a wave-cooperative gated brute force
         const unsigned long long regate =
@@ -1348,7 +1526,7 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
 
 // Grid kernel (ACCEL_GRID): the grid's cell offsets and references staged in LDS once per
 // persistent block: [references (float4) | reference ids | cell offsets | big-sphere table].
-template <bool COUNT, int MODE, bool IN_LDS>
+template <bool COUNT, int MODE, bool IN_LDS, bool COOP = false>
 __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace_grid_kernel(const rt::TraceParams P) {
     UTIL_INIT;
     PLACEMENT_RECORD(P);
@@ -1372,7 +1550,7 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
     for (uint32_t i = threadIdx.x; i < nc1; i += kTraceBlock) cst[i] = P.cell_start[i];
     const BigTable big = stage_big(P, lds + nr + n_id4 + n_cs4, threadIdx.x, kTraceBlock);
     __syncthreads();
-    lbvh_loop<COUNT, LAYOUT_GRID, MODE>(P, reinterpret_cast<const float4*>(cst), lds, ids,
+    lbvh_loop<COUNT, COOP ? LAYOUT_GRID_COOP : LAYOUT_GRID, MODE>(P, reinterpret_cast<const float4*>(cst), lds, ids,
                                         reinterpret_cast<const float4*>(P.geom),
                                         reinterpret_cast<const float4*>(P.mat), big);
 }
@@ -1521,6 +1699,9 @@ static const void* pick_mode(uint32_t accel, bool count) {
             return count ? RT_FN(rt_trace_top_kernel<true, MODE>) : RT_FN(rt_trace_top_kernel<false, MODE>);
         case ACCEL_GRID:
             return count ? RT_FN(rt_trace_grid_kernel<true, MODE, true>) : RT_FN(rt_trace_grid_kernel<false, MODE, true>);
+        case ACCEL_GRID_COOP:
+            return count ? RT_FN(rt_trace_grid_kernel<true, MODE, true, true>)
+                         : RT_FN(rt_trace_grid_kernel<false, MODE, true, true>);
         case ACCEL_GRID_GLOBAL:
             return count ? RT_FN(rt_trace_grid_kernel<true, MODE, false>)
                          : RT_FN(rt_trace_grid_kernel<false, MODE, false>);

@@ -23,8 +23,9 @@ LBVH_GLOBAL = 10   # test-only alias: accel LBVH, every node from L2 (options.re
 LBVH_OCT = 8       # test-only alias: accel LBVH, the tree's 8 octant copies in LDS (host trees) or the
                    # treelet (device trees) (options.reserved[1] = 8)
 GRID = 12          # test-only alias: the uniform grid (options.reserved[1] = 12)
-WALK_FORM = {LBVH_LDS1: 6, LBVH_GLOBAL: 10, LBVH_OCT: 8, GRID: 12}
-FORMS = [BRUTE, LBVH, LBVH_OCT, LBVH_LDS1, LBVH_GLOBAL]   # LBVH: the default form (the grid for host scenes)
+GRID_COOP = 14     # test-only alias: the uniform grid in LDS, wave-cooperative walk (options.reserved[1] = 14)
+WALK_FORM = {LBVH_LDS1: 6, LBVH_GLOBAL: 10, LBVH_OCT: 8, GRID: 12, GRID_COOP: 14}
+FORMS = [BRUTE, LBVH, LBVH_OCT, LBVH_LDS1, LBVH_GLOBAL, GRID_COOP]   # LBVH: the default form (the grid for host scenes)
 STREAM, COUNTER, HASH = 0, 1, 2
 
 
@@ -293,10 +294,11 @@ def test_grid_near_cull_slack_mixed_radii(rtvk, renderer, torch, oracle, builder
         for rng_mode in (STREAM, HASH):
             ra, ro, _ = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=rng_mode))
             for full in (None, "1"):
-                with env(RT_GRID_FULL_SLACK=full):
-                    a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH, rng_mode=rng_mode,
-                                         builder=builder)
-                assert_same(a, o, ra, ro)
+                for accel in ((LBVH, GRID_COOP) if builder is None else (LBVH,)):
+                    with env(RT_GRID_FULL_SLACK=full):
+                        a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=accel, rng_mode=rng_mode,
+                                             builder=builder)
+                    assert_same(a, o, ra, ro)
 
 
 @pytest.mark.parametrize("builder", [None, "gpu"])
@@ -322,7 +324,7 @@ def test_grid_lattice_axis_rays(rtvk, renderer, torch, oracle, builder):
         f[8:11] = cam
         f[12:15] = [look[k] - cam[k] for k in range(3)]
         ra, ro, _ = oracle.render(sc, rci, W, H)
-        for accel in (BRUTE, LBVH, GRID, LBVH_OCT, LBVH_GLOBAL):
+        for accel in (BRUTE, LBVH, GRID, GRID_COOP, LBVH_OCT, LBVH_GLOBAL):
             a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=accel, builder=builder)
             assert_same(a, o, ra, ro)
 
