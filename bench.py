@@ -172,6 +172,8 @@ WALK_NAMES = {   # rt_debug_launch_info form -> (kernel, walk)
     "grid-global": ("rt_trace_grid_kernel<grid from L2>", "uniform grid (3D DDA), from L2"),
     "grid-lds-coop": ("rt_trace_grid_kernel<grid in LDS, wave-cooperative>",
                       "uniform grid (3D DDA) staged in LDS, reference tests spread over the wave's lanes"),
+    "grid-global-coop": ("rt_trace_grid_kernel<grid from L2, wave-cooperative>",
+                         "uniform grid (3D DDA) from L2, reference loads and tests spread over the wave's lanes"),
 }
 
 

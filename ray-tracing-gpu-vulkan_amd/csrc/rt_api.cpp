@@ -777,11 +777,14 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
         // cameras within its pad radius
         accel = ctx->grid_bytes ? rt::ACCEL_GRID : rt::ACCEL_GRID_GLOBAL;
         lds = ctx->grid_bytes ? ctx->grid_bytes : rt::kBigLdsBytes;
-        // the wave-cooperative walk of the LDS grid: form 14, or RT_GRID_COOP=1
+        // the wave-cooperative walk: form 14, or RT_GRID_COOP=1
         const char* ce = std::getenv("RT_GRID_COOP");
-        if (accel == rt::ACCEL_GRID && (form == 14u || (form == 0u && ce && std::strcmp(ce, "1") == 0)) &&
+        const bool coop = form == 14u || (form == 0u && ce && std::strcmp(ce, "1") == 0);
+        if (coop && accel == rt::ACCEL_GRID &&
             ctx->grid_bytes + rt::kLaneSumLdsBytes + rt::kCoopLdsBytes <= kMaxLdsBytes)
             accel = rt::ACCEL_GRID_COOP;
+        else if (coop && accel == rt::ACCEL_GRID_GLOBAL)
+            accel = rt::ACCEL_GRID_GLOBAL_COOP;
     } else if (ctx->oct_bytes && (form == 0u || form == 8u)) {
         accel = rt::ACCEL_LBVH_OCT;
         lds = ctx->oct_bytes;
@@ -829,7 +832,8 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     P.nodes_oct = d.nodes_oct;
     P.treelet = d.treelet;
     P.treelet_count = d.treelet_count;
-    const bool grid_walk = accel == rt::ACCEL_GRID || accel == rt::ACCEL_GRID_GLOBAL || accel == rt::ACCEL_GRID_COOP;
+    const bool grid_walk = accel == rt::ACCEL_GRID || accel == rt::ACCEL_GRID_GLOBAL || accel == rt::ACCEL_GRID_COOP ||
+                           accel == rt::ACCEL_GRID_GLOBAL_COOP;
     if (grid_walk) {   // (cell_start also marks a walk)
         P.grid = d.grid;
         P.cell_start = d.cell_start;

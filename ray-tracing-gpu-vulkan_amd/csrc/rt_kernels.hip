@@ -1534,7 +1534,7 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
     if (!IN_LDS) {   // grids too big for LDS: offsets and references from L2 / HBM
         const BigTable big = stage_big(P, lds, threadIdx.x, kTraceBlock);
         __syncthreads();
-        lbvh_loop<COUNT, LAYOUT_GRID_L2, MODE>(P, reinterpret_cast<const float4*>(P.cell_start),
+        lbvh_loop<COUNT, COOP ? LAYOUT_GRID_COOP : LAYOUT_GRID_L2, MODE>(P, reinterpret_cast<const float4*>(P.cell_start),
                                             reinterpret_cast<const float4*>(P.grid_rec), P.grid_ids,
                                             reinterpret_cast<const float4*>(P.geom),
                                             reinterpret_cast<const float4*>(P.mat), big);
@@ -1702,6 +1702,9 @@ static const void* pick_mode(uint32_t accel, bool count) {
         case ACCEL_GRID_COOP:
             return count ? RT_FN(rt_trace_grid_kernel<true, MODE, true, true>)
                          : RT_FN(rt_trace_grid_kernel<false, MODE, true, true>);
+        case ACCEL_GRID_GLOBAL_COOP:
+            return count ? RT_FN(rt_trace_grid_kernel<true, MODE, false, true>)
+                         : RT_FN(rt_trace_grid_kernel<false, MODE, false, true>);
         case ACCEL_GRID_GLOBAL:
             return count ? RT_FN(rt_trace_grid_kernel<true, MODE, false>)
                          : RT_FN(rt_trace_grid_kernel<false, MODE, false>);

@@ -294,7 +294,7 @@ def test_grid_near_cull_slack_mixed_radii(rtvk, renderer, torch, oracle, builder
         for rng_mode in (STREAM, HASH):
             ra, ro, _ = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=rng_mode))
             for full in (None, "1"):
-                for accel in ((LBVH, GRID_COOP) if builder is None else (LBVH,)):
+                for accel in (LBVH, GRID_COOP):
                     with env(RT_GRID_FULL_SLACK=full):
                         a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=accel, rng_mode=rng_mode,
                                              builder=builder)
