@@ -172,10 +172,22 @@ __device__ __forceinline__ float4 lds_reload(const float4* p) {
     return make_float4(v.x, v.y, v.z, v.w);
 }
 
+// Launch parameters that a lane selects per lane, staged in LDS by every walk kernel before its
+// first barrier (stage_walk_params): the grid's (cell size, origin) per axis for the DDA step and
+// the two absolute cull slacks. Read with a per-lane LDS address (lgkmcnt wait only) instead of
+// the compiler's per-lane select of kernel-argument addresses and a global load, whose
+// vmcnt(0) wait also waited for every store and atomic the wave had in flight.
+__shared__ float2 s_walk_par[4];   // (cs[k], gmin[k]) k = 0..2, (cull_near_abs, cull_abs)
+__device__ __forceinline__ void stage_walk_params(const rt::TraceParams& P, uint32_t tid) {
+    if (tid < 3u) s_walk_par[tid] = make_float2(P.grid.cs[tid], P.grid.gmin[tid]);
+    if (tid == 3u) s_walk_par[3] = make_float2(P.cull_near_abs, P.cull_abs);
+}
+
 // Cull limit of a closest-so-far t: best + cull_abs + cull_rel best, with
 // the smaller absolute slack of grid walks for t <= cull_near_t (rt_api.cpp; -1 elsewhere).
 __device__ __forceinline__ float cull_limit(const rt::TraceParams& P, float t) {
-    const float abs_slack = t <= P.cull_near_t ? P.cull_near_abs : P.cull_abs;
+    const float* slack = reinterpret_cast<const float*>(&s_walk_par[3]);
+    const float abs_slack = slack[t <= P.cull_near_t ? 0 : 1];
     return fminf(__builtin_fmaf(t, P.cull_rel, t + abs_slack), 10000.0f);
 }
 
@@ -1027,9 +1039,9 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
         if (uint32_t(cx) >= G.n[0] || uint32_t(cy) >= G.n[1] || uint32_t(cz) >= G.n[2]) break;
         cell += mx ? dxc : my ? dyc : dzc;
         const int c = mx ? cx : my ? cy : cz, s = mx ? sx : my ? sy : sz;
-        const float csk = mx ? G.cs[0] : my ? G.cs[1] : G.cs[2], g0 = mx ? G.gmin[0] : my ? G.gmin[1] : G.gmin[2];
+        const float2 cg = s_walk_par[mx ? 0 : my ? 1 : 2];   // (cs[k], gmin[k])
         const float ok = mx ? r.o.x : my ? r.o.y : r.o.z, ik = mx ? r.inv.x : my ? r.inv.y : r.inv.z;
-        const float tnew = (__builtin_fmaf(float(c + (s > 0 ? 1 : 0)), csk, g0) - ok) * ik;
+        const float tnew = (__builtin_fmaf(float(c + (s > 0 ? 1 : 0)), cg.x, cg.y) - ok) * ik;
         tx = mx ? tnew : tx;
         ty = my ? tnew : ty;
         tz = mz ? tnew : tz;
@@ -1191,10 +1203,9 @@ __device__ __forceinline__ void grid_walk_coop(const rt::TraceParams& P, const u
                 } else {
                     cell += mx ? sx : my ? sy * int(G.n[0]) : sz * int(G.n[0] * G.n[1]);
                     const int c = mx ? cx : my ? cy : cz, sg = mx ? sx : my ? sy : sz;
-                    const float csk = mx ? G.cs[0] : my ? G.cs[1] : G.cs[2];
-                    const float g0 = mx ? G.gmin[0] : my ? G.gmin[1] : G.gmin[2];
+                    const float2 cg = s_walk_par[mx ? 0 : my ? 1 : 2];   // (cs[k], gmin[k])
                     const float ok = mx ? r.o.x : my ? r.o.y : r.o.z, ik = mx ? r.inv.x : my ? r.inv.y : r.inv.z;
-                    const float tnew = (__builtin_fmaf(float(c + (sg > 0 ? 1 : 0)), csk, g0) - ok) * ik;
+                    const float tnew = (__builtin_fmaf(float(c + (sg > 0 ? 1 : 0)), cg.x, cg.y) - ok) * ik;
                     tx = mx ? tnew : tx;
                     ty = my ? tnew : ty;
                     tz = mz ? tnew : tz;
@@ -1460,6 +1471,7 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
     PLACEMENT_RECORD(P);
     extern __shared__ float4 lds[];   // the big-sphere table only
     const BigTable big = stage_big(P, lds, threadIdx.x, kTraceBlock);
+    stage_walk_params(P, threadIdx.x);
     __syncthreads();
     lbvh_loop<COUNT, LAYOUT_GLOBAL, MODE>(P, reinterpret_cast<const float4*>(P.nodes),
                                           reinterpret_cast<const float4*>(P.leaf_geom), P.leaf_ids,
@@ -1519,6 +1531,7 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
     const float4* geom4 = reinterpret_cast<const float4*>(P.geom);
     const float4* mat4 = reinterpret_cast<const float4*>(P.mat);
     const BigTable big = stage_big(P, lds + base, threadIdx.x, kTraceBlock);
+    stage_walk_params(P, threadIdx.x);
     __syncthreads();
     lbvh_loop<COUNT, NOCT == 8 ? LAYOUT_OCT : LAYOUT_LDS1, MODE>(
         P, lds, lds + n_node4, reinterpret_cast<const uint32_t*>(lds + n_node4 + n_leaf4), geom4, mat4, big);
@@ -1533,6 +1546,7 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
     extern __shared__ float4 lds[];
     if (!IN_LDS) {   // grids too big for LDS: offsets and references from L2 / HBM
         const BigTable big = stage_big(P, lds, threadIdx.x, kTraceBlock);
+        stage_walk_params(P, threadIdx.x);
         __syncthreads();
         lbvh_loop<COUNT, COOP ? LAYOUT_GRID_COOP : LAYOUT_GRID_L2, MODE>(P, reinterpret_cast<const float4*>(P.cell_start),
                                             reinterpret_cast<const float4*>(P.grid_rec), P.grid_ids,
@@ -1549,6 +1563,7 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
     uint32_t* cst = reinterpret_cast<uint32_t*>(lds + nr + n_id4);
     for (uint32_t i = threadIdx.x; i < nc1; i += kTraceBlock) cst[i] = P.cell_start[i];
     const BigTable big = stage_big(P, lds + nr + n_id4 + n_cs4, threadIdx.x, kTraceBlock);
+    stage_walk_params(P, threadIdx.x);
     __syncthreads();
     lbvh_loop<COUNT, COOP ? LAYOUT_GRID_COOP : LAYOUT_GRID, MODE>(P, reinterpret_cast<const float4*>(cst), lds, ids,
                                         reinterpret_cast<const float4*>(P.geom),
@@ -1575,6 +1590,7 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
                                      __uint_as_float(int32_t(hit) >= 0 ? lbase + hit * 32u : hit));
     }
     const BigTable big = stage_big(P, lds + 2u * rt::kTreeletCap, threadIdx.x, kTraceBlock);
+    stage_walk_params(P, threadIdx.x);
     __syncthreads();
     lbvh_loop<COUNT, LAYOUT_TOP, MODE>(P, lds, reinterpret_cast<const float4*>(P.leaf_geom), P.leaf_ids,
                                        reinterpret_cast<const float4*>(P.geom),
