@@ -157,6 +157,8 @@ void make_octant_orders(const std::vector<rt::BvhNode>& n, std::vector<rt::BvhNo
 
 // LDS budget of the staged forms: 160 KiB per CU, one 1024-thread block per CU; 4 KiB kept free.
 constexpr size_t kMaxLdsBytes = 156 * 1024;
+// ... and of a form that must keep two 768-thread blocks per CU (static + dynamic LDS).
+constexpr size_t kTwoBlockLdsBytes = 78 * 1024;
 // The LDS walk's leaf words hold a leaf index in 10 bits (<= 4096 slots of 4) and an escape node
 // of the 8 copies in 19 bits.
 constexpr uint32_t kMaxLdsLeafSlots = 4096;
@@ -785,6 +787,16 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
             accel = rt::ACCEL_GRID_COOP;
         else if (coop && accel == rt::ACCEL_GRID_GLOBAL)
             accel = rt::ACCEL_GRID_GLOBAL_COOP;
+        // the LDS grid kernel also stages the winner's gate and shading records ({c, r} + the
+        // material record, 48 B per sphere) when two blocks per CU still fit;
+        // RT_GRID_REC=0: not (A/B)
+        const size_t rec_bytes = size_t(d.n_spheres) * 48u;
+        const char* re = std::getenv("RT_GRID_REC");
+        if (accel == rt::ACCEL_GRID && !(re && std::strcmp(re, "0") == 0) &&
+            ctx->grid_bytes + rec_bytes + rt::kLaneSumLdsBytes <= kTwoBlockLdsBytes) {
+            accel = rt::ACCEL_GRID_REC;
+            lds = ctx->grid_bytes + rec_bytes;
+        }
     } else if (ctx->oct_bytes && (form == 0u || form == 8u)) {
         accel = rt::ACCEL_LBVH_OCT;
         lds = ctx->oct_bytes;
@@ -833,7 +845,7 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     P.treelet = d.treelet;
     P.treelet_count = d.treelet_count;
     const bool grid_walk = accel == rt::ACCEL_GRID || accel == rt::ACCEL_GRID_GLOBAL || accel == rt::ACCEL_GRID_COOP ||
-                           accel == rt::ACCEL_GRID_GLOBAL_COOP;
+                           accel == rt::ACCEL_GRID_GLOBAL_COOP || accel == rt::ACCEL_GRID_REC;
     if (grid_walk) {   // (cell_start also marks a walk)
         P.grid = d.grid;
         P.cell_start = d.cell_start;

@@ -129,7 +129,7 @@ struct DeviceScene {
 // L2) is the A/B reference of TOP (options.reserved[1] = 10).
 enum : uint32_t { ACCEL_BRUTE = 1, ACCEL_LBVH_GLOBAL = 2, ACCEL_LBVH_LDS = 3, ACCEL_LBVH_OCT = 4,
                   ACCEL_LBVH_TOP = 5, ACCEL_GRID = 6, ACCEL_GRID_GLOBAL = 7, ACCEL_GRID_COOP = 8,
-                  ACCEL_GRID_GLOBAL_COOP = 9, ACCEL_COUNT = 10 };
+                  ACCEL_GRID_GLOBAL_COOP = 9, ACCEL_GRID_REC = 10, ACCEL_COUNT = 11 };
 
 // Random stream layout of a launch (template parameter of the trace kernels).
 //   STREAM: the reference's per-pixel LCG stream (random.glsl), or with rng_counter the TEA

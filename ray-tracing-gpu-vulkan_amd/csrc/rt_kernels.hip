@@ -1224,10 +1224,13 @@ __device__ __forceinline__ void grid_walk_coop(const rt::TraceParams& P, const u
 // (iii)), so W was tested and R <= W: R = W. If R fails the gate (a rounding corner: the quadratic
 // reports a hit whose ray misses the box; ~1 segment in 7e7 on config 3), the segment's answer is
 // recomputed by the contract's rule itself: gated brute force (regate_brute).
+// REC: geom4 holds {cx, cy, cz, r} records staged in LDS (rt_trace_grid_kernel<..., REC>), else
+// the HBM GeomRec array {cx, cy, cz, r^2} with the radii in P.radius.
+template <bool REC>
 __device__ __forceinline__ bool winner_gated(const rt::TraceParams& P, const float4* __restrict__ geom4, const Ray& r) {
     if (r.bi == 0xffffffffu) return true;
     const float4 g = geom4[r.bi];
-    return aabb_hit(g.x, g.y, g.z, P.radius[r.bi], r.o, r.inv);
+    return aabb_hit(g.x, g.y, g.z, REC ? g.w : P.radius[r.bi], r.o, r.inv);
 }
 
 // Gated brute force for the lanes in `need` (wave-uniform), one ray at a time with the whole wave:
@@ -1360,7 +1363,7 @@ __device__ __forceinline__ void walk(const rt::TraceParams& P, const float4* __r
 // longest walk ends. Stamp slots: 0 loop head, 4 sample start, 5 refill, 6 block fetch, 1 ray
 // setup (big spheres), 2 LBVH walk, 3 shading, 7 other.
 // ---------------------------------------------------------------------------------------------
-template <bool COUNT, int LAYOUT, int MODE>
+template <bool COUNT, int LAYOUT, int MODE, bool REC = false>
 __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4* __restrict__ nodes4,
                                           const float4* __restrict__ leaf4,
                                           const uint32_t* __restrict__ leaf_ids,
@@ -1425,8 +1428,9 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
         // the AABB gate of the winner only (winner_gated); the rare lanes whose winner fails it
         // get the contract's answer by a wave-cooperative gated brute force
         const unsigned long long regate =
-            __ballot(st == ST_TRACING && (P.force_regate || !winner_gated(P, geom4, r)));
-        if (__builtin_expect(regate != 0ull, 0)) regate_brute<COUNT>(P, geom4, lane, regate, r);
+            __ballot(st == ST_TRACING && (P.force_regate || !winner_gated<REC>(P, geom4, r)));
+        if (__builtin_expect(regate != 0ull, 0))
+            regate_brute<COUNT>(P, reinterpret_cast<const float4*>(P.geom), lane, regate, r);
         if (COUNT && st == ST_TRACING) {   // walk-length histogram (diagnostic, COUNT builds only)
             const uint32_t len = min(n_box - box0, 63u);
             atomicAdd(&P.counters->walk_hist[r.bi != 0xffffffffu ? 1 : 0][len], 1ull);
@@ -1539,7 +1543,7 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
 
 // Grid kernel (ACCEL_GRID): the grid's cell offsets and references staged in LDS once per
 // persistent block: [references (float4) | reference ids | cell offsets | big-sphere table].
-template <bool COUNT, int MODE, bool IN_LDS, bool COOP = false>
+template <bool COUNT, int MODE, bool IN_LDS, bool COOP = false, bool REC = false>
 __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace_grid_kernel(const rt::TraceParams P) {
     UTIL_INIT;
     PLACEMENT_RECORD(P);
@@ -1564,6 +1568,20 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
     for (uint32_t i = threadIdx.x; i < nc1; i += kTraceBlock) cst[i] = P.cell_start[i];
     const BigTable big = stage_big(P, lds + nr + n_id4 + n_cs4, threadIdx.x, kTraceBlock);
     stage_walk_params(P, threadIdx.x);
+    if (REC) {   // the winner's gate and shading records in LDS too: {cx, cy, cz, r} + 2 x MatRec float4
+        float4* srec = lds + nr + n_id4 + n_cs4 + rt::kBigLdsBytes / 16u;
+        float4* smat = srec + P.n_spheres;
+        const float4* mat4 = reinterpret_cast<const float4*>(P.mat);
+        for (uint32_t i = threadIdx.x; i < P.n_spheres; i += kTraceBlock) {
+            const rt::GeomRec g = P.geom[i];
+            srec[i] = make_float4(g.cx, g.cy, g.cz, P.radius[i]);
+            smat[2 * i] = mat4[2 * i];
+            smat[2 * i + 1] = mat4[2 * i + 1];
+        }
+        __syncthreads();
+        lbvh_loop<COUNT, LAYOUT_GRID, MODE, true>(P, reinterpret_cast<const float4*>(cst), lds, ids, srec, smat, big);
+        return;
+    }
     __syncthreads();
     lbvh_loop<COUNT, COOP ? LAYOUT_GRID_COOP : LAYOUT_GRID, MODE>(P, reinterpret_cast<const float4*>(cst), lds, ids,
                                         reinterpret_cast<const float4*>(P.geom),
@@ -1718,6 +1736,9 @@ static const void* pick_mode(uint32_t accel, bool count) {
         case ACCEL_GRID_COOP:
             return count ? RT_FN(rt_trace_grid_kernel<true, MODE, true, true>)
                          : RT_FN(rt_trace_grid_kernel<false, MODE, true, true>);
+        case ACCEL_GRID_REC:
+            return count ? RT_FN(rt_trace_grid_kernel<true, MODE, true, false, true>)
+                         : RT_FN(rt_trace_grid_kernel<false, MODE, true, false, true>);
         case ACCEL_GRID_GLOBAL_COOP:
             return count ? RT_FN(rt_trace_grid_kernel<true, MODE, false, true>)
                          : RT_FN(rt_trace_grid_kernel<false, MODE, false, true>);

@@ -212,7 +212,7 @@ class Renderer:
         v = (ctypes.c_uint32 * 4)()
         check(self._lib.rt_debug_launch_info(self._ctx, v))
         forms = {1: "brute", 2: "lbvh-global", 3: "lbvh-lds", 4: "lbvh-octant-lds", 5: "lbvh-treelet", 6: "grid-lds", 7: "grid-global",
-                 8: "grid-lds-coop", 9: "grid-global-coop"}
+                 8: "grid-lds-coop", 9: "grid-global-coop", 10: "grid-lds"}
         return {"chunks": int(v[0]), "form": forms.get(int(v[1]), str(v[1])), "lds_bytes": int(v[2]),
                 "cus": int(v[3])}
 
