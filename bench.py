@@ -160,7 +160,8 @@ def pmc_record(key: str, sha: str) -> dict:
         return {"pmc": f"no PMC record for {key} in profiles/pmc.json"}
     if rec.get("lib_sha256") != sha:
         return {"pmc": f"stale: profiles/pmc.json {key} measured on build {rec.get('lib_sha256')}, this build is {sha}"}
-    return {k: rec[k] for k in ("valu_issue_busy", "lane_util", "hbm_bytes_per_launch", "kernel_ms") if k in rec}
+    return {k: rec[k] for k in ("valu_issue_busy", "lane_util", "hbm_bytes_per_launch", "kernel_ms", "l2_hit_rate")
+            if k in rec}
 
 
 WALK_NAMES = {   # rt_debug_launch_info form -> (kernel, walk)
@@ -198,10 +199,15 @@ def roofline_block(cs, scale, form: str, kernel_ms: float, step_ms: float, n_gpu
                            f"(SURVEY.md 8(d)); counts from the instrumented build of the same kernel"
                            + (f", x{scale:g} to the frame's spp" if scale != 1 else "")),
             "lib_sha256": sha}
-    roof.update({k: v for k, v in pmc.items() if k in ("valu_issue_busy", "lane_util", "pmc")})
+    roof.update({k: v for k, v in pmc.items() if k in ("valu_issue_busy", "lane_util", "pmc", "l2_hit_rate")})
     if "valu_issue_busy" in pmc and "lane_util" in pmc:
         # every executed lane-op (traversal control, shading, sampling included) against peak
         roof["valu_lane_frac"] = round(pmc["valu_issue_busy"] * pmc["lane_util"], 4)
+    if pmc.get("hbm_bytes_per_launch") and kernel_ms > 0:   # HBM GB/s against 8 TB/s
+        gbs = pmc["hbm_bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9
+        roof["hbm"] = {"achieved": round(gbs, 1), "peak": 8000.0 * n_gpus, "unit": "GB/s",
+                       "frac": round(gbs / (8000.0 * n_gpus), 5),
+                       "basis": "PMC 2 x FETCH_SIZE + WRITE_SIZE per launch / the launch's duration"}
     lds_bytes = (cs.box_tests * bytes_step + cs.sphere_tests * BYTES_PER_SPHERE_TEST) * scale
     lds_tbps = lds_bytes / (kernel_ms * 1e-3) / 1e12 if kernel_ms > 0 else 0.0
     roof["lds"] = {"achieved": round(lds_tbps, 3), "peak": round(LDS_PEAK_TBPS * n_gpus, 1), "unit": "TB/s",

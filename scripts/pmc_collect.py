@@ -9,7 +9,8 @@ build is excluded), per dispatch, median over dispatches:
   lane_util       = SQ_THREAD_CYCLES_VALU / (64 x SQ_INSTS_VALU): active lanes per VALU issue
   hbm_bytes_per_launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB counters; gfx950 FETCH_SIZE reports half
                     of wide coalesced reads, MI355X_MICROARCH.md §HBM: doubled)
-Usage: pmc_collect.py KEY LIB_SO VALU_DIR FETCH_DIR WRITE_DIR [SQ_DIR] [OUT_JSON]"""
+  l2_hit_rate     = TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum) (MI355X_MICROARCH.md §L2), from --tcc DIR
+Usage: pmc_collect.py KEY LIB_SO VALU_DIR FETCH_DIR WRITE_DIR [SQ_DIR] [--tcc TCC_DIR] [OUT_JSON]"""
 import csv
 import glob
 import hashlib
@@ -40,6 +41,11 @@ def dispatches(d):
 
 
 def main():
+    tcc = None
+    if "--tcc" in sys.argv:
+        i = sys.argv.index("--tcc")
+        tcc = sys.argv[i + 1]
+        del sys.argv[i:i + 2]
     key, lib, vdir, fdir, wdir = sys.argv[1:6]
     sqdir = sys.argv[6] if len(sys.argv) > 6 and not sys.argv[6].endswith(".json") else None
     out = Path(sys.argv[-1]) if sys.argv[-1].endswith(".json") else Path("profiles/pmc.json")
@@ -67,8 +73,16 @@ def main():
                 vals = [e[c] for e in s if c in e]
                 if vals:
                     rec[c] = statistics.median(vals)
+    if tcc:
+        t = [e for e in dispatches(tcc) if "TCC_HIT_sum" in e and "TCC_MISS_sum" in e]
+        if t:
+            hits = statistics.median(e["TCC_HIT_sum"] for e in t)
+            miss = statistics.median(e["TCC_MISS_sum"] for e in t)
+            rec["l2_hit_rate"] = round(hits / max(1.0, hits + miss), 4)
+            rec["tcc_hit"], rec["tcc_miss"] = hits, miss
     rec["note"] = ("busy = SQ_INSTS_VALU x 2 cyc / (1024 SIMD x 2.4 GHz x duration); lane_util = "
-                   "SQ_THREAD_CYCLES_VALU / (64 x SQ_INSTS_VALU); hbm = 2 x FETCH_SIZE + WRITE_SIZE")
+                   "SQ_THREAD_CYCLES_VALU / (64 x SQ_INSTS_VALU); hbm = 2 x FETCH_SIZE + WRITE_SIZE; "
+                   "l2_hit_rate = TCC_HIT_sum / (TCC_HIT_sum + TCC_MISS_sum)")
     data = json.loads(out.read_text()) if out.exists() else {}
     data[key] = rec
     out.write_text(json.dumps(data, indent=1) + "\n")
