@@ -451,7 +451,7 @@ __global__ void __launch_bounds__(kBlock) k_grid_refs(const Sphere* __restrict__
                 const uint32_t c = (z * g.n[1] + y) * g.n[0] + x;
                 const uint32_t j = atomicAdd(&cnt[c], 1u);   // FILL: cnt holds each cell's next slot
                 if (FILL) {
-                    rec[j] = GeomRec{s.x, s.y, s.z, s.w};
+                    rec[j] = GeomRec{s.x, s.y, s.z, s.w * s.w};   // r^2 (rt_grid.h)
                     ids[j] = i;
                 }
             }

@@ -105,7 +105,7 @@ bool build_grid_host(const Sphere* sph, uint32_t n, const std::vector<uint32_t>&
                             if (++refs > max_refs) return false;
                         } else {
                             const uint32_t j = fill[c]++;
-                            out.rec[j] = GeomRec{g.x, g.y, g.z, g.w};
+                            out.rec[j] = GeomRec{g.x, g.y, g.z, g.w * g.w};   // r^2 (rt_grid.h)
                             out.ids[j] = i;
                         }
                     }

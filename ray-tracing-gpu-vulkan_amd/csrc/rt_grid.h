@@ -14,7 +14,7 @@ namespace rt {
 struct HostGrid {
     GridInfo info{};
     std::vector<uint32_t> cell_start;   // n_cells + 1 offsets into the reference lists
-    std::vector<GeomRec> rec;           // per reference: center, RADIUS (cell-major, index order)
+    std::vector<GeomRec> rec;           // per reference: center, r^2 (cell-major, index order; r*r in binary32, test1)
     std::vector<uint32_t> ids;          // per reference: sphere index
 };
 

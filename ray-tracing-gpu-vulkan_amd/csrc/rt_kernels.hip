@@ -239,11 +239,14 @@ __device__ __forceinline__ void test4(const float4 s0, const float4 s1, const fl
     }
 }
 
-// One sphere (a grid cell's reference): test4's arithmetic for a single record.
-__device__ __forceinline__ void test1(const float4 sp, const uint32_t* __restrict__ id_at, V3 o, V3 d, V3 inv,
+// One sphere (a grid cell's reference {cx, cy, cz, r^2}): test4's arithmetic for a single record,
+// with r*r precomputed by the grid build (the same binary32 product). IdAt yields the sphere id
+// when a candidate needs it (an LDS read, or a value loaded with the record from L2).
+template <typename IdAt>
+__device__ __forceinline__ void test1(const float4 sp, IdAt id_at, V3 o, V3 d, V3 inv,
                                       float a, float ia, float& best, uint32_t& bi, float& limit,
                                       const rt::TraceParams& P) {
-    const float rr = sp.w * sp.w;
+    const float rr = sp.w;
     const float ocx = o.x - sp.x, ocy = o.y - sp.y, ocz = o.z - sp.z;
     const float b = __builtin_fmaf(ocz, d.z, __builtin_fmaf(ocy, d.y, ocx * d.x));
     const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - rr;
@@ -254,7 +257,7 @@ __device__ __forceinline__ void test1(const float4 sp, const uint32_t* __restric
         float t = (-b - sq) * ia;
         if (!(t >= T_MIN)) t = (-b + sq) * ia;     // report t1 if t1 >= tmin, else t2
         if (t >= T_MIN && t <= best) {
-            const uint32_t id = *id_at;
+            const uint32_t id = id_at();
             if (t < best || id < bi) {   // AABB gate deferred to the segment's winner (winner_gated)
                 best = t;
                 bi = id;
@@ -641,10 +644,21 @@ __device__ __forceinline__ void sample_end(const rt::TraceParams& P, Path& ps, c
 // (`fresh`): the scattered and the camera direction share one normalisation, and the loop head's
 // sample start runs only for units just taken. Returns true when the lane traces again (o, d hold
 // the next ray), false when its unit's samples are done.
+// The hit sphere's records shade() reads: its geometry record and its two material records.
+struct HitRec {
+    float4 g, m0, m1;
+};
+
+__device__ __forceinline__ HitRec load_hit(const float4* __restrict__ geom4, const float4* __restrict__ mat4,
+                                           uint32_t bi) {
+    return HitRec{geom4[bi], mat4[2 * bi], mat4[2 * bi + 1]};
+}
+
+// hr: the records of sphere bi (load_hit), loaded by the caller so that they can travel with the
+// winner gate's loads (lbvh_loop); unused on a miss.
 template <int MODE, bool LSUM>
-__device__ __forceinline__ bool shade(const rt::TraceParams& P, const Camera& cam, const float4* __restrict__ geom4,
-                                      const float4* __restrict__ mat4, Path& ps, uint32_t bi,
-                                      float best, V3& o, V3& d, bool& fresh) {
+__device__ __forceinline__ bool shade_rec(const rt::TraceParams& P, const Camera& cam, const HitRec& hr, Path& ps,
+                                          uint32_t bi, float best, V3& o, V3& d, bool& fresh) {
     V3 att;
     bool scatter = false;
     V3 sd = v3(0.0f, 0.0f, 0.0f);
@@ -657,9 +671,9 @@ __device__ __forceinline__ bool shade(const rt::TraceParams& P, const Camera& ca
         UTIL(10, true);
         p = v3(__builtin_fmaf(best, d.x, o.x), __builtin_fmaf(best, d.y, o.y),
                __builtin_fmaf(best, d.z, o.z));
-        const float4 gc4 = geom4[bi];
-        const float4 m0 = mat4[2 * bi];
-        const float4 m1 = mat4[2 * bi + 1];
+        const float4 gc4 = hr.g;
+        const float4 m0 = hr.m0;
+        const float4 m1 = hr.m1;
         const uint32_t tt = __float_as_uint(m1.w);
         const uint32_t mtype = tt & 0xffu, ttype = (tt >> 8) & 0xffu;
         const V3 outward = normalize(sub(p, v3(gc4.x, gc4.y, gc4.z)));
@@ -729,6 +743,15 @@ __device__ __forceinline__ bool shade(const rt::TraceParams& P, const Camera& ca
     return more;
 }
 
+template <int MODE, bool LSUM>
+__device__ __forceinline__ bool shade(const rt::TraceParams& P, const Camera& cam, const float4* __restrict__ geom4,
+                                      const float4* __restrict__ mat4, Path& ps, uint32_t bi,
+                                      float best, V3& o, V3& d, bool& fresh) {
+    HitRec hr{};
+    if (bi != 0xffffffffu) hr = load_hit(geom4, mat4, bi);
+    return shade_rec<MODE, LSUM>(P, cam, hr, ps, bi, best, o, d, fresh);
+}
+
 
 // Finished unit: its chain length (traced segments) feeds the next launch's hand-out order.
 __device__ __forceinline__ void record_tile_cost(const rt::TraceParams& P, const Path& ps) {
@@ -745,6 +768,9 @@ __device__ __forceinline__ void record_tile_cost(const rt::TraceParams& P, const
 // block per CU at 4 waves per SIMD (98 VGPRs), although the 80-VGPR budget spills ~31 VGPRs
 // outside the walk loop; 8 waves per SIMD (64 VGPRs) spill more and took 180 ms; blocks whose
 // wave count is not a multiple of 4 (640, 896 threads) leave SIMDs unevenly loaded (+50 %).
+#ifndef RT_FUSE_GATE_LOADS
+#define RT_FUSE_GATE_LOADS 1
+#endif
 #ifndef RT_BRUTE_WAVES_PER_SIMD
 #define RT_BRUTE_WAVES_PER_SIMD 6
 #endif
@@ -1015,17 +1041,28 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
         if (COUNT) n_cell++;
         uint32_t j = b;
         if (PAIRS) {   // references from L2: two at a time (two record loads in flight; config 5 -3.5 %)
+          // the ids are loaded with the records (one L2 round trip instead of a second, dependent
+          // one for every candidate that passes the t test)
           for (; j + 1 < e; j += 2) {
             UTIL(1, true);
             const float4 s0 = rec[j], s1 = rec[j + 1];
-            test1(s0, ids + j, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
-            test1(s1, ids + j + 1, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
+            const uint32_t i0 = ids[j], i1 = ids[j + 1];
+            test1(s0, [&] { return i0; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
+            test1(s1, [&] { return i1; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
             if (COUNT) n_sph += 2;
+          }
+          if (j < e) {
+            UTIL(1, true);
+            const float4 s0 = rec[j];
+            const uint32_t i0 = ids[j];
+            test1(s0, [&] { return i0; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
+            if (COUNT) n_sph++;
+            ++j;
           }
         }
         for (; j < e; ++j) {   // from LDS one at a time (pairs measured 1 % slower there)
             UTIL(1, true);
-            test1(rec[j], ids + j, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
+            test1(rec[j], [&] { return ids[j]; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
             if (COUNT) n_sph++;
         }
         UTIL(0, true);
@@ -1165,7 +1202,7 @@ __device__ __forceinline__ void grid_walk_coop(const rt::TraceParams& P, const u
             if (s < total) {
                 const uint32_t j = s + offL;
                 const float4 A = rayA[L], B = rayB[L], sp = rec[j];
-                const float rr = sp.w * sp.w;
+                const float rr = sp.w;   // grid record: r^2
                 const float ocx = A.x - sp.x, ocy = A.y - sp.y, ocz = A.z - sp.z;
                 const float bb = __builtin_fmaf(ocz, B.z, __builtin_fmaf(ocy, B.y, ocx * B.x));
                 const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - rr;
@@ -1426,11 +1463,29 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
             if (st == ST_TRACING) walk<COUNT, LAYOUT>(P, nodes4, leaf4, leaf_ids, r, n_box, n_sph);
         }
         // the AABB gate of the winner only (winner_gated); the rare lanes whose winner fails it
-        // get the contract's answer by a wave-cooperative gated brute force
+        // get the contract's answer by a wave-cooperative gated brute force. The winner's shading
+        // records are loaded with the gate's (one round trip to L2 per segment, not two).
+        HitRec hr{};
+#if RT_FUSE_GATE_LOADS
+        float rad = 0.0f;
+        if (st == ST_TRACING && r.bi != 0xffffffffu) {
+            hr = load_hit(geom4, mat4, r.bi);
+            rad = REC ? hr.g.w : P.radius[r.bi];
+        }
+        const unsigned long long regate = __ballot(
+            st == ST_TRACING && (P.force_regate || (r.bi != 0xffffffffu && !aabb_hit(hr.g.x, hr.g.y, hr.g.z, rad, r.o,
+                                                                                       r.inv))));
+        if (__builtin_expect(regate != 0ull, 0)) {
+            regate_brute<COUNT>(P, reinterpret_cast<const float4*>(P.geom), lane, regate, r);
+            if (((regate >> lane) & 1ull) && r.bi != 0xffffffffu) hr = load_hit(geom4, mat4, r.bi);
+        }
+#else
         const unsigned long long regate =
             __ballot(st == ST_TRACING && (P.force_regate || !winner_gated<REC>(P, geom4, r)));
         if (__builtin_expect(regate != 0ull, 0))
             regate_brute<COUNT>(P, reinterpret_cast<const float4*>(P.geom), lane, regate, r);
+        if (st == ST_TRACING && r.bi != 0xffffffffu) hr = load_hit(geom4, mat4, r.bi);
+#endif
         if (COUNT && st == ST_TRACING) {   // walk-length histogram (diagnostic, COUNT builds only)
             const uint32_t len = min(n_box - box0, 63u);
             atomicAdd(&P.counters->walk_hist[r.bi != 0xffffffffu ? 1 : 0][len], 1ull);
@@ -1444,7 +1499,7 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
         bool fresh = false;   // a sample started inside shade()
         if (st == ST_TRACING) {
             ps.segs++;
-            if (!shade<MODE, LSUM>(P, cam, geom4, mat4, ps, r.bi, r.best, r.o, r.d, fresh)) {
+            if (!shade_rec<MODE, LSUM>(P, cam, hr, ps, r.bi, r.best, r.o, r.d, fresh)) {
                 // The unit's last sample ended: finish it here, and the lane asks for a unit at
                 // the top of the next iteration.
                 finish_unit<MODE, LSUM>(P, ps);
