@@ -25,6 +25,11 @@ using namespace rtd;
 
 namespace {
 
+// Code shape switch (1 = shipped; 0 builds the previous form for A/B timing): the winner's
+// shading records loaded with its gate.
+#ifndef RT_FUSE_GATE_LOADS
+#define RT_FUSE_GATE_LOADS 1
+#endif
 constexpr float T_MIN = 0.001f;               // shader.rgen:75
 constexpr float T_MAX_SUCC = 0x1.388002p+13f; // successor of 10000.0f (shader.rgen:26): a report
                                               // at exactly tMax is accepted, so compare with '<'.
@@ -241,8 +246,9 @@ __device__ __forceinline__ void test4(const float4 s0, const float4 s1, const fl
 
 // One sphere (a grid cell's reference {cx, cy, cz, r^2}): test4's arithmetic for a single record,
 // with r*r precomputed by the grid build (the same binary32 product). IdAt yields the sphere id
-// when a candidate needs it (an LDS read, or a value loaded with the record from L2).
-template <typename IdAt>
+// when a candidate needs it (an LDS read, or a value loaded with the record from L2); ID_READY:
+// the id is already in a register, so the two acceptance tests fold into one branch.
+template <bool ID_READY = false, typename IdAt>
 __device__ __forceinline__ void test1(const float4 sp, IdAt id_at, V3 o, V3 d, V3 inv,
                                       float a, float ia, float& best, uint32_t& bi, float& limit,
                                       const rt::TraceParams& P) {
@@ -256,7 +262,14 @@ __device__ __forceinline__ void test1(const float4 sp, IdAt id_at, V3 o, V3 d, V
         const float sq = sqrt_cr(D);
         float t = (-b - sq) * ia;
         if (!(t >= T_MIN)) t = (-b + sq) * ia;     // report t1 if t1 >= tmin, else t2
-        if (t >= T_MIN && t <= best) {
+        if (ID_READY) {
+            const uint32_t id = id_at();
+            if ((t >= T_MIN) & (t <= best) & ((t < best) | (id < bi))) {   // one predicate, one branch
+                best = t;
+                bi = id;
+                limit = cull_limit(P, t);
+            }
+        } else if (t >= T_MIN && t <= best) {
             const uint32_t id = id_at();
             if (t < best || id < bi) {   // AABB gate deferred to the segment's winner (winner_gated)
                 best = t;
@@ -768,9 +781,6 @@ __device__ __forceinline__ void record_tile_cost(const rt::TraceParams& P, const
 // block per CU at 4 waves per SIMD (98 VGPRs), although the 80-VGPR budget spills ~31 VGPRs
 // outside the walk loop; 8 waves per SIMD (64 VGPRs) spill more and took 180 ms; blocks whose
 // wave count is not a multiple of 4 (640, 896 threads) leave SIMDs unevenly loaded (+50 %).
-#ifndef RT_FUSE_GATE_LOADS
-#define RT_FUSE_GATE_LOADS 1
-#endif
 #ifndef RT_BRUTE_WAVES_PER_SIMD
 #define RT_BRUTE_WAVES_PER_SIMD 6
 #endif
@@ -1047,15 +1057,15 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
             UTIL(1, true);
             const float4 s0 = rec[j], s1 = rec[j + 1];
             const uint32_t i0 = ids[j], i1 = ids[j + 1];
-            test1(s0, [&] { return i0; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
-            test1(s1, [&] { return i1; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
+            test1<true>(s0, [&] { return i0; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
+            test1<true>(s1, [&] { return i1; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
             if (COUNT) n_sph += 2;
           }
           if (j < e) {
             UTIL(1, true);
             const float4 s0 = rec[j];
             const uint32_t i0 = ids[j];
-            test1(s0, [&] { return i0; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
+            test1<true>(s0, [&] { return i0; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
             if (COUNT) n_sph++;
             ++j;
           }
