@@ -265,6 +265,10 @@ int rt_debug_walk_hist(rt_context* ctx, uint64_t* out128);
  * (0..64) of the wave tracing in that iteration (the persistent kernel's lane occupancy), then
  * three s_memrealtime stamps (100 MHz): first wave start, pixel queue dry, last wave exit. */
 int rt_debug_lane_hist(rt_context* ctx, uint64_t* out68);
+/* Diagnostic: tail steals of ctx's last instrumented launch (options.reserved[0] & 1;
+ * RT_RNG_SAMPLE_HASH: once the work queue is empty, an idle lane takes half of the samples its
+ * wave's busiest lane has not started). */
+int rt_debug_steals(rt_context* ctx, uint64_t* out);
 /* Diagnostic: per 8x8 tile of ctx's last LBVH launch, the traced segments of its most expensive
  * pixel (the key its next launch over the same band geometry hands tiles out by, longest
  * first); *count = tiles (ceil(W/8) x ceil(H/8), row-major), 0 before the first launch. */

@@ -1110,6 +1110,16 @@ int rt_debug_lane_hist(rt_context* ctx, uint64_t* out68) {
     return RT_OK;
 }
 
+int rt_debug_steals(rt_context* ctx, uint64_t* out) {
+    if (!ctx || !out) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    DeviceGuard g(ctx->device);
+    if (ctx->ev_valid) RT_HIP(hipEventSynchronize(ctx->ev_last));
+    rt::Counters c;
+    RT_HIP(hipMemcpy(&c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
+    *out = c.steals;
+    return RT_OK;
+}
+
 // Diagnostic export: walk-length histogram of the last COUNT launch (2 x 64 bins: miss, hit).
 int rt_debug_walk_hist(rt_context* ctx, uint64_t* out128) {
     if (!ctx || !out128) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");

@@ -167,6 +167,7 @@ struct Counters {
     unsigned long long stamp[8];   // diagnostic builds only (-DRT_STAMPS): cycles per phase
     unsigned long long util[2 * 16];   // diagnostic builds only (-DRT_UTIL): per code point k, wave
                                        // passes [2k] and active lanes summed over them [2k + 1]
+    unsigned long long steals;     // counter-based stream: tail steals (rt_kernels.hip steal_tail)
 };
 
 // Kernel launch parameters (passed by value as the kernel argument).

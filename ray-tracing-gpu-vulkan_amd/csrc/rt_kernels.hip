@@ -27,6 +27,9 @@ namespace {
 
 // Code shape switch (1 = shipped; 0 builds the previous form for A/B timing): the winner's
 // shading records loaded with its gate.
+#ifndef RT_TAIL_STEAL
+#define RT_TAIL_STEAL 1
+#endif
 #ifndef RT_FUSE_GATE_LOADS
 #define RT_FUSE_GATE_LOADS 1
 #endif
@@ -477,9 +480,46 @@ __device__ __forceinline__ void begin_unit(const rt::TraceParams& P, Path& ps, u
     }
 }
 
-template <int MODE>
+// Tail stealing (counter-based stream only: any lane may run any sample of a pixel). Once the
+// work queue is exhausted, a lane without work takes the upper half of the samples not yet started
+// by the wave's lane with the most left (ties: lowest lane), one steal per call (one loop
+// iteration), while the victim has at least 2 kStealMin left. The wave's last units are thus shared by its idle
+// lanes instead of ending at the longest one; chunk sums are integers, so the split changes no bit.
+constexpr uint32_t kStealMin = 4;
+
+template <bool COUNT>
+__device__ __forceinline__ void steal_tail(const rt::TraceParams& P, uint32_t lane, uint32_t& st, Path& ps) {
+    const unsigned long long idle = __ballot(st == ST_RETIRED);
+    if (!idle) return;
+    const uint32_t rem = st == ST_TRACING ? ps.s_end - ps.s - 1u : st == ST_NEED_SAMPLE ? ps.s_end - ps.s : 0u;
+    uint32_t key = (min(rem, (1u << 25) - 1u) << 6) | (63u - lane);
+    for (int off = 32; off > 0; off >>= 1) key = max(key, (uint32_t)__shfl_xor(key, off));
+    const uint32_t vrem = key >> 6;
+    if (vrem < 2u * kStealMin) return;   // wave-uniform
+    const int v = int(63u - (key & 63u));
+    const int th = __ffsll(idle) - 1;
+    const uint32_t k = vrem / 2u;
+    const uint32_t vend = __shfl(ps.s_end, v), vpx = __shfl(ps.px, v), vseed = __shfl(ps.pixel_seed, v);
+    if (int(lane) == v) ps.s_end -= k;
+    if (COUNT && lane == 0) atomicAdd(&P.counters->steals, 1ull);
+    if (int(lane) == th) {
+        ps.px = vpx;
+        ps.pixel_seed = vseed;
+        ps.seed = vseed;
+        ps.s = vend - k;
+        ps.s_end = vend;
+        ps.segs = 0;
+        ps.qx = ps.qy = ps.qz = 0u;
+        st = ST_NEED_SAMPLE;
+    }
+}
+
+template <int MODE, bool COUNT>
 __device__ __forceinline__ void refill(const rt::TraceParams& P, uint32_t lane, uint32_t& st, Path& ps,
                                        WaveBlock& blk, Stamps& stamps) {
+#if RT_TAIL_STEAL
+    if (MODE == rt::MODE_HASH && blk.done) steal_tail<COUNT>(P, lane, st, ps);   // wave-uniform condition
+#endif
     const unsigned long long need = __ballot(st == ST_NEED_UNIT);
     if (!need) return;
     STAMP(5);
@@ -806,7 +846,7 @@ __global__ __launch_bounds__(kBruteBlock, RT_BRUTE_WAVES_PER_SIMD) void rt_trace
     first_block(P, lane, blk);
     STAMP_DECL;
     for (;;) {
-        refill<MODE>(P, lane, st, ps, blk, stamps);
+        refill<MODE, COUNT>(P, lane, st, ps, blk, stamps);
         if (st == ST_NEED_SAMPLE) {
             if (start_sample<MODE, false>(P, cam, ps, o, d)) { st = ST_TRACING; n_smp++; }
             else st = ST_NEED_UNIT;
@@ -1439,7 +1479,7 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
     STAMP_DECL;
     for (;;) {
         STAMP(0);
-        refill<MODE>(P, lane, st, ps, blk, stamps);
+        refill<MODE, COUNT>(P, lane, st, ps, blk, stamps);
         if (!saw_dry && __ballot(st == ST_RETIRED)) {   // this wave saw the queue run dry
             saw_dry = true;
             if (lane == 0) atomicMin(&P.counters->t_dry, __builtin_amdgcn_s_memrealtime());

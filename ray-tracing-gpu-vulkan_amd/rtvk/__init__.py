@@ -206,6 +206,13 @@ class Renderer:
         check(self._lib.rt_get_stats(self._ctx, ctypes.byref(st)))
         return st
 
+    def steals(self) -> int:
+        """Tail steals of the last instrumented launch (count_tests; rt_debug_steals; counter-based
+        stream only)."""
+        v = ctypes.c_uint64()
+        check(self._lib.rt_debug_steals(self._ctx, ctypes.byref(v)))
+        return int(v.value)
+
     def launch_info(self) -> dict:
         """Of the last launch: sample chunks per pixel, the kernel form it ran, its dynamic LDS
         bytes, the CU count (rt_debug_launch_info)."""

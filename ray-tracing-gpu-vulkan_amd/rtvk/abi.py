@@ -130,6 +130,7 @@ EXPORTS = {
     "rt_build_info": (ctypes.c_char_p, []),
     "rt_debug_walk_hist": (_I, [_P, _P]),
     "rt_debug_lane_hist": (_I, [_P, _P]),
+    "rt_debug_steals": (_I, [_P, _P]),
     "rt_debug_tile_cost": (_I, [_P, _P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     "rt_debug_scene": (_I, [_P, _U32, _P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     "ray_trace": (None, [_U32, ctypes.c_bool, _U32, _U32, _U32]),

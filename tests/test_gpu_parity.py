@@ -392,6 +392,29 @@ def test_hash_chunk_invariance(rtvk, renderer, torch, oracle, chunks):
                 assert renderer.launch_info()["chunks"] == min(int(chunks), spp)
 
 
+def test_hash_tail_steals(rtvk, renderer, torch, oracle):
+    """Tail stealing (rt_kernels.hip steal_tail): one chunk per pixel and fewer units than lanes,
+    so the queue is empty at once and lanes whose pixels end early (sky) take halves of the
+    samples their wave's busiest lanes have not started. The frame keeps the oracle's bits and
+    counts for the grid and brute-force kernels (the instrumented builds count the steals; the
+    production builds run the same stealing code); the reference stream never steals."""
+    W, H, spp = 40, 24, 400
+    sc = oracle.generate_scene()
+    rci = oracle.render_call_info(spp, W, H)
+    ra, ro, rs = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=HASH), threads=16)
+    with env(RT_SAMPLE_CHUNKS=1):
+        for accel in (LBVH, BRUTE):
+            for count in (False, True):
+                a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, rng_mode=HASH, accel=accel, count=count)
+                assert_same(a, o, ra, ro)
+                assert (st.segments, st.samples) == rs[:2]
+                assert renderer.launch_info()["chunks"] == 1
+            assert renderer.steals() > 0
+    gpu_render(rtvk, renderer, torch, sc, oracle.render_call_info(4, W, H), W, H, rng_mode=STREAM, accel=LBVH,
+               count=True)
+    assert renderer.steals() == 0
+
+
 @pytest.mark.parametrize("rng_mode", [STREAM, HASH])
 def test_host_rt_render_bands(rtvk, oracle, rng_mode):
     """rt_render with 3 contiguous bands (one per GPU in the reference, src/ray_trace.cpp:74-93;
