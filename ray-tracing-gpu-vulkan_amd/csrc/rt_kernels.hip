@@ -25,8 +25,12 @@ using namespace rtd;
 
 namespace {
 
-// Code shape switch (1 = shipped; 0 builds the previous form for A/B timing): the winner's
-// shading records loaded with its gate.
+// Code shape switches (1 = shipped; 0 builds the previous form for A/B timing): the winner's
+// shading records loaded with its gate; the LDS grid's reference records read one ahead; tail
+// stealing in the counter-based stream.
+#ifndef RT_LDS_PIPE
+#define RT_LDS_PIPE 1
+#endif
 #ifndef RT_TAIL_STEAL
 #define RT_TAIL_STEAL 1
 #endif
@@ -1110,11 +1114,29 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
             ++j;
           }
         }
+#if RT_LDS_PIPE
+        if (!PAIRS && j < e) {   // two records in flight, no register copies (unrolled by two)
+            float4 A = rec[j], B;
+            for (;;) {
+                UTIL(1, true);
+                B = rec[j + 1];   // one past the run: the next cell's record or the id array (LDS)
+                test1(A, [&] { return ids[j]; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
+                if (COUNT) n_sph++;
+                if (++j >= e) break;
+                UTIL(1, true);
+                A = rec[j + 1];
+                test1(B, [&] { return ids[j]; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
+                if (COUNT) n_sph++;
+                if (++j >= e) break;
+            }
+        }
+#else
         for (; j < e; ++j) {   // from LDS one at a time (pairs measured 1 % slower there)
             UTIL(1, true);
             test1(rec[j], [&] { return ids[j]; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
             if (COUNT) n_sph++;
         }
+#endif
         UTIL(0, true);
         const float tm = fminf(fminf(tx, ty), tz);
         if (!(tm <= r.limit)) break;   // the next cell starts beyond every closer candidate
