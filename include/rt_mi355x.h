@@ -261,6 +261,10 @@ int rt_debug_util(rt_context* ctx, uint64_t* out32);
 /* Diagnostic: histogram of LBVH box tests per segment of the last instrumented launch
  * (options.reserved[0] & 1), 2 x 64 bins: [0] segments that miss, [1] segments that hit. */
 int rt_debug_walk_hist(rt_context* ctx, uint64_t* out128);
+/* Diagnostic: walk work (cells + references) of ctx's last instrumented launch per segment pass,
+   max over the wave's tracing lanes [0] and over its bounce (depth > 0) lanes [1], summed over
+   passes; the primary (depth 0) lanes' summed work [2] and their count [3]. */
+int rt_debug_walk_split(rt_context* ctx, uint64_t* out4);
 /* Diagnostic: segment-loop iterations of the last instrumented launch by the number of lanes
  * (0..64) of the wave tracing in that iteration (the persistent kernel's lane occupancy), then
  * three s_memrealtime stamps (100 MHz): first wave start, pixel queue dry, last wave exit. */

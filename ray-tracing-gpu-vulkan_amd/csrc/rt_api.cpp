@@ -1120,6 +1120,18 @@ int rt_debug_steals(rt_context* ctx, uint64_t* out) {
     return RT_OK;
 }
 
+// Diagnostic export: walk work of the last COUNT launch split by primary / bounce segments
+// (rt_internal.h Counters::walk_split).
+int rt_debug_walk_split(rt_context* ctx, uint64_t* out4) {
+    if (!ctx || !out4) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    DeviceGuard g(ctx->device);
+    if (ctx->ev_valid) RT_HIP(hipEventSynchronize(ctx->ev_last));
+    rt::Counters c;
+    RT_HIP(hipMemcpy(&c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
+    std::memcpy(out4, c.walk_split, sizeof(c.walk_split));
+    return RT_OK;
+}
+
 // Diagnostic export: walk-length histogram of the last COUNT launch (2 x 64 bins: miss, hit).
 int rt_debug_walk_hist(rt_context* ctx, uint64_t* out128) {
     if (!ctx || !out128) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");

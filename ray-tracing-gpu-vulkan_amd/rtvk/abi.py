@@ -129,6 +129,7 @@ EXPORTS = {
     "rt_debug_kernel_times": (_I, [_P, _P, _U32, ctypes.POINTER(_U32)]),
     "rt_build_info": (ctypes.c_char_p, []),
     "rt_debug_walk_hist": (_I, [_P, _P]),
+    "rt_debug_walk_split": (_I, [_P, _P]),
     "rt_debug_lane_hist": (_I, [_P, _P]),
     "rt_debug_steals": (_I, [_P, _P]),
     "rt_debug_tile_cost": (_I, [_P, _P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),

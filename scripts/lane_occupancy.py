@@ -12,12 +12,13 @@ from rtvk import abi  # noqa: E402
 
 W, H = 1920, 1080
 spp = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+rng = rtvk.HASH if len(sys.argv) > 2 and sys.argv[2] == "hash" else rtvk.STREAM   # usage: [spp] [hash|stream]
 r = rtvk.Renderer(0)
 r.set_scene(rtvk.generateRandomScene())
 acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
 out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
 r.render_device(rtvk.canonical_render_call_info(spp, W, H), acc, out,
-                options=rtvk.make_options(accel=2, count_tests=True))
+                options=rtvk.make_options(rng_mode=rng, count_tests=True))
 torch.cuda.synchronize()
 h = (ctypes.c_uint64 * 68)()
 abi.check(abi.load_library().rt_debug_lane_hist(r._ctx, h))
@@ -31,7 +32,7 @@ for lo, hi in [(0, 16), (16, 32), (32, 48), (48, 60), (60, 65)]:
     sel = slice(lo, hi)
     print(f"  {lo:2d}-{hi - 1:2d} lanes: {h[sel].sum() / iters * 100:5.1f} % of iterations, "
           f"{np.dot(h[sel], k[sel]) / np.dot(h, k) * 100:5.1f} % of lane-segments")
-r.render_device(rtvk.canonical_render_call_info(spp, W, H), acc, out, options=rtvk.make_options(accel=2))
+r.render_device(rtvk.canonical_render_call_info(spp, W, H), acc, out, options=rtvk.make_options(rng_mode=rng))
 torch.cuda.synchronize()
 h2 = (ctypes.c_uint64 * 68)()
 abi.check(abi.load_library().rt_debug_lane_hist(r._ctx, h2))
