@@ -32,6 +32,7 @@ hipError_t trace_occupancy(uint32_t accel, bool count, int mode, size_t lds_byte
 hipError_t launch_resolve_fixed(unsigned long long* fixed, uint64_t n_texels, uint32_t accumulate, uint32_t spp,
                                 float* accum, uint8_t* out, hipStream_t st);
 hipError_t launch_tonemap(const float* accum, uint64_t n_texels, uint32_t spp, uint8_t* out, hipStream_t st);
+hipError_t launch_big_table(const TraceParams& P, float* tab, hipStream_t st);
 uint32_t block_size(uint32_t accel);
 hipError_t launch_scatter_rows(const float* src_acc, const uint8_t* src_px, const uint32_t* rows,
                                uint32_t n_rows, uint32_t width, uint32_t dst_rows, float* dst_acc, uint8_t* dst_px,
@@ -48,6 +49,7 @@ struct rt_context {
     std::vector<void*> scene_allocs;
     std::vector<void*> grid_allocs;              // device-built grid arrays (rebuilt by every refit)
     rt::Counters* counters = nullptr;            // device
+    float* big_tab = nullptr;                    // device, in the counters' allocation (TraceParams::big_tab)
     // Every device operation of a context (scene upload / build, render) is ordered after the
     // previous one, whatever streams they are issued on: an op on a stream other than the last
     // one first waits for `ev_last`, and every op records it when issued.
@@ -423,9 +425,11 @@ int rt_context_create(int device, rt_context** out) {
     ctx->device = device;
     RT_HIP(hipDeviceGetAttribute(&ctx->cu_count, hipDeviceAttributeMultiprocessorCount, device));
     void* c = nullptr;
-    RT_HIP(hipMalloc(&c, sizeof(rt::Counters)));
-    RT_HIP(hipMemset(c, 0, sizeof(rt::Counters)));
+    constexpr size_t kBigOff = (sizeof(rt::Counters) + 255) & ~size_t(255);
+    RT_HIP(hipMalloc(&c, kBigOff + rt::kBigMax * 20u));
+    RT_HIP(hipMemset(c, 0, kBigOff + rt::kBigMax * 20u));
     ctx->counters = static_cast<rt::Counters*>(c);
+    ctx->big_tab = reinterpret_cast<float*>(static_cast<char*>(c) + kBigOff);
     for (auto& a : ctx->occ_lds)
         for (auto& b : a)
             for (auto& v : b) v = ~size_t(0);
@@ -1012,6 +1016,8 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     hipEvent_t* kev = ctx->kev[ctx->kev_count % rt_context::kKernelEvents];
     for (int k = 0; k < 2; k++)
         if (!kev[k]) RT_HIP(hipEventCreate(&kev[k]));
+    if (P.n_big) RT_HIP(rt::launch_big_table(P, ctx->big_tab, st));
+    P.big_tab = ctx->big_tab;
     RT_HIP(hipEventRecord(kev[0], st));
     RT_HIP(rt::launch_trace(P, accel, count, mode, grid, lds, st));
     RT_HIP(hipEventRecord(kev[1], st));

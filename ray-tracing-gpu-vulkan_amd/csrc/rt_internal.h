@@ -232,6 +232,9 @@ struct TraceParams {
     uint32_t* out;                 // STREAM: band_w * band_h packed rgba8
     unsigned long long* fixed;     // HASH: 3 planes of band_w * band_h u64 (r, g, b), zero on entry
     Counters* counters;
+    const float* big_tab;          // the big spheres as kBigMax records {cx, cy, cz, r} (padded to a
+                                   // multiple of 4 by repeating the last) + kBigMax ids, filled per
+                                   // launch (rt_big_table_kernel), read through the scalar cache
 };
 
 // HASH mode fixed point: a sample colour channel c in [0, 1] (every colour and the sky are <= 1,
