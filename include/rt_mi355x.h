@@ -250,8 +250,10 @@ int rt_debug_kernel_times(rt_context* ctx, float* out_ms, uint32_t capacity, uin
 /* Build provenance of this library: "sources_sha256=<16 hex of the sources it was compiled
  * from>;arch=gfx950;flags=...". Static string. */
 const char* rt_build_info(void);
-/* Diagnostic: of ctx's last launch, {sample chunks per pixel, the kernel form it ran (rt_internal.h
- * ACCEL_*; before any launch: the scene's default form), its dynamic LDS bytes, CU count}. */
+/* Diagnostic: of ctx's last launch, {sample chunks per pixel (low 16 bits: of the LPT order's tail
+ * tiles; high 16 bits: of its head tiles, 0 when the launch had no head), the kernel form it ran
+ * (rt_internal.h ACCEL_*; before any launch: the scene's default form), its dynamic LDS bytes, CU
+ * count}. */
 int rt_debug_launch_info(rt_context* ctx, uint32_t* out4);
 /* Diagnostic: per-phase cycle sums of ctx's last launch, filled only by -DRT_STAMPS builds. */
 int rt_debug_stamps(rt_context* ctx, uint64_t* out8);

@@ -935,6 +935,7 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     // sample, so its floor scales down with n (488 spheres: 5 samples; config 2, 100 spp: 1 -> 20
     // chunks).
     uint64_t chunks = 1;
+    bool chunks_forced = false;
     if (mode == rt::MODE_HASH && spp > 1) {
         uint64_t per_lane = 128, min_samples = 256;
         if (accel == rt::ACCEL_BRUTE) min_samples = std::min<uint64_t>(256, std::max<uint64_t>(4, 2560 / std::max(1u, d.n_spheres)));
@@ -942,16 +943,17 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
         if (const char* e = std::getenv("RT_UNIT_MIN_SAMPLES")) min_samples = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
         const uint64_t pixels = uint64_t(band_width) * band_height;
         chunks = std::min<uint64_t>((lanes * per_lane + pixels - 1) / pixels, std::max<uint64_t>(1, spp / min_samples));
-        if (const char* e = std::getenv("RT_SAMPLE_CHUNKS")) chunks = std::strtoull(e, nullptr, 10);
+        if (const char* e = std::getenv("RT_SAMPLE_CHUNKS")) {
+            chunks = std::strtoull(e, nullptr, 10);
+            chunks_forced = true;
+        }
         chunks = std::max<uint64_t>(1, std::min<uint64_t>({chunks, spp, 4096}));
         while (chunks > 1 && n_tiles * chunks * 64u >= (1ull << 31)) chunks /= 2;   // unit ids in 32 bits
     }
     if (n_tiles * chunks * 64u >= (1ull << 32)) return fail(RT_ERR_INVALID_ARGUMENT, "band too large");
     P.chunks = uint32_t(chunks);
-    ctx->last_chunks = P.chunks;
     ctx->last_accel = accel;
     ctx->last_lds = lds;
-    P.n_units = uint32_t(n_tiles * chunks * 64u);
     const uint64_t texels = uint64_t(band_width) * band_height;
     if (mode == rt::MODE_HASH) {
         if (ctx->fixed_cap < texels) {
@@ -984,6 +986,40 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
         RT_HIP(hipMemsetAsync(sc.cost[sc.cur], 0, size_t(sc.n) * 4, st));
         P.tile_cost = sc.cost[sc.cur];
         P.tile_cost_sum = (e && std::strcmp(e, "sum") == 0) ? 1u : 0u;
+    }
+    // Head and tail of the LPT order (HASH): the frame's tail is made of the units
+    // still running when the queue runs dry, so only the last ranks (the shortest fifth of the
+    // tiles) need short units, 2/5 of `chunks` (the count that keeps a uniform split
+    // throughput-bound); the head ranks run chunks / 8 longer ones, which end while the tail
+    // runs. A fifth of the units at config 3 (25 -> 3 / 10 chunks), so fewer unit starts and
+    // flushes, and fewer 64-bit fixed-point atomics, whose memory-side requests are most of the
+    // kernel's HBM traffic: 6.6 -> 0.98 GB per frame at -0.6 % frame time (10 tail chunks; 25:
+    // 1.6 GB at -0.9 %; profiles/r03_tail_chunks_traffic.txt). RT_HEAD_CHUNKS / RT_TAIL_TILES_PM
+    // (tail tiles per mille) override; RT_SAMPLE_CHUNKS sets the tail count itself.
+    uint64_t head_tiles = 0, head_chunks = chunks;
+    if (mode == rt::MODE_HASH && chunks > 1 && P.tile_order) {
+        const uint64_t tail_chunks = chunks_forced ? chunks : std::max<uint64_t>(1, (chunks * 2 + 4) / 5);
+        head_chunks = std::max<uint64_t>(1, chunks / 8);
+        uint64_t tail_pm = 200;
+        if (const char* e = std::getenv("RT_HEAD_CHUNKS")) head_chunks = std::strtoull(e, nullptr, 10);
+        if (const char* e = std::getenv("RT_TAIL_TILES_PM")) tail_pm = std::strtoull(e, nullptr, 10);
+        head_chunks = std::max<uint64_t>(1, std::min<uint64_t>(head_chunks, tail_chunks));
+        const uint64_t tail = std::min<uint64_t>(n_tiles, (n_tiles * std::min<uint64_t>(tail_pm, 1000) + 999) / 1000);
+        if (head_chunks < tail_chunks) {
+            head_tiles = n_tiles - tail;
+            P.chunks = uint32_t(tail_chunks);
+        }
+    }
+    chunks = P.chunks;
+    P.head_tiles = uint32_t(head_tiles);
+    P.head_chunks = uint32_t(head_tiles ? head_chunks : chunks);
+    P.n_units = uint32_t((head_tiles * P.head_chunks + (n_tiles - head_tiles) * chunks) * 64u);
+    ctx->last_chunks = P.chunks | (head_tiles ? P.head_chunks << 16 : 0u);
+    if (P.tile_cost) {   // this launch's chunk split, for the cost normalisation of the next order
+        rt::TileSchedule& sc = ctx->sched;
+        sc.rec_head_tiles[sc.cur] = P.head_tiles;
+        sc.rec_head_chunks[sc.cur] = P.head_chunks;
+        sc.rec_chunks[sc.cur] = P.chunks;
     }
     RT_HIP(hipMemsetAsync(ctx->counters, 0, sizeof(rt::Counters), st));
     // first-time stamps start at the maximum (atomicMin); 0xff bytes = ~0ull

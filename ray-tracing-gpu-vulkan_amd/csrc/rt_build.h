@@ -77,6 +77,11 @@ struct TileSchedule {
     size_t tmp_bytes = 0;
     int cur = 0;                   // table the next launch records into
     bool valid = false;            // cost[cur ^ 1] holds a completed launch of this geometry
+    // the head / tail chunk split of the launch that recorded cost[k] (TraceParams head_tiles,
+    // head_chunks, chunks; head_tiles = 0: one chunk count): its unit chains are per chunk, so
+    // schedule_order scales each tile's cost by its chunk count before sorting (a per-pixel chain
+    // estimate, comparable between head and tail tiles)
+    uint32_t rec_head_tiles[2] = {0, 0}, rec_head_chunks[2] = {1, 1}, rec_chunks[2] = {1, 1};
 };
 // (Re)allocates for n tiles when the geometry changes (tables zeroed, valid = false).
 hipError_t schedule_reserve(TileSchedule& s, uint32_t n, hipStream_t st);

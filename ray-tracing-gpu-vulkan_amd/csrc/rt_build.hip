@@ -596,7 +596,23 @@ hipError_t schedule_reserve(TileSchedule& s, uint32_t n, hipStream_t st) {
     return hipSuccess;
 }
 
+// cost[order[r]] *= the chunk count of rank r in the launch that recorded it (saturating).
+__global__ void k_cost_norm(uint32_t* __restrict__ cost, const uint32_t* __restrict__ order, uint32_t n,
+                            uint32_t head_tiles, uint32_t head_chunks, uint32_t chunks) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const uint32_t t = order[r];
+    const uint64_t v = uint64_t(cost[t]) * (r < head_tiles ? head_chunks : chunks);
+    cost[t] = uint32_t(v < 0xffffffffull ? v : 0xffffffffull);
+}
+
 hipError_t schedule_order(TileSchedule& s, hipStream_t st) {
+    const int last = s.cur ^ 1;
+    if (s.rec_head_tiles[last]) {   // `order` still holds the ranks that launch handed out
+        k_cost_norm<<<blocks(s.n), kBlock, 0, st>>>(s.cost[last], s.order, s.n, s.rec_head_tiles[last],
+                                                   s.rec_head_chunks[last], s.rec_chunks[last]);
+        if (hipError_t e = hipGetLastError()) return e;
+    }
     size_t tb = s.tmp_bytes;
     return hipcub::DeviceRadixSort::SortPairsDescending(s.tmp, tb, s.cost[s.cur ^ 1], s.keys, s.iota, s.order,
                                                         int(s.n), 0, 32, st);

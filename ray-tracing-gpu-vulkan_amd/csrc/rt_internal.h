@@ -176,9 +176,10 @@ struct Counters {
 // Kernel launch parameters (passed by value as the kernel argument).
 //
 // Work units: unit u = (8x8 tile, sample chunk, pixel of the tile). Block b = u / 64 covers one
-// chunk of one tile's 64 pixels; tile rank = b / chunks, chunk = b % chunks; the tile is
-// tile_order[rank] (LPT hand-out) or the rank itself. Chunk c of a pixel runs samples
-// [c * spp / chunks, (c + 1) * spp / chunks). STREAM launches have chunks = 1.
+// chunk of one tile's 64 pixels; tile rank = b / n, chunk = b % n for the n = head_chunks chunks
+// of the head ranks, then likewise over the remaining blocks with n = chunks; the tile is
+// tile_order[rank] (LPT hand-out) or the rank itself. Chunk c of n runs samples
+// [c * spp / n, (c + 1) * spp / n). STREAM launches have one chunk.
 struct TraceParams {
     // Camera / viewport (shader.rgen:92-115), computed once per launch on the host.
     float lf[3], hor[3], ver[3], ulc[3], cup[3], crt[3];
@@ -194,7 +195,10 @@ struct TraceParams {
     uint32_t band_w, band_h;
     uint32_t tiles_x;              // ceil(band_w / 8)
     uint32_t chunks;               // sample chunks per pixel (>= 1)
-    uint32_t n_units;              // tiles * chunks * 64
+    uint32_t head_tiles;           // hand-out ranks [0, head_tiles) (the head of the LPT order, the
+    uint32_t head_chunks;          // longest tiles) split a pixel into head_chunks chunks, the
+                                   // other ranks into `chunks`; 0 tiles: no head
+    uint32_t n_units;              // 64 * (head_tiles * head_chunks + (tiles - head_tiles) * chunks)
     uint32_t n_block_units;        // units [0, n_block_units) go out as whole 64-unit blocks (one
                                    // atomic per block per wave), the rest unit by unit
     uint32_t first_blocks;         // blocks [0, first_blocks) start on wave id = block (no atomic)

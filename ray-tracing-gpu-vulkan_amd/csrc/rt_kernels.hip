@@ -431,10 +431,23 @@ __device__ __forceinline__ uint32_t tile_pixel_seed(const rt::TraceParams& P, ui
     return tea(tea(P.seed_local ? lx : gx, P.seed_local ? ly : gy), P.number);
 }
 
-// First sample of chunk c (the chunk runs [chunk_begin(c), chunk_begin(c + 1))). The host keeps
-// chunks * spp below 2^32.
-__device__ __forceinline__ uint32_t chunk_begin(const rt::TraceParams& P, uint32_t c) {
-    return (c * P.spp) / P.chunks;
+// Block b's tile rank, chunk c and chunk count n: the head ranks' blocks come first, n =
+// head_chunks, then the others', n = chunks (TraceParams). Chunk c of n runs samples
+// [chunk_begin(c, n), chunk_begin(c + 1, n)); the host keeps n * spp below 2^32.
+struct BlockChunk { uint32_t rank, c, n; };
+
+__device__ __forceinline__ BlockChunk block_chunk(const rt::TraceParams& P, uint32_t b) {
+    const uint32_t hb = P.head_tiles * P.head_chunks;
+    if (b < hb) {
+        const uint32_t rank = b / P.head_chunks;
+        return BlockChunk{rank, b - rank * P.head_chunks, P.head_chunks};
+    }
+    const uint32_t b2 = b - hb, r2 = b2 / P.chunks;
+    return BlockChunk{P.head_tiles + r2, b2 - r2 * P.chunks, P.chunks};
+}
+
+__device__ __forceinline__ uint32_t chunk_begin(const rt::TraceParams& P, uint32_t c, uint32_t n) {
+    return (c * P.spp) / n;
 }
 
 // Unit hand-out. A wave takes whole 64-unit blocks (one chunk of one 8x8 tile, one atomic) from
@@ -456,17 +469,17 @@ struct WaveBlock {
 
 __device__ __forceinline__ void take_block(const rt::TraceParams& P, uint32_t lane, WaveBlock& blk,
                                            uint32_t b, uint32_t tile) {
-    const uint32_t c = b % P.chunks;
+    const BlockChunk bc = block_chunk(P, b);
     blk.next = b * 64u;
     blk.end = blk.next + 64u;
     blk.tile = tile;
-    blk.s0 = chunk_begin(P, c);
-    blk.s1 = chunk_begin(P, c + 1u);
+    blk.s0 = chunk_begin(P, bc.c, bc.n);
+    blk.s1 = chunk_begin(P, bc.c + 1u, bc.n);
     blk.seed = tile_pixel_seed(P, tile, lane);
 }
 
 __device__ __forceinline__ uint32_t block_tile(const rt::TraceParams& P, uint32_t b) {
-    const uint32_t rank = b / P.chunks;
+    const uint32_t rank = block_chunk(P, b).rank;
     return P.tile_order ? load_now(P.tile_order + rank) : rank;
 }
 
@@ -570,10 +583,11 @@ __device__ __forceinline__ void refill(const rt::TraceParams& P, uint32_t lane, 
     if (st != ST_NEED_UNIT) return;
     if (per_lane) {
         if (u >= P.n_units) { st = ST_RETIRED; return; }
-        const uint32_t b = u >> 6, c = b % P.chunks;
-        t = block_tile(P, b);
-        s0 = chunk_begin(P, c);
-        s1 = chunk_begin(P, c + 1u);
+        const uint32_t b = u >> 6;
+        const BlockChunk bc = block_chunk(P, b);
+        t = P.tile_order ? load_now(P.tile_order + bc.rank) : bc.rank;
+        s0 = chunk_begin(P, bc.c, bc.n);
+        s1 = chunk_begin(P, bc.c + 1u, bc.n);
     }
     const uint32_t w = u & 63u;
     const uint32_t lx = (t % P.tiles_x) * 8u + (w & 7u);
@@ -815,9 +829,14 @@ __device__ __forceinline__ bool shade(const rt::TraceParams& P, const Camera& ca
 }
 
 
-// Finished unit: its chain length (traced segments) feeds the next launch's hand-out order.
+// Finished unit: its chain length (traced segments) feeds the next launch's hand-out order. HASH:
+// only the units of the tile's 16 pixels with even coordinates record (a quarter of the
+// memory-side atomic requests; the image does not depend on the order); STREAM: every pixel, the
+// frame ends with the longest chain.
+template <int MODE>
 __device__ __forceinline__ void record_tile_cost(const rt::TraceParams& P, const Path& ps) {
     if (!P.tile_cost) return;
+    if (MODE == rt::MODE_HASH && (ps.px & 0x00010001u)) return;
     const uint32_t lx = ps.px & 0xffffu, ly = ps.px >> 16;
     uint32_t* c = &P.tile_cost[(ly >> 3) * P.tiles_x + (lx >> 3)];
     if (P.tile_cost_sum) atomicAdd(c, ps.segs); else atomicMax(c, ps.segs);
@@ -1559,7 +1578,7 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
                 started = true;
             } else {   // empty unit (spp = 0): stored at once
                 st = ST_NEED_UNIT;
-                record_tile_cost(P, ps);
+                record_tile_cost<MODE>(P, ps);
             }
         }
         smp_w += __popcll(__ballot(started));
@@ -1620,7 +1639,7 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
                 // The unit's last sample ended: finish it here, and the lane asks for a unit at
                 // the top of the next iteration.
                 finish_unit<MODE, LSUM>(P, ps);
-                record_tile_cost(P, ps);
+                record_tile_cost<MODE>(P, ps);
                 st = ST_NEED_UNIT;
             }
         }

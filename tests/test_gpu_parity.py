@@ -392,6 +392,27 @@ def test_hash_chunk_invariance(rtvk, renderer, torch, oracle, chunks):
                 assert renderer.launch_info()["chunks"] == min(int(chunks), spp)
 
 
+@pytest.mark.parametrize("head,tail_pm", [("1", "0"), ("2", "300"), ("5", "500"), ("1", "1"), ("3", "1000")])
+def test_hash_head_tail_chunks(rtvk, renderer, torch, oracle, head, tail_pm):
+    """RT_RNG_SAMPLE_HASH with the LPT order split into a head (the longest tiles, RT_HEAD_CHUNKS
+    chunks per pixel) and a tail (RT_TAIL_TILES_PM per mille of the tiles, `chunks` = 7 chunks):
+    the oracle's bits and counts for every split, from all-head (0 per mille) to all-tail (1000,
+    no head), on a ragged band; the first launch has no LPT order (no head), the second has."""
+    W, H, spp = 77, 45, 13
+    sc = oracle.generate_scene()
+    rci = oracle.render_call_info(spp, W, H)
+    ra, ro, rs = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=HASH))
+    with env(RT_SAMPLE_CHUNKS="7", RT_HEAD_CHUNKS=head, RT_TAIL_TILES_PM=tail_pm):
+        for k in range(3):
+            a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, rng_mode=HASH, accel=LBVH, count=k == 2)
+            assert_same(a, o, ra, ro)
+            assert (st.segments, st.samples) == rs[:2]
+            info = renderer.launch_info()
+            assert info["chunks"] == 7
+            if k > 0:
+                assert info["head_chunks"] == (None if tail_pm == "1000" else int(head))
+
+
 def test_hash_tail_steals(rtvk, renderer, torch, oracle):
     """Tail stealing (rt_kernels.hip steal_tail): one chunk per pixel and fewer units than lanes,
     so the queue is empty at once and lanes whose pixels end early (sky) take halves of the
