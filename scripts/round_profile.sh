@@ -13,12 +13,12 @@ mkdir -p "$OUT" gpurun_out/profiles_new
 export TMPDIR=/tmp
 ROOT=$(pwd)
 if [ "$CONFIG" = 5 ]; then
-    BARGS=${BENCH_ARGS:-"--config 5 --steps 2 --warmup 1 --profile"}
-    PARGS=${PMC_BENCH_ARGS:-"--config 5 --steps 1 --warmup 1 --profile"}
+    BARGS=${BENCH_ARGS:-"--config 5 --steps 2 --warmup 2 --profile"}
+    PARGS=${PMC_BENCH_ARGS:-"--config 5 --steps 1 --warmup 2 --profile"}
     KEY=${KEY:-lbvh-hash-3840x2160-1000spp-grid158-n1}
 else
-    BARGS=${BENCH_ARGS:-"--steps 3 --warmup 1 --profile"}
-    PARGS=${PMC_BENCH_ARGS:-"--steps 1 --warmup 1 --profile"}
+    BARGS=${BENCH_ARGS:-"--steps 3 --warmup 2 --profile"}
+    PARGS=${PMC_BENCH_ARGS:-"--steps 1 --warmup 2 --profile"}
     KEY=${KEY:-lbvh-hash-1920x1080-10000spp-grid11-n1}
 fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/stats" -o run -- \
