@@ -915,6 +915,19 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
             ctx->padded_for = ctx->pad_radius;
         }
     }
+    // The row map of a banded launch (N > 1 strips) is staged in the walk kernels' dynamic LDS
+    // after their own data (band_row, rt_kernels.hip) when that keeps the blocks per CU; else it
+    // is read from global memory.
+    P.rows_lds = rt::kNoRowsLds;
+    if (rows && accel != rt::ACCEL_BRUTE) {
+        const size_t off = (lds + 15) & ~size_t(15), with = off + size_t(band_height) * 4u;
+        int b0 = 0, b1 = 0;
+        if (with <= kMaxLdsBytes && rt::trace_occupancy(accel, count, mode, lds, &b0) == hipSuccess &&
+            rt::trace_occupancy(accel, count, mode, with, &b1) == hipSuccess && b1 >= b0 && b1 > 0) {
+            P.rows_lds = uint32_t(off);
+            lds = with;
+        }
+    }
     // Grid: one persistent block per CU slot the occupancy allows.
     const int ci = count ? 1 : 0;
     if (ctx->occ_lds[accel][ci][mode] != lds) {
@@ -990,16 +1003,21 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     // Head and tail of the LPT order (HASH): the frame's tail is made of the units
     // still running when the queue runs dry, so only the last ranks (the shortest fifth of the
     // tiles) need short units, 2/5 of `chunks` (the count that keeps a uniform split
-    // throughput-bound); the head ranks run chunks / 8 longer ones, which end while the tail
-    // runs. A fifth of the units at config 3 (25 -> 3 / 10 chunks), so fewer unit starts and
-    // flushes, and fewer 64-bit fixed-point atomics, whose memory-side requests are most of the
+    // throughput-bound); the head ranks run longer ones, about 12 per lane (a head unit ~1/12 of
+    // the frame, so it ends while the tail runs), and only when that is fewer chunks than the
+    // tail's (not at 1080p / 1000 spp, whose uniform units are already that long). Config 3:
+    // 25 -> 3 head / 10 tail chunks, config 5: 3 -> 1 / 3. A sixth of the units at config 3, so
+    // fewer unit starts and flushes, and fewer 64-bit fixed-point atomics, whose memory-side requests are most of the
     // kernel's HBM traffic: 6.6 -> 0.98 GB per frame at -0.6 % frame time (10 tail chunks; 25:
     // 1.6 GB at -0.9 %; profiles/r03_tail_chunks_traffic.txt). RT_HEAD_CHUNKS / RT_TAIL_TILES_PM
     // (tail tiles per mille) override; RT_SAMPLE_CHUNKS sets the tail count itself.
     uint64_t head_tiles = 0, head_chunks = chunks;
     if (mode == rt::MODE_HASH && chunks > 1 && P.tile_order) {
-        const uint64_t tail_chunks = chunks_forced ? chunks : std::max<uint64_t>(1, (chunks * 2 + 4) / 5);
-        head_chunks = std::max<uint64_t>(1, chunks / 8);
+        const uint64_t pixels = uint64_t(band_width) * band_height;
+        head_chunks = std::max<uint64_t>(1, (12u * lanes + pixels - 1) / std::max<uint64_t>(1, pixels));
+        // tail units: at most 2.5x the uniform ones, and at least 3x shorter than the head's
+        const uint64_t tail_chunks =
+            chunks_forced ? chunks : std::max<uint64_t>((chunks * 2 + 4) / 5, std::min<uint64_t>(chunks, 3 * head_chunks));
         uint64_t tail_pm = 200;
         if (const char* e = std::getenv("RT_HEAD_CHUNKS")) head_chunks = std::strtoull(e, nullptr, 10);
         if (const char* e = std::getenv("RT_TAIL_TILES_PM")) tail_pm = std::strtoull(e, nullptr, 10);

@@ -205,6 +205,8 @@ struct TraceParams {
     uint32_t isolate_blocks;       // waves of the first LPT blocks take no further work
     uint32_t force_regate;         // test only: every segment's winner recomputed by the gated brute force
     const uint32_t* rows;          // optional global row per band row
+    uint32_t rows_lds;             // rows staged in dynamic LDS at this byte offset by the walk
+                                   // kernels' prologue (kNoRowsLds: read from global memory)
     const uint32_t* tile_order;    // optional: hand-out rank -> 8x8 tile index (null: row-major)
     uint32_t* tile_cost;           // optional: per 8x8 tile, traced segments of its longest unit
                                    // (zeroed by the host)
@@ -253,6 +255,7 @@ constexpr uint32_t kFixedFlush = 128;
 // records (center, radius) and ids in LDS once per block: kBigLdsBytes at the end of the block's
 // dynamic LDS.
 constexpr uint32_t kBigMax = 64;
+constexpr uint32_t kNoRowsLds = 0xffffffffu;
 constexpr uint32_t kBigLdsBytes = kBigMax * 16u + kBigMax * 4u;
 constexpr uint32_t kHashMaxSpp = 1u << 19;
 

@@ -422,12 +422,30 @@ __device__ __forceinline__ void flush_fixed(const rt::TraceParams& P, Path& ps) 
     ps.qx = ps.qy = ps.qz = 0u;
 }
 
+// Global row of band row ly: the row map (rows), staged in LDS by the walk kernels when it fits
+// their LDS plan (an lgkmcnt wait instead of a global load whose vmcnt(0) wait also drains the
+// wave's stores and atomics; N > 1 strips: one per sample start), else loaded
+// from global memory; without a map, off_y + ly.
+extern __shared__ float4 rt_dyn_lds[];   // the dynamic LDS of the launch (the kernels' `lds`)
+__device__ __forceinline__ uint32_t band_row(const rt::TraceParams& P, uint32_t ly) {
+    if (!P.rows) return P.off_y + ly;
+    if (P.rows_lds != rt::kNoRowsLds)
+        return reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(rt_dyn_lds) + P.rows_lds)[ly];
+    return load_now(P.rows + ly);
+}
+// (before the prologue's barrier)
+__device__ __forceinline__ void stage_rows(const rt::TraceParams& P, uint32_t tid, uint32_t nthr) {
+    if (!P.rows || P.rows_lds == rt::kNoRowsLds) return;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(rt_dyn_lds) + P.rows_lds);
+    for (uint32_t i = tid; i < P.band_h; i += nthr) dst[i] = P.rows[i];
+}
+
 // shader.rgen:40 seed of pixel w (0..63) of 8x8 tile t of the band.
 __device__ __forceinline__ uint32_t tile_pixel_seed(const rt::TraceParams& P, uint32_t t, uint32_t w) {
     const uint32_t lx = (t % P.tiles_x) * 8u + (w & 7u);
     const uint32_t ly = (t / P.tiles_x) * 8u + (w >> 3);
     const uint32_t gx = P.off_x + lx;
-    const uint32_t gy = P.rows ? load_now(P.rows + (ly < P.band_h ? ly : P.band_h - 1u)) : P.off_y + ly;   // ragged edge: unused
+    const uint32_t gy = band_row(P, ly < P.band_h ? ly : P.band_h - 1u);   // ragged edge: unused
     return tea(tea(P.seed_local ? lx : gx, P.seed_local ? ly : gy), P.number);
 }
 
@@ -647,7 +665,7 @@ __device__ __forceinline__ void camera_ray(const rt::TraceParams& P, const Camer
     UTIL(7, true);
     const uint32_t lx = ps.px & 0xffffu, ly = ps.px >> 16;
     const uint32_t gx = P.off_x + lx;
-    const uint32_t gy = P.rows ? load_now(P.rows + ly) : P.off_y + ly;
+    const uint32_t gy = band_row(P, ly);
     if (MODE == rt::MODE_HASH) ps.seed = sample_seed_hash(ps.pixel_seed, P.sample_base + ps.s);
     else if (P.rng_counter) ps.seed = tea(ps.pixel_seed, P.sample_base + ps.s);
     float ux = float(gx) + rnd(ps.seed);
@@ -1667,6 +1685,7 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
     extern __shared__ float4 lds[];   // the big-sphere table only
     const BigTable big = stage_big(P, lds, threadIdx.x, kTraceBlock);
     stage_walk_params(P, threadIdx.x);
+    stage_rows(P, threadIdx.x, kTraceBlock);
     __syncthreads();
     lbvh_loop<COUNT, LAYOUT_GLOBAL, MODE>(P, reinterpret_cast<const float4*>(P.nodes),
                                           reinterpret_cast<const float4*>(P.leaf_geom), P.leaf_ids,
@@ -1727,6 +1746,7 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
     const float4* mat4 = reinterpret_cast<const float4*>(P.mat);
     const BigTable big = stage_big(P, lds + base, threadIdx.x, kTraceBlock);
     stage_walk_params(P, threadIdx.x);
+    stage_rows(P, threadIdx.x, kTraceBlock);
     __syncthreads();
     lbvh_loop<COUNT, NOCT == 8 ? LAYOUT_OCT : LAYOUT_LDS1, MODE>(
         P, lds, lds + n_node4, reinterpret_cast<const uint32_t*>(lds + n_node4 + n_leaf4), geom4, mat4, big);
@@ -1742,6 +1762,7 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
     if (!IN_LDS) {   // grids too big for LDS: offsets and references from L2 / HBM
         const BigTable big = stage_big(P, lds, threadIdx.x, kTraceBlock);
         stage_walk_params(P, threadIdx.x);
+    stage_rows(P, threadIdx.x, kTraceBlock);
         __syncthreads();
         lbvh_loop<COUNT, COOP ? LAYOUT_GRID_COOP : LAYOUT_GRID_L2, MODE>(P, reinterpret_cast<const float4*>(P.cell_start),
                                             reinterpret_cast<const float4*>(P.grid_rec), P.grid_ids,
@@ -1759,6 +1780,7 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
     for (uint32_t i = threadIdx.x; i < nc1; i += kTraceBlock) cst[i] = P.cell_start[i];
     const BigTable big = stage_big(P, lds + nr + n_id4 + n_cs4, threadIdx.x, kTraceBlock);
     stage_walk_params(P, threadIdx.x);
+    stage_rows(P, threadIdx.x, kTraceBlock);
     if (REC) {   // the winner's gate and shading records in LDS too: {cx, cy, cz, r} + 2 x MatRec float4
         float4* srec = lds + nr + n_id4 + n_cs4 + rt::kBigLdsBytes / 16u;
         float4* smat = srec + P.n_spheres;
@@ -1800,6 +1822,7 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
     }
     const BigTable big = stage_big(P, lds + 2u * rt::kTreeletCap, threadIdx.x, kTraceBlock);
     stage_walk_params(P, threadIdx.x);
+    stage_rows(P, threadIdx.x, kTraceBlock);
     __syncthreads();
     lbvh_loop<COUNT, LAYOUT_TOP, MODE>(P, lds, reinterpret_cast<const float4*>(P.leaf_geom), P.leaf_ids,
                                        reinterpret_cast<const float4*>(P.geom),
