@@ -84,62 +84,107 @@ def host_cpus() -> dict:
             "nproc": os.cpu_count(), "model": model}
 
 
+def _psnr(a, b) -> float | str:
+    import numpy as np
+    mse = float(np.mean((a[..., :3].astype(np.float64) - b[..., :3]) ** 2))
+    return "inf" if mse == 0.0 else round(float(10.0 * np.log10(255.0 ** 2 / mse)), 2)
+
+
 def cpu_baseline(width: int, height: int, spp: int, grid: int, rng_mode: int, gpu_accum=None, gpu_rgba8=None,
-                 target_s: float = 15.0) -> dict:
+                 other=None, target_s: float = 12.0) -> dict:
     """The CPU oracle (C++ restatement of the shaders, brute-force closest hit) on this host's
-    cores, on a bounded sample of the bench frame itself: 8 blocks (one row per thread, a few
-    pixels wide) of the frame at its full spp, spread over the image, sized to ~`target_s` of CPU work from a timed config-1 frame
-    (1920x1080 at 1 spp). The same pixels of the GPU's bench frame (numpy [H, W, 4]) are compared
-    with the oracle's: exact match and PSNR of the rgba8 pixels (BASELINE.json's "PSNR vs CPU ref")."""
+    cores. Config 1 (1920x1080, 1 spp) is timed as a full frame, median of 3, and once more at 16
+    spp (the rate is spp-independent). The reported value is a bounded sample of the
+    bench frame itself: 8 blocks of pixels at its full spp, spread over the image, sized to
+    ~`target_s` of CPU work. Parity: the same pixels of the GPU's bench frame (numpy [H, W, 4]) are
+    compared with the oracle's, bit for bit (BASELINE.json's "PSNR vs CPU ref"). `other` = (accum,
+    rgba8, rng_mode) of the same frame in the other random stream (the bench's side line): its
+    pixels are checked the same way, and when it is the reference's per-pixel LCG stream also
+    against the oracle's literal readings of the GLSL (LIT_RINT: shader.rint:46-55 as written;
+    LIT_ALL: every dot / normalize too): the north star's "PSNR >= 50 dB vs
+    reference at identical seed", measured on the headline frame."""
     import numpy as np
     from oracle import oracle
     oracle.build()
     sc = oracle.generate_scene(0.0, grid)
     cpus = host_cpus()
     threads = cpus["threads"]
-    opts = oracle.options(rng_mode=rng_mode)
-    t0 = time.perf_counter()
-    _, _, st1 = oracle.render(oracle.generate_scene(0.0), oracle.render_call_info(1, 1920, 1080), 1920, 1080,
-                              threads=threads)
-    t1 = time.perf_counter() - t0
+    canon = oracle.generate_scene(0.0)
+    c1 = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        oracle.render(canon, oracle.render_call_info(1, 1920, 1080), 1920, 1080, threads=threads)
+        c1.append(time.perf_counter() - t0)
+    t1 = sorted(c1)[1]
     rate = 1920 * 1080 / t1   # samples/s on the canonical scene at 1 spp (spp-independent, SURVEY.md 8(d))
-    # blocks of `nr` rows x bw pixels (one oracle thread per row), evenly spread
-    nr = min(threads, height)
+    t0 = time.perf_counter()
+    oracle.render(canon, oracle.render_call_info(16, 1920, 1080), 1920, 1080, threads=threads)
+    t16 = time.perf_counter() - t0
+    rate16 = 1920 * 1080 * 16 / t16
+    # blocks of nr rows x bw pixels, evenly spread (the oracle threads over runs of 8 pixels)
+    nr = 16
     cost_scale = max(1.0, len(sc) / 488.0)   # brute force: cost per sample ~ sphere count
     pixels = max(nr, int(rate * target_s / cost_scale / max(1, spp)))
     n_blocks = 8
     bw = max(1, min(width, pixels // (n_blocks * nr)))
     ys = np.linspace(0, height - nr, n_blocks).round().astype(int)
     xs = np.linspace(0, width - bw, n_blocks).round().astype(int)[::-1]
-    samples, dt, same_acc, same_px, sq = 0, 0.0, True, True, []
-    st = [0, 0, 0]
-    for y, x in zip(ys, xs):
-        rows = np.arange(y, y + nr, dtype=np.uint32)
-        t0 = time.perf_counter()
-        acc, out, s = oracle.render(sc, oracle.render_call_info(spp, width, height, (int(x), 0)), bw, len(rows),
-                                    rows=rows, opts=opts, threads=threads)
-        dt += time.perf_counter() - t0
-        samples += bw * len(rows) * spp
-        st = [a + b for a, b in zip(st, s)]
-        if gpu_accum is not None:
-            ga = gpu_accum[y:y + nr, x:x + bw]
-            go = gpu_rgba8[y:y + nr, x:x + bw]
-            same_acc &= bool(np.array_equal(ga, acc))
-            same_px &= bool(np.array_equal(go, out))
-            sq.append(((go[..., :3].astype(np.float64) - out[..., :3]) ** 2).ravel())
+
+    def blocks(rng, lit=oracle.LIT_CONTRACT):
+        """The oracle's render of the blocks: (accum, rgba8, seconds, samples, stats)."""
+        accs, outs, dt, st = [], [], 0.0, [0, 0, 0]
+        for y, x in zip(ys, xs):
+            rows = np.arange(y, y + nr, dtype=np.uint32)
+            t0 = time.perf_counter()
+            acc, out, s = oracle.render(sc, oracle.render_call_info(spp, width, height, (int(x), 0)), bw, nr,
+                                        rows=rows, opts=oracle.options(rng_mode=rng, lit=lit), threads=threads)
+            dt += time.perf_counter() - t0
+            accs.append(acc)
+            outs.append(out)
+            st = [a + b for a, b in zip(st, s)]
+        return np.concatenate(accs), np.concatenate(outs), dt, n_blocks * nr * bw * spp, st
+
+    def gpu_blocks(a):
+        return np.concatenate([a[y:y + nr, x:x + bw] for y, x in zip(ys, xs)])
+
+    acc, out, dt, samples, st = blocks(rng_mode)
+    stream_name = {0: "reference", 2: "hash"}.get(rng_mode, str(rng_mode))
     res = {"value": round(samples / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
            "nproc": cpus["nproc"], "cpu_model": cpus["model"], "affinity": cpus["affinity"],
            "cgroup_quota": cpus["cgroup_quota"],
            "sample": f"{n_blocks} blocks of {nr} rows x {bw} px of the bench frame ({width}x{height}, {spp} spp, "
-                     f"depth 50, {len(sc)} spheres, {'hash' if rng_mode == 2 else 'reference'} stream), brute-force "
-                     f"closest hit, {threads} threads, {dt:.2f} s; config 1 frame (1920x1080, 1 spp) alone "
-                     f"{t1:.2f} s = {rate / 1e6:.3f} Msamples/s; {st[0] / max(1, st[1]):.3f} segments/sample",
-           "config1_frame_s": round(t1, 3), "config1_msamples_per_s": round(rate / 1e6, 4)}
+                     f"depth 50, {len(sc)} spheres, {stream_name} stream), brute-force closest hit, {threads} "
+                     f"threads, {dt:.2f} s; config 1 frame (1920x1080, 1 spp, canonical scene) median of 3 "
+                     f"{t1:.3f} s = {rate / 1e6:.3f} Msamples/s; at 16 spp {t16:.2f} s = {rate16 / 1e6:.3f} "
+                     f"Msamples/s; {st[0] / max(1, st[1]):.3f} segments/sample",
+           "config1_frame_s": round(t1, 3), "config1_runs": [round(v, 3) for v in c1],
+           "config1_msamples_per_s": round(rate / 1e6, 4), "spp16_frame_s": round(t16, 3),
+           "spp16_msamples_per_s": round(rate16 / 1e6, 4),
+           "spp_independent": bool(abs(rate16 / rate - 1.0) < 0.25)}
     if gpu_accum is not None:
-        mse = float(np.mean(np.concatenate(sq))) if sq else 0.0
-        res["parity"] = {"pixels": int(n_blocks * nr * bw), "accum_bit_exact": same_acc,
-                         "rgba8_equal": same_px,
-                         "psnr_db": "inf" if mse == 0.0 else round(float(10.0 * np.log10(255.0 ** 2 / mse)), 2)}
+        ga, go = gpu_blocks(gpu_accum), gpu_blocks(gpu_rgba8)
+        res["parity"] = {"pixels": int(n_blocks * nr * bw), "stream": stream_name,
+                         "accum_bit_exact": bool(np.array_equal(ga, acc)),
+                         "rgba8_equal": bool(np.array_equal(go, out)), "psnr_db": _psnr(go, out)}
+        if other is not None:
+            o_acc, o_px, o_rng = other
+            oa, oo, odt, _, _ = blocks(o_rng)
+            ga, go = gpu_blocks(o_acc), gpu_blocks(o_px)
+            leg = {"stream": {0: "reference", 2: "hash"}.get(o_rng, str(o_rng)),
+                   "accum_bit_exact": bool(np.array_equal(ga, oa)), "rgba8_equal": bool(np.array_equal(go, oo)),
+                   "psnr_db": _psnr(go, oo), "cpu_s": round(odt, 2)}
+            if o_rng == 0:
+                leg["vs_literal_glsl"] = {}
+                for name, lit in (("rint", oracle.LIT_RINT), ("all", oracle.LIT_ALL)):
+                    la, lo, ldt, _, _ = blocks(0, lit)
+                    leg["vs_literal_glsl"][name] = {
+                        "psnr_db": _psnr(go, lo), "rgba8_identical": round(float(np.mean(np.all(go[..., :3] == lo[..., :3], -1))), 4),
+                        "accum_bit_identical": round(float(np.mean(np.all(ga[..., :3] == la[..., :3], -1))), 4),
+                        "cpu_s": round(ldt, 2)}
+                leg["vs_literal_glsl"]["what"] = (
+                    "the GPU's reference-stream frame (identical seed) against the oracle reading shader.rint:46-55 "
+                    "as written (rint) and every dot / normalize as written too (all); north star: >= 50 dB")
+            res["parity"]["reference_stream" if o_rng == 0 else "hash_stream"] = leg
     return res
 
 
@@ -170,6 +215,8 @@ WALK_NAMES = {   # rt_debug_launch_info form -> (kernel, walk)
     "lbvh-treelet": ("rt_trace_top_kernel", "LBVH, LDS treelet over L2 subtrees"),
     "lbvh-global": ("rt_trace_global_kernel", "LBVH, every node from L2"),
     "grid-lds": ("rt_trace_grid_kernel<grid in LDS>", "uniform grid (3D DDA), staged in LDS"),
+    "grid-lds-rec": ("rt_trace_grid_kernel<grid + shading records in LDS>",
+                     "uniform grid (3D DDA) staged in LDS, with the winner's gate and shading records"),
     "grid-global": ("rt_trace_grid_kernel<grid from L2>", "uniform grid (3D DDA), from L2"),
     "grid-lds-coop": ("rt_trace_grid_kernel<grid in LDS, wave-cooperative>",
                       "uniform grid (3D DDA) staged in LDS, reference tests spread over the wave's lanes"),
@@ -217,6 +264,108 @@ def roofline_block(cs, scale, form: str, kernel_ms: float, step_ms: float, n_gpu
     return roof
 
 
+def config5_line(dev, steps: int, warmup: int, sha: str, count_spp: int = 20, oracle_check: bool = True) -> dict:
+    """BASELINE config 5 on this GPU: 3840x2160, 99 860 spheres (generateRandomScene grid 316x316),
+    1 000 spp, the counter-based stream; every frame rebuilds the scene on the device (Morton LBVH +
+    grid, rt_build.hip) as the reference rebuilds BLAS/TLAS, then renders it (grid walked from L2).
+    Timed like the headline (frames back to back between syncs); the trace kernel from the
+    library's HIP events; image checks: a 64-row band through the default walk equals the LDS
+    treelet walk bit for bit, and 4 blocks of the timed frame equal the CPU oracle bit for bit."""
+    import numpy as np
+    import torch
+
+    import rtvk
+    from rtvk import abi
+    W, H, spp, grid = CONFIGS[5][:4]
+    scene = rtvk.generateRandomScene(0.0, grid)
+    r = rtvk.Renderer(dev.index)
+    stream = torch.cuda.Stream(device=dev)
+    opts = rtvk.make_options(accel=abi.RT_ACCEL_LBVH, rng_mode=abi.RT_RNG_SAMPLE_HASH)
+    rci = rtvk.canonical_render_call_info(spp, W, H)
+    acc = torch.zeros((H, W, 4), dtype=torch.float32, device=dev)
+    out = torch.zeros((H, W, 4), dtype=torch.uint8, device=dev)
+
+    def frame():
+        with torch.cuda.stream(stream):
+            r.set_scene(scene, stream=stream)
+            r.render_device(rci, acc, out, options=opts, stream=stream)
+
+    for _ in range(max(1, warmup)):
+        frame()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        frame()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    ks = r.kernel_times(steps)
+    kernel_ms = sum(ks) / max(1, len(ks))
+    step_ms = elapsed / steps * 1e3
+    info = r.launch_info()
+    device_built = r.scene_array(8)["device_built"]
+    frame_np = (acc.cpu().numpy(), out.cpu().numpy())
+    st = r.stats()
+    cnt = rtvk.make_options(accel=abi.RT_ACCEL_LBVH, rng_mode=abi.RT_RNG_SAMPLE_HASH, count_tests=True)
+    r.render_device(rtvk.canonical_render_call_info(count_spp, W, H), acc, out, options=cnt, stream=stream)
+    torch.cuda.synchronize(dev)
+    cs = r.stats()
+    key = f"lbvh-hash-{W}x{H}-{spp}spp-grid{grid}-n1"
+    roof = roofline_block(cs, spp / count_spp, info["form"], kernel_ms, step_ms, 1, sha, pmc_record(key, sha),
+                          f"mean trace-kernel duration of the {len(ks)} timed launches (HIP events on the launch stream)")
+    # walk check: a 64-row band, default walk (grid from L2) vs the LDS treelet over L2 subtrees
+    y0 = 1056
+    band = rtvk.canonical_render_call_info(spp, W, H)
+    band.offset.y = y0
+    ba = [torch.zeros((64, W, 4), dtype=torch.float32, device=dev) for _ in range(2)]
+    bo = [torch.zeros((64, W, 4), dtype=torch.uint8, device=dev) for _ in range(2)]
+    forms = []
+    for i, form in enumerate((0, 8)):
+        o = rtvk.make_options(accel=abi.RT_ACCEL_LBVH, rng_mode=abi.RT_RNG_SAMPLE_HASH)
+        o.reserved[1] = form
+        r.render_device(band, ba[i], bo[i], options=o, stream=stream)
+        torch.cuda.synchronize(dev)
+        forms.append(r.launch_info()["form"])
+    band_equal = bool(torch.equal(ba[0], ba[1]) and torch.equal(bo[0], bo[1]))
+    band_vs_frame = bool(np.array_equal(ba[0].cpu().numpy(), frame_np[0][y0:y0 + 64]))
+    res = {"workload": "BASELINE config 5: 3840x2160, 99 860 spheres, 1000 spp, depth 50, hash stream, "
+                       "device LBVH + grid rebuilt every frame",
+           "value": round(W * H * spp * steps / elapsed / 1e6, 2), "unit": "Msamples/s", "steps": steps,
+           "warmup": warmup, "ms_per_step": round(step_ms, 3), "kernel_ms": round(kernel_ms, 3),
+           "step_minus_kernel_ms": round(step_ms - kernel_ms, 3),
+           "accel": info["form"], "structure_build": "device" if device_built else "host",
+           "sample_chunks": info["chunks"], "head_chunks": info["head_chunks"],
+           "segments_per_sample": round(st.segments / max(1, st.samples), 4), "roofline": roof,
+           "walk_check": {"rows": f"{y0}..{y0 + 63}", "forms": forms, "bit_equal": band_equal,
+                          "band_equals_timed_frame": band_vs_frame}}
+    if oracle_check:
+        from oracle import oracle
+        oracle.build()
+        sc = oracle.generate_scene(0.0, grid)
+        same_a = same_o = True
+        nb, bh, bw = 4, 4, 8
+        t0 = time.perf_counter()
+        for y, x in zip(np.linspace(0, H - bh, nb).round().astype(int), np.linspace(0, W - bw, nb).round().astype(int)):
+            rows = np.arange(y, y + bh, dtype=np.uint32)
+            oa, oo, _ = oracle.render(sc, oracle.render_call_info(spp, W, H, (int(x), 0)), bw, bh, rows=rows,
+                                      opts=oracle.options(rng_mode=abi.RT_RNG_SAMPLE_HASH), threads=host_cpus()["threads"])
+            same_a &= bool(np.array_equal(frame_np[0][y:y + bh, x:x + bw], oa))
+            same_o &= bool(np.array_equal(frame_np[1][y:y + bh, x:x + bw], oo))
+        res["oracle_check"] = {"pixels": nb * bh * bw, "accum_bit_exact": same_a, "rgba8_equal": same_o,
+                               "cpu_s": round(time.perf_counter() - t0, 2),
+                               "what": f"{nb} blocks of {bh} rows x {bw} px of the timed frame vs the CPU oracle "
+                                       "(brute force over all 99 860 spheres)"}
+    r.close()
+    return res
+
+
+def env_knobs() -> dict:
+    """RT_* variables of this process. The library reads only RT_RNG (ray_trace(), not this bench's
+    path) and RT_BVH_BUILD; rtvk reads RT_LIB (another library); bench.py reads RT_BENCH_BACKEND
+    (the gloo rehearsal, marked in the line). Any other, and RT_BVH_BUILD / RT_LIB, would make the
+    line describe a build or configuration other than the shipped one: refused."""
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith("RT_")}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -245,6 +394,9 @@ def main() -> int:
     ap.add_argument("--walk", type=int, default=0,
                     help="walk form (A/B only): 0 auto, 6 one LDS LBVH copy, 8 octant LBVH copies, 10 LBVH from L2, "
                          "12 grid")
+    ap.add_argument("--no-config5", action="store_true", help="skip the BASELINE config 5 side line")
+    ap.add_argument("--no-rebuild-check", action="store_true",
+                    help="skip recompiling the library on this machine and comparing it with the shipped binary")
     ap.add_argument("--inflight", type=int, default=1,
                     help="frames in flight (single path): contexts + streams used round robin. Default 1: with "
                          "sample chunks the tail is short and a second frame only interferes (DESIGN.md §6)")
@@ -256,7 +408,13 @@ def main() -> int:
     accel_name = args.accel or accel0
     if args.profile:
         args.inflight = 1
-
+    knobs = env_knobs()
+    bad = sorted(set(knobs) - {"RT_RNG", "RT_BENCH_BACKEND"})
+    if bad:
+        print(f"error: {', '.join(bad)} set: the line would not describe the shipped build / configuration "
+              "(tuning goes through rt_debug_tune in tests and A/B scripts, never through the environment)",
+              file=sys.stderr)
+        return 2
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -286,6 +444,17 @@ def main() -> int:
     if mode == "single" and args.gpus != 1:
         print("error: --path single renders on one GPU; use --gpus 1", file=sys.stderr)
         return 2
+    rebuild = None
+    if not args.no_rebuild_check and not args.profile and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        # Build provenance: compile the library from this tree's sources on this machine and compare
+        # it with the shipped binary; when they differ, the fresh binary replaces it before it loads.
+        import shutil
+        import __graft_entry__ as ge
+        rebuild = ge.rebuild_check()
+        if not rebuild["identical"]:
+            shutil.copy2(rebuild["box_built"], ROOT / "ray-tracing-gpu-vulkan_amd" / "lib" / "librt_mi355x.so")
+            rebuild["replaced_shipped"] = True
+        shutil.rmtree(Path(rebuild.pop("box_built")).parents[2], ignore_errors=True)
     n_gpus = args.gpus
     # RCCL (backend "nccl"); RT_BENCH_BACKEND=gloo rehearses N ranks sharing the visible GPUs
     # (bands staged through host memory): a test of the N > 1 code path, never a reported number.
@@ -407,6 +576,16 @@ def main() -> int:
         kernel_ms = sum(ks) / max(1, len(ks))
         k_basis = (f"mean trace-kernel duration of the {len(ks)} launches of the timed region (HIP events "
                    f"recorded by the library around the kernel on its launch stream)")
+        if len(slots) > 1:
+            # with frames in flight a launch's events also span the wait for CUs the other slot's
+            # frame holds: time 3 frames alone (one at a time) for the kernel's own duration
+            for _ in range(3):
+                slots[0].frame()
+                sync_all()
+            ks = slots[0].renderer.kernel_times(3)
+            kernel_ms = sum(ks) / max(1, len(ks))
+            k_basis = (f"mean trace-kernel duration of 3 frames rendered one at a time after the timed region "
+                       f"(HIP events on the launch stream); the timed region had {len(slots)} frames in flight")
     if mode == "per-process":
         t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -517,7 +696,8 @@ def main() -> int:
             "scene_setup_ms": round(t_scene * 1e3, 2),
             "msegments_per_s": round(st.segments / max(1, st.samples) * value, 2),
             "roofline": roof,
-            "build": abi.build_info(),
+            "build": {**abi.build_info(), "env": knobs,
+                      "rebuild": rebuild if rebuild is not None else "skipped"},
             **({"rehearsal": f"{backend} backend, {world} ranks sharing {n_vis} GPU(s): "
                                "code-path test, not a measurement"} if backend != "nccl" and mode == "per-process" else {}),
             "context": {"reference_rx6800xt_vulkan_rt_msamples": 1658.9,
@@ -542,7 +722,8 @@ def main() -> int:
         if n_gpus == 1:
             frame_np = (fa.cpu().numpy(), fo.cpu().numpy())
     # Side lines (single GPU): the same frame with the other random stream and with the LBVH walk
-    # (BASELINE config 3 names LBVH traversal), and BASELINE config 2 as specified.
+    # (BASELINE config 3 names LBVH traversal), and BASELINE configs 2 and 5 as specified.
+    other_frame = None
     if mode == "single" and not args.no_side_lines and not args.profile:
         def time_frames(o, w, h, s, n):
             a = torch.zeros((h, w, 4), dtype=torch.float32, device=dev)
@@ -559,8 +740,9 @@ def main() -> int:
             return e0.elapsed_time(e1) / n, a, b
         if accel != abi.RT_ACCEL_BRUTE:
             other = abi.RT_RNG_PIXEL_STREAM if rng_mode == abi.RT_RNG_SAMPLE_HASH else abi.RT_RNG_SAMPLE_HASH
-            oms, _, ob = time_frames(rtvk.make_options(accel=accel, rng_mode=other), W, H, spp, 1)
+            oms, oa, ob = time_frames(rtvk.make_options(accel=accel, rng_mode=other), W, H, spp, 1)
             o_np = ob.cpu().numpy()
+            other_frame = (oa.cpu().numpy(), o_np, other)
             mse = float(np.mean((o_np[..., :3].astype(np.float64) - frame_np[1][..., :3]) ** 2))
             result["reference_stream" if other == abi.RT_RNG_PIXEL_STREAM else "hash_stream"] = {
                 "value": round(samples_per_step / (oms * 1e-3) / 1e6, 2), "unit": "Msamples/s",
@@ -601,8 +783,10 @@ def main() -> int:
                 "roofline": {"bound": "valu-fp32", "achieved": round(bflops / (bms * 1e-3) / 1e12, 3),
                              "peak": VALU_FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                              "frac": round(bflops / (bms * 1e-3) / 1e12 / VALU_FP32_PEAK_TFLOPS, 4)}}
+        if args.config == 3 and not args.no_config5 and (W, H, spp, grid) == CONFIGS[3][:4]:
+            result["config5"] = config5_line(dev, steps=3, warmup=1, sha=result["roofline"]["lib_sha256"])
     if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline and not args.profile:
-        result["cpu_baseline"] = cpu_baseline(W, H, spp, grid, rng_mode, frame_np[0], frame_np[1])
+        result["cpu_baseline"] = cpu_baseline(W, H, spp, grid, rng_mode, frame_np[0], frame_np[1], other=other_frame)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if mode == "multi":

@@ -141,13 +141,18 @@ int rt_canonical_render_call_info(uint32_t spp, uint32_t width, uint32_t height,
 int rt_context_create(int device, rt_context** out);
 int rt_context_destroy(rt_context* ctx);
 /* Uploads `count` spheres (host memory) and builds the closest-hit structure: a binned-SAH tree
- * built on the host for scenes of up to 4096 spheres (the cheaper walk), the parallel device
- * LBVH build (rt_build.hip) above that. RT_BVH_BUILD=gpu|sah|morton forces one builder (A/B).
- * `spheres` may be reused as soon as it returns. The new scene is ordered on `stream`: launches
- * already queued on `stream` render the old one (a host build runs while they execute, the
- * upload is queued behind them); launches on other streams are waited for first. */
+ * built on the host for scenes of up to 1024 spheres (the cheaper walk), the parallel device
+ * LBVH build (rt_build.hip) + device grid above that. RT_BVH_BUILD=gpu|sah|morton forces one
+ * builder (A/B). `spheres` may be reused as soon as it returns. Launches already queued render
+ * the old scene; every later launch of ctx renders the new one, on any stream. Host-built scenes
+ * are built while queued launches execute and uploaded in order on `stream`. Device builds run on
+ * the context's own build stream into the one of two scene arenas that no queued launch reads
+ * (the one used two scenes ago, whose launches they wait for), so frame k + 1's build overlaps
+ * frame k's tail; the call returns once the build's summary is back on the host (no wait for
+ * queued launches) and its grid build is queued. */
 int rt_set_scene(rt_context* ctx, const Sphere* spheres, uint32_t count, void* stream);
-/* As rt_set_scene, spheres already in DEVICE memory (read during the call only). */
+/* As rt_set_scene, spheres already in DEVICE memory, written by earlier work on `stream` (the
+ * build copies them after that work; the caller may reuse them once the call returns). */
 int rt_set_scene_device(rt_context* ctx, const Sphere* d_spheres, uint32_t count, void* stream);
 /*
  * Per-frame update of an animated scene (the reference rebuilds BLAS/TLAS every frame,
@@ -196,7 +201,9 @@ typedef struct rt_multi rt_multi;
 int rt_multi_create(uint32_t gpu_count, rt_multi** out);
 int rt_multi_destroy(rt_multi* m);
 int rt_multi_device_count(const rt_multi* m, uint32_t* n);
-/* rt_set_scene on every device (host spheres). */
+/* The scene on every device (host spheres), as rt_set_scene: every device's build is issued before
+ * any is waited for (device builds run on all GPUs at once), and a host-built scene is built once
+ * and uploaded to every device. */
 int rt_multi_set_scene(rt_multi* m, const Sphere* spheres, uint32_t count);
 /*
  * One frame of the whole image rci->image_size (rci->offset ignored). The rows are cut into
@@ -248,8 +255,18 @@ int rt_debug_exact_exhaustive(int device, uint64_t* mismatches3);
  * min(capacity, launches kept). Synchronises on those events. */
 int rt_debug_kernel_times(rt_context* ctx, float* out_ms, uint32_t capacity, uint32_t* count);
 /* Build provenance of this library: "sources_sha256=<16 hex of the sources it was compiled
- * from>;arch=gfx950;flags=...". Static string. */
+ * from>;arch=<offload arch>;flags=<compiler flags>;variant=<A/B variant flags, empty for the
+ * shipped build>". Static string. */
 const char* rt_build_info(void);
+/* Diagnostic (tests, A/B timing): sets one launch-plan parameter of ctx (value -1 restores the
+ * default). None of them changes an image; the defaults are the measured best. Keys: "grid" (0: no
+ * uniform grid), "grid_scale", "grid_coop" (1: wave-cooperative grid walk), "grid_rec" (0: no
+ * shading records in LDS), "grid_full_slack", "units_per_lane", "unit_min_samples",
+ * "sample_chunks", "head_chunks", "tail_tiles_pm", "schedule" (0 LPT, 1 row-major, 2 LPT by tile
+ * sum), "refill_reserve", "isolate_tiles", "sah_knobs". Unknown keys: RT_ERR_INVALID_ARGUMENT.
+ * Scene-build keys (grid, grid_scale, sah_knobs) apply from the next rt_set_scene. The library
+ * reads no environment variable for any of them. */
+int rt_debug_tune(rt_context* ctx, const char* key, double value);
 /* Diagnostic: of ctx's last launch, {sample chunks per pixel (low 16 bits: of the LPT order's tail
  * tiles; high 16 bits: of its head tiles, 0 when the launch had no head), the kernel form it ran
  * (rt_internal.h ACCEL_*; before any launch: the scene's default form), its dynamic LDS bytes, CU

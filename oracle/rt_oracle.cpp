@@ -37,6 +37,7 @@
  *   * pow(x, 2.0)    = x*x (rchit:131, Q7);  pow(x, 5.0) = NaN for x < 0 else (x*x)*(x*x)*x (Q8)
  *   * everything else exactly as written in GLSL, left to right, one rounding per operator.
  */
+#include <algorithm>
 #include <atomic>
 #include <cmath>
 #include <cstdint>
@@ -596,13 +597,18 @@ int orc_render(const Sphere* spheres, uint32_t n, const RenderCallInfo* rci, con
     job.accum = accum; job.out = out;
     if (!job.opt.accumulate) std::memset(accum, 0, size_t(band_w) * band_h * 4 * sizeof(float));
     unsigned nt = threads > 0 ? unsigned(threads) : std::max(1u, std::thread::hardware_concurrency());
-    std::atomic<uint32_t> next_row{0};
+    // pixels are independent: threads take runs of up to 8 pixels of a row, so narrow bands (a
+    // few rows of a high-spp frame) still use every thread
+    const uint32_t runs_per_row = (band_w + 7u) / 8u;
+    const uint64_t n_runs = uint64_t(runs_per_row) * band_h;
+    std::atomic<uint64_t> next_run{0};
     std::vector<Counters> cnts(nt);
     auto worker = [&](unsigned tid) {
         for (;;) {
-            uint32_t y = next_row.fetch_add(1);
-            if (y >= band_h) break;
-            for (uint32_t x = 0; x < band_w; x++) {
+            const uint64_t r = next_run.fetch_add(1);
+            if (r >= n_runs) break;
+            const uint32_t y = uint32_t(r / runs_per_row), x0 = uint32_t(r % runs_per_row) * 8u;
+            for (uint32_t x = x0; x < std::min(band_w, x0 + 8u); x++) {
                 if (lit == LIT_CONTRACT) render_pixel<LIT_CONTRACT>(job, x, y, cnts[tid]);
                 else if (lit == LIT_RINT) render_pixel<LIT_RINT>(job, x, y, cnts[tid]);
                 else render_pixel<LIT_ALL>(job, x, y, cnts[tid]);

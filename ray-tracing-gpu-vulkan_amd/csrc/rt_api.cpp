@@ -41,13 +41,58 @@ hipError_t launch_debug_math(int op, const float* in, float* out, uint32_t n, hi
 hipError_t launch_debug_exact(unsigned long long* bad, hipStream_t st);
 }  // namespace rt
 
+// Launch-plan parameters that tests and A/B scripts vary through rt_debug_tune() (per context; the
+// shipped defaults are the measured best). None changes an image. The library reads
+// no environment variable for them: only RT_RNG (ray_trace) and RT_BVH_BUILD are read, both
+// documented.
+struct Tuning {
+    static constexpr double kUnset = -1.0;
+    double grid = kUnset;               // 0: no uniform grid (LBVH walks only)
+    double grid_scale = kUnset;         // cell size scale (rt_grid.h kGridCellScale)
+    double grid_coop = kUnset;          // 1: the wave-cooperative grid walk
+    double grid_rec = kUnset;           // 0: no shading records in the LDS grid kernel's LDS
+    double grid_full_slack = kUnset;    // 1: the full cull slack in grid walks
+    double units_per_lane = kUnset;     // sample-chunk targets (counter-based stream)
+    double unit_min_samples = kUnset;
+    double sample_chunks = kUnset;      // forced chunk count (tail count when the LPT order is split)
+    double head_chunks = kUnset;        // head / tail split of the LPT order
+    double tail_tiles_pm = kUnset;
+    double schedule = kUnset;           // 0 LPT (longest unit chain), 1 row-major, 2 LPT by tile sum
+    double refill_reserve = kUnset;     // units handed out one by one at the end of the queue
+    double isolate_tiles = kUnset;      // reference stream: waves on the first LPT blocks take no more
+    double sah_knobs = kUnset;          // host SAH builder variants (rt_bvh.h)
+    static double get(double v, double def) { return v == kUnset ? def : v; }
+};
+
+// One arena of device-built scenes (rt_context::slot; rt_api.cpp device_build_begin).
+struct SceneSlot {
+    rt::DeviceScene scene;            // its arrays (pointers into mem / grid_mem) and counts
+    void* mem = nullptr;              // every per-sphere array of the build, one allocation
+    uint32_t cap_n = 0;               // spheres it holds
+    void* grid_mem = nullptr;         // cell offsets, fill cursor, references, ids, scan scratch
+    size_t grid_cap = 0;              // bytes
+    hipEvent_t ev_free = nullptr;     // recorded after every launch that reads this arena
+    bool used = false;                // ev_free has been recorded
+};
+
 struct rt_context {
     int device = 0;
+    Tuning tune;
     int cu_count = 0;
-    rt::DeviceScene scene;
+    rt::DeviceScene scene;                       // the current scene (host blob or an arena)
     bool scene_set = false;                      // a set/refit call has succeeded (RT_ERR_NO_SCENE)
-    std::vector<void*> scene_allocs;
-    std::vector<void*> grid_allocs;              // device-built grid arrays (rebuilt by every refit)
+    // device-built scenes: two arenas used alternately, built on the context's own stream
+    SceneSlot slot[2];
+    int slot_cur = -1;                           // arena of the current scene (-1: host-built / none)
+    hipStream_t build_stream = nullptr;
+    hipEvent_t ev_summary = nullptr;             // the build's summary has reached pinned memory
+    hipEvent_t ev_caller = nullptr;              // device spheres: the caller's stream reached the call
+    rt::BuildSummary* summary = nullptr;         // pinned
+    void* sph_stage = nullptr;                   // pinned staging of host spheres
+    size_t sph_stage_cap = 0;
+    bool pending = false;                        // a build begun, not yet ended (rt_multi_set_scene)
+    int pending_slot = 0;
+    uint32_t pending_count = 0;
     rt::Counters* counters = nullptr;            // device
     float* big_tab = nullptr;                    // device, in the counters' allocation (TraceParams::big_tab)
     // Every device operation of a context (scene upload / build, render) is ordered after the
@@ -169,25 +214,16 @@ constexpr uint32_t kMaxLdsNodes = 0x7fffeu / 8u;
 void size_lds_forms(rt_context* ctx) {
     const rt::DeviceScene& d = ctx->scene;
     const size_t tree = size_t(2 * d.n_nodes + d.n_leaf + (d.n_leaf + 3) / 4) * 16;
-    const size_t lds1 = tree + rt::kBigLdsBytes;   // shading records stay in HBM (rt_kernels.hip)
+    const size_t lds1 = tree;   // shading records stay in HBM (rt_kernels.hip)
     const bool ok = d.n_nodes && d.n_leaf <= kMaxLdsLeafSlots && d.n_nodes <= kMaxLdsNodes;
     ctx->lds1_bytes = (ok && lds1 <= kMaxLdsBytes) ? lds1 : 0;
     const size_t oct = lds1 + size_t(14u) * d.n_nodes * 16u;
     ctx->oct_bytes = (ok && oct <= kMaxLdsBytes) ? oct : 0;
     const rt::GridInfo& g = d.grid;
-    const size_t grid = (size_t(g.n_refs) + (g.n_refs + 3) / 4 + (size_t(g.n_cells) + 4) / 4) * 16 + rt::kBigLdsBytes;
+    const size_t grid = (size_t(g.n_refs) + (g.n_refs + 3) / 4 + (size_t(g.n_cells) + 4) / 4) * 16;
     ctx->grid_bytes = (g.n_refs && grid + rt::kLaneSumLdsBytes <= kMaxLdsBytes) ? grid : 0;
 }
 
-void free_scene(rt_context* ctx) {
-    for (void* p : ctx->scene_allocs) (void)hipFree(p);
-    ctx->scene_allocs.clear();
-    for (void* p : ctx->grid_allocs) (void)hipFree(p);
-    ctx->grid_allocs.clear();
-    ctx->scene = rt::DeviceScene{};
-    ctx->has_grid = false;
-    ctx->grid_bytes = 0;
-}
 
 // Stream chaining of a context's device operations (rt_context::ev_last).
 int order_on(rt_context* ctx, hipStream_t st) {
@@ -441,7 +477,16 @@ int rt_context_destroy(rt_context* ctx) {
     if (!ctx) return RT_OK;
     DeviceGuard g(ctx->device);
     (void)hipDeviceSynchronize();
-    free_scene(ctx);
+    for (SceneSlot& s : ctx->slot) {
+        if (s.mem) (void)hipFree(s.mem);
+        if (s.grid_mem) (void)hipFree(s.grid_mem);
+        if (s.ev_free) (void)hipEventDestroy(s.ev_free);
+    }
+    if (ctx->build_stream) (void)hipStreamDestroy(ctx->build_stream);
+    if (ctx->ev_summary) (void)hipEventDestroy(ctx->ev_summary);
+    if (ctx->ev_caller) (void)hipEventDestroy(ctx->ev_caller);
+    if (ctx->summary) (void)hipHostFree(ctx->summary);
+    if (ctx->sph_stage) (void)hipHostFree(ctx->sph_stage);
     rt::build_release(ctx->ws);
     rt::schedule_release(ctx->sched);
     if (ctx->blob) (void)hipFree(ctx->blob);
@@ -464,170 +509,295 @@ int rt_context_destroy(rt_context* ctx) {
 
 namespace {
 
-// Host-built tree (rt_bvh.cpp, binned SAH or Morton split): the default for scenes whose tree and
-// records fit LDS, and the A/B reference of the device builder.
-int set_scene_host(rt_context* ctx, const Sphere* spheres, uint32_t count, hipStream_t st, bool sah) {
-    try {
-        if (ctx->gpu_tree || !ctx->scene_allocs.empty()) {   // leaving a device-built scene
-            RT_HIP(hipDeviceSynchronize());
-            free_scene(ctx);
-        }
-        ctx->scene = rt::DeviceScene{};
-        ctx->has_grid = false;
-        ctx->gpu_tree = false;
-        BlobUpload up;
-        std::vector<rt::GeomRec> geom(count);
-        std::vector<float> radius(count);
-        std::vector<rt::MatRec> mat(count);
-        ctx->colours_unit = true;
-        for (uint32_t i = 0; i < count; i++) {
-            const Sphere& s = spheres[i];
-            if (!rt::colours_in_unit(s)) ctx->colours_unit = false;
-            const float r = s.geometry.w;
-            geom[i] = rt::GeomRec{s.geometry.x, s.geometry.y, s.geometry.z, r * r};
-            radius[i] = r;
-            mat[i] = rt::make_mat(s.colors[0].x, s.colors[0].y, s.colors[0].z, s.materialSpecificAttribute,
+// ---- host-built scenes ---------------------------------------------------------------------
+// Host-built tree (rt_bvh.cpp, binned SAH or Morton split) + host uniform grid: the default for
+// scenes whose tree and records fit LDS, and the A/B reference of the device builder. Built once
+// into a HostPackage, which any number of contexts upload (rt_multi builds it once for every GPU).
+}  // namespace
+
+namespace rt {
+struct HostPackage {
+    uint32_t count = 0;
+    std::vector<GeomRec> geom;
+    std::vector<float> radius;
+    std::vector<MatRec> mat;
+    HostBvh bvh;                        // nodes padded for pad_radius, leaf ids padded to 4
+    std::vector<BvhNode> nodes_host;    // unpadded (far-camera re-pad)
+    std::vector<BvhNode> oct;           // 8 near-child-first orders of the padded nodes
+    HostGrid grid;
+    bool has_grid = false;
+    bool colours_unit = true;
+    float scene_radius = 0.0f, pad_radius = 0.0f;
+};
+void HostPackageDeleter::operator()(HostPackage* p) const { delete p; }
+}  // namespace rt
+
+namespace {
+
+rt::HostPackagePtr build_host_package(const rt_context* ctx, const Sphere* spheres, uint32_t count, bool sah) {
+    rt::HostPackagePtr pk(new rt::HostPackage());
+    pk->count = count;
+    pk->geom.resize(count);
+    pk->radius.resize(count);
+    pk->mat.resize(count);
+    for (uint32_t i = 0; i < count; i++) {
+        const Sphere& s = spheres[i];
+        if (!rt::colours_in_unit(s)) pk->colours_unit = false;
+        const float r = s.geometry.w;
+        pk->geom[i] = rt::GeomRec{s.geometry.x, s.geometry.y, s.geometry.z, r * r};
+        pk->radius[i] = r;
+        pk->mat[i] = rt::make_mat(s.colors[0].x, s.colors[0].y, s.colors[0].z, s.materialSpecificAttribute,
                                   s.colors[1].x, s.colors[1].y, s.colors[1].z, s.materialType, s.textureType);
-        }
-        // Brute-force padding: whole batches of 8; the pad spheres sit 1e19 away with
-        // radius^2 = -1e38, so D = b^2 - a(|oc|^2 + 1e38) < 0 for every ray.
-        while (geom.size() % 8) geom.push_back(rt::GeomRec{0.0f, 1e19f, 0.0f, -1e38f});
-        rt::HostBvh bvh;
-        rt::build_lbvh_host(spheres, count, bvh, sah);
-        rt::DeviceScene& d = ctx->scene;
-        d.n_spheres = count;
-        up.add(geom, &d.geom);
-        up.add(radius, &d.radius);
-        d.small_rmax = bvh.small_rmax;
-        d.small_rmin = bvh.small_rmin;
-        up.add(mat, &d.mat);
-        d.n_big = uint32_t(bvh.big_ids.size());
-        up.add(bvh.big_ids, &d.big_ids);
-        d.n_nodes = uint32_t(bvh.nodes.size());
-        d.n_leaf = uint32_t(bvh.leaf_ids.size());
-        // leaf ids are read as uint4: pad to a multiple of 4
-        while (bvh.leaf_ids.size() % 4) bvh.leaf_ids.push_back(0u);
-        // pad node boxes for origins within the scene radius (hit points) and a nearby camera
-        float R = 0.0f;
-        for (uint32_t i = 0; i < count; i++) {
-            const rt_vec4& gg = spheres[i].geometry;
-            R = std::max(R, std::sqrt(gg.x * gg.x + gg.y * gg.y + gg.z * gg.z) + std::fabs(gg.w));
-        }
-        ctx->scene_radius = R;
-        ctx->pad_radius = R * 1.01f + 100.0f;
-        ctx->padded_for = ctx->pad_radius;
-        ctx->nodes_host = bvh.nodes;
-        pad_nodes(ctx->nodes_host, bvh.nodes, pad_for(ctx->pad_radius));
-        std::vector<rt::BvhNode> oct;
-        make_octant_orders(bvh.nodes, oct);
-        up.add(oct, &d.nodes_oct);
-        // Uniform grid (rt_grid.h) when the scene suits one: the default walk.
-        // RT_GRID=0 disables it, RT_GRID_SCALE scales the cell size (A/B).
-        rt::HostGrid grid;
-        const char* ge = std::getenv("RT_GRID");
-        const float gscale = std::getenv("RT_GRID_SCALE") ? float(std::atof(std::getenv("RT_GRID_SCALE"))) : rt::kGridCellScale;
-        if (!(ge && std::strcmp(ge, "0") == 0) &&
-            rt::build_grid_host(spheres, count, bvh.big_ids, 64.0f * 0x1p-24f * ctx->pad_radius, gscale, 1u << 22,
-                                grid)) {
-            d.grid = grid.info;
-            up.add(grid.cell_start, &d.cell_start);
-            up.add(grid.rec, &d.grid_rec);
-            up.add(grid.ids, &d.grid_ids);
-            ctx->grid_pad_radius = ctx->pad_radius;
-            ctx->has_grid = true;
-        }
-        size_lds_forms(ctx);
-        up.add(bvh.nodes, &d.nodes);
-        up.add(bvh.leaf_geom, &d.leaf_geom);
-        up.add(bvh.leaf_ids, &d.leaf_ids);
-        return up.commit(ctx, st);   // packs the host vectors before they die
-    } catch (const std::exception& e) {
-        return fail(RT_ERR_OUT_OF_MEMORY, e.what());
     }
+    // Brute-force padding: whole batches of 8; the pad spheres sit 1e19 away with
+    // radius^2 = -1e38, so D = b^2 - a(|oc|^2 + 1e38) < 0 for every ray.
+    while (pk->geom.size() % 8) pk->geom.push_back(rt::GeomRec{0.0f, 1e19f, 0.0f, -1e38f});
+    rt::build_lbvh_host(spheres, count, pk->bvh, sah, uint32_t(Tuning::get(ctx->tune.sah_knobs, 0)));
+    // leaf ids are read as uint4: pad to a multiple of 4
+    while (pk->bvh.leaf_ids.size() % 4) pk->bvh.leaf_ids.push_back(0u);
+    // pad node boxes for origins within the scene radius (hit points) and a nearby camera
+    float R = 0.0f;
+    for (uint32_t i = 0; i < count; i++) {
+        const rt_vec4& gg = spheres[i].geometry;
+        R = std::max(R, std::sqrt(gg.x * gg.x + gg.y * gg.y + gg.z * gg.z) + std::fabs(gg.w));
+    }
+    pk->scene_radius = R;
+    pk->pad_radius = R * 1.01f + 100.0f;
+    pk->nodes_host = pk->bvh.nodes;
+    pad_nodes(pk->nodes_host, pk->bvh.nodes, pad_for(pk->pad_radius));
+    make_octant_orders(pk->bvh.nodes, pk->oct);
+    // Uniform grid (rt_grid.h) when the scene suits one: the default walk.
+    // Tuning grid = 0 disables it, grid_scale scales the cell size (A/B).
+    const float gscale = float(Tuning::get(ctx->tune.grid_scale, rt::kGridCellScale));
+    pk->has_grid = Tuning::get(ctx->tune.grid, 1) != 0 &&
+                   rt::build_grid_host(spheres, count, pk->bvh.big_ids, 64.0f * 0x1p-24f * pk->pad_radius, gscale,
+                                       1u << 22, pk->grid);
+    return pk;
 }
 
-template <typename T>
-int scene_alloc(rt_context* ctx, T** dst, size_t count, bool grid = false) {
+// Uploads a host package into ctx's blob (one stream-ordered copy, BlobUpload) and makes it the
+// context's scene.
+int commit_host_package(rt_context* ctx, const rt::HostPackage& pk, hipStream_t st) {
+    ctx->scene = rt::DeviceScene{};
+    ctx->slot_cur = -1;
+    ctx->gpu_tree = false;
+    ctx->colours_unit = pk.colours_unit;
+    BlobUpload up;
+    rt::DeviceScene& d = ctx->scene;
+    d.n_spheres = pk.count;
+    up.add(pk.geom, &d.geom);
+    up.add(pk.radius, &d.radius);
+    up.add(pk.mat, &d.mat);
+    d.small_rmax = pk.bvh.small_rmax;
+    d.small_rmin = pk.bvh.small_rmin;
+    d.n_big = uint32_t(pk.bvh.big_ids.size());
+    up.add(pk.bvh.big_ids, &d.big_ids);
+    d.n_nodes = uint32_t(pk.bvh.nodes.size());
+    d.n_leaf = uint32_t(pk.bvh.leaf_geom.size());
+    ctx->scene_radius = pk.scene_radius;
+    ctx->pad_radius = pk.pad_radius;
+    ctx->padded_for = pk.pad_radius;
+    ctx->nodes_host = pk.nodes_host;
+    up.add(pk.oct, &d.nodes_oct);
+    ctx->has_grid = pk.has_grid;
+    if (pk.has_grid) {
+        d.grid = pk.grid.info;
+        up.add(pk.grid.cell_start, &d.cell_start);
+        up.add(pk.grid.rec, &d.grid_rec);
+        up.add(pk.grid.ids, &d.grid_ids);
+        ctx->grid_pad_radius = pk.pad_radius;
+    }
+    size_lds_forms(ctx);
+    up.add(pk.bvh.nodes, &d.nodes);
+    up.add(pk.bvh.leaf_geom, &d.leaf_geom);
+    up.add(pk.bvh.leaf_ids, &d.leaf_ids);
+    return up.commit(ctx, st);
+}
+
+// ---- device-built scenes (rt_build.hip) ------------------------------------------------------
+// Two arenas used alternately (rt_context::slot): frame k + 1's build writes the arena frame k
+// does not read, on the context's own build stream, so it runs beside frame k (in the CUs its
+// tail frees) instead of after it, and no arena is freed or allocated per frame. The build waits
+// only for the launches that read its arena two scenes ago (SceneSlot::ev_free). The host reads
+// one summary back (counts, radii, root box) to lay out the grid; the next launch of the context
+// waits for the build's last kernel (ev_last on the build stream), on whatever stream it runs.
+size_t round256(size_t b) { return (b + 255u) & ~size_t(255); }
+
+int ensure_build_stream(rt_context* ctx) {
+    if (ctx->build_stream) return RT_OK;
+    RT_HIP(hipStreamCreateWithFlags(&ctx->build_stream, hipStreamNonBlocking));
+    RT_HIP(hipEventCreateWithFlags(&ctx->ev_summary, hipEventDisableTiming));
+    RT_HIP(hipEventCreateWithFlags(&ctx->ev_caller, hipEventDisableTiming));
+    for (SceneSlot& s : ctx->slot) RT_HIP(hipEventCreateWithFlags(&s.ev_free, hipEventDisableTiming));
     void* p = nullptr;
-    RT_HIP(hipMalloc(&p, std::max<size_t>(count, 1) * sizeof(T) + 16));
-    (grid ? ctx->grid_allocs : ctx->scene_allocs).push_back(p);
-    *dst = static_cast<T*>(p);
+    RT_HIP(hipHostMalloc(&p, sizeof(rt::BuildSummary), hipHostMallocDefault));
+    ctx->summary = static_cast<rt::BuildSummary*>(p);
     return RT_OK;
 }
 
-// Device-built tree (rt_build.hip) from spheres already in device memory. refit: keep the
-// topology of the previous build over the same count (positions / radii / materials may change).
-int set_scene_gpu(rt_context* ctx, const Sphere* d_sph, uint32_t count, hipStream_t st, bool refit) {
-    rt::DeviceScene& d = ctx->scene;
-    if (!refit) {
-        free_scene(ctx);
-        ctx->gpu_tree = true;
-        if (int rc = scene_alloc(ctx, &d.geom, (size_t(count) + 7u) & ~size_t(7))) return rc;
-        if (int rc = scene_alloc(ctx, &d.radius, count)) return rc;
-        if (int rc = scene_alloc(ctx, &d.mat, count)) return rc;
-        if (int rc = scene_alloc(ctx, &d.big_ids, 64)) return rc;
-        if (int rc = scene_alloc(ctx, &d.nodes, 2 * size_t(count))) return rc;
-        if (int rc = scene_alloc(ctx, &d.nodes_raw, 2 * size_t(count))) return rc;
-        if (int rc = scene_alloc(ctx, &d.leaf_geom, 4 * size_t(count))) return rc;
-        if (int rc = scene_alloc(ctx, &d.leaf_ids, 4 * size_t(count))) return rc;
-        if (int rc = scene_alloc(ctx, &d.treelet, 8 * size_t(rt::kTreeletCap))) return rc;
-        if (int rc = scene_alloc(ctx, &d.treelet_count, 1)) return rc;
+// Frees memory an arena's queued launches may still read: waits for them and for the build stream.
+int retire_slot_memory(rt_context* ctx, SceneSlot& s, void*& mem) {
+    if (!mem) return RT_OK;
+    if (s.used) RT_HIP(hipEventSynchronize(s.ev_free));
+    RT_HIP(hipStreamSynchronize(ctx->build_stream));
+    RT_HIP(hipFree(mem));
+    mem = nullptr;
+    return RT_OK;
+}
+
+// Per-sphere arrays of an arena for n spheres, carved out of one allocation (12.5 % headroom).
+int slot_reserve(rt_context* ctx, SceneSlot& s, uint32_t n) {
+    if (s.mem && s.cap_n >= n) return RT_OK;
+    if (int rc = retire_slot_memory(ctx, s, s.mem)) return rc;
+    s.cap_n = 0;
+    const size_t c = std::max<size_t>(64, size_t(n) + n / 8);
+    const size_t sz[] = {((c + 7) & ~size_t(7)) * sizeof(rt::GeomRec), c * 4, c * sizeof(rt::MatRec), 64 * 4,
+                         2 * c * sizeof(rt::BvhNode), 2 * c * sizeof(rt::BvhNode), 4 * c * sizeof(rt::GeomRec),
+                         4 * c * 4, 8 * size_t(rt::kTreeletCap) * 4, 16};
+    size_t off[10], total = 0;
+    for (int i = 0; i < 10; i++) { off[i] = total; total += round256(sz[i]); }
+    RT_HIP(hipMalloc(&s.mem, total));
+    char* b = static_cast<char*>(s.mem);
+    rt::DeviceScene& d = s.scene;
+    d = rt::DeviceScene{};
+    d.geom = reinterpret_cast<rt::GeomRec*>(b + off[0]);
+    d.radius = reinterpret_cast<float*>(b + off[1]);
+    d.mat = reinterpret_cast<rt::MatRec*>(b + off[2]);
+    d.big_ids = reinterpret_cast<uint32_t*>(b + off[3]);
+    d.nodes = reinterpret_cast<rt::BvhNode*>(b + off[4]);
+    d.nodes_raw = reinterpret_cast<rt::BvhNode*>(b + off[5]);
+    d.leaf_geom = reinterpret_cast<rt::GeomRec*>(b + off[6]);
+    d.leaf_ids = reinterpret_cast<uint32_t*>(b + off[7]);
+    d.treelet = reinterpret_cast<float*>(b + off[8]);
+    d.treelet_count = reinterpret_cast<uint32_t*>(b + off[9]);
+    s.cap_n = uint32_t(c);
+    return RT_OK;
+}
+
+int stage_spheres(rt_context* ctx, const Sphere* spheres, uint32_t count, bool device_ptr, hipStream_t st) {
+    const size_t bytes = size_t(count) * sizeof(Sphere);
+    if (count > ctx->d_spheres_cap) {   // the previous build's kernels may still read it
+        if (ctx->d_spheres) {
+            RT_HIP(hipStreamSynchronize(ctx->build_stream));
+            RT_HIP(hipFree(ctx->d_spheres));
+        }
+        ctx->d_spheres = nullptr;
+        ctx->d_spheres_cap = 0;
+        void* p = nullptr;
+        RT_HIP(hipMalloc(&p, bytes));
+        ctx->d_spheres = static_cast<Sphere*>(p);
+        ctx->d_spheres_cap = count;
     }
-    ctx->treelet_stale = true;
-    rt::BuildOutputs o{d.geom, d.radius, d.mat, d.big_ids, d.nodes, d.nodes_raw, d.leaf_geom, d.leaf_ids};
-    rt::BuildSummary sm;
-    const hipError_t e = rt::build_scene_gpu(ctx->ws, d_sph, count, o, refit, st, &sm);
-    if (e != hipSuccess) {
-        if (!refit) free_scene(ctx);
+    if (!count) return RT_OK;
+    if (device_ptr) {   // written by the caller's earlier work on st; copied so the build (and
+                        // the grid build, which runs after the call returns) never reads it later
+        RT_HIP(hipEventRecord(ctx->ev_caller, st));
+        RT_HIP(hipStreamWaitEvent(ctx->build_stream, ctx->ev_caller, 0));
+        RT_HIP(hipMemcpyAsync(ctx->d_spheres, spheres, bytes, hipMemcpyDeviceToDevice, ctx->build_stream));
+        return RT_OK;
+    }
+    // host spheres through a pinned buffer: an asynchronous copy (a pageable one would block the
+    // host until the previous frame's GPU work leaves the copy engine)
+    if (ctx->sph_stage_cap < bytes) {
+        if (ctx->sph_stage) {
+            RT_HIP(hipStreamSynchronize(ctx->build_stream));
+            RT_HIP(hipHostFree(ctx->sph_stage));
+        }
+        ctx->sph_stage = nullptr;
+        ctx->sph_stage_cap = 0;
+        RT_HIP(hipHostMalloc(&ctx->sph_stage, bytes + bytes / 8, hipHostMallocDefault));
+        ctx->sph_stage_cap = bytes + bytes / 8;
+    }
+    std::memcpy(ctx->sph_stage, spheres, bytes);   // the previous copy from it ended with its build
+    RT_HIP(hipMemcpyAsync(ctx->d_spheres, ctx->sph_stage, bytes, hipMemcpyHostToDevice, ctx->build_stream));
+    return RT_OK;
+}
+
+// Phase 1 of a device build: the spheres to the device and the LBVH build of the free arena, all on
+// the build stream, up to the summary's copy to pinned memory (ev_summary). refit: keep the
+// topology of the last full build (same count; positions / radii / materials may change).
+int device_build_begin(rt_context* ctx, const Sphere* spheres, uint32_t count, bool device_ptr, hipStream_t st,
+                       bool refit) {
+    if (int rc = ensure_build_stream(ctx)) return rc;
+    const int k = ctx->slot_cur == 0 ? 1 : 0;
+    SceneSlot& s = ctx->slot[k];
+    const hipStream_t bs = ctx->build_stream;
+    if (s.used) RT_HIP(hipStreamWaitEvent(bs, s.ev_free, 0));   // its last readers (two scenes ago)
+    if (int rc = slot_reserve(ctx, s, count)) return rc;
+    if (int rc = stage_spheres(ctx, spheres, count, device_ptr, st)) return rc;
+    rt::DeviceScene& d = s.scene;
+    if (refit)   // the big set is the topology's (a refit does not re-select it)
+        RT_HIP(hipMemcpyAsync(d.big_ids, ctx->slot[ctx->slot_cur].scene.big_ids, 64 * 4, hipMemcpyDeviceToDevice, bs));
+    const rt::BuildOutputs o{d.geom, d.radius, d.mat, d.big_ids, d.nodes, d.nodes_raw, d.leaf_geom, d.leaf_ids};
+    const hipError_t e = rt::build_scene_gpu(ctx->ws, ctx->d_spheres, count, o, refit, bs, ctx->summary);
+    if (e != hipSuccess)
         return fail(e == hipErrorOutOfMemory ? RT_ERR_OUT_OF_MEMORY : RT_ERR_DEVICE,
                     std::string("device LBVH build: ") + hipGetErrorString(e));
-    }
-    d.n_spheres = count;
-    ctx->colours_unit = sm.colour_out_of_range == 0u;
+    RT_HIP(hipEventRecord(ctx->ev_summary, bs));
+    ctx->pending = true;
+    ctx->pending_slot = k;
+    ctx->pending_count = count;
+    return RT_OK;
+}
+
+// Phase 2: the summary (host wait for the build only, not for earlier launches), the device grid
+// over the small spheres (the default walk) from the tree's root box, and the
+// arena becomes the context's scene.
+int device_build_end(rt_context* ctx) {
+    if (!ctx->pending) return RT_OK;
+    ctx->pending = false;
+    const int k = ctx->pending_slot;
+    SceneSlot& s = ctx->slot[k];
+    const hipStream_t bs = ctx->build_stream;
+    RT_HIP(hipEventSynchronize(ctx->ev_summary));
+    const rt::BuildSummary sm = *ctx->summary;
+    rt::DeviceScene& d = s.scene;
+    d.n_spheres = ctx->pending_count;
     d.n_big = sm.n_big;
     d.n_nodes = sm.n_nodes;
     d.n_leaf = sm.n_leaf_slots;
     d.small_rmax = rt::summary_float(sm.rmax_o);
     d.small_rmin = rt::summary_float(sm.rmin_o);
-    ctx->scene_radius = rt::summary_float(sm.R_o);
-    ctx->pad_radius = ctx->scene_radius * 1.01f + 100.0f;   // the build padded for this radius
-    ctx->padded_for = ctx->pad_radius;
-    // Uniform grid over the small spheres (the default walk), built on the device
-    // from the tree's root box (the small spheres' AABB union). RT_GRID=0 disables it.
-    ctx->has_grid = false;
     d.grid = rt::GridInfo{};
     d.cell_start = d.grid_ids = nullptr;
     d.grid_rec = nullptr;
-    // the previous build's grid (a refit rebuilds it; before, every refit leaked one): every
-    // earlier launch of the context has finished, build_scene_gpu waited for its stream
-    for (void* p : ctx->grid_allocs) (void)hipFree(p);
-    ctx->grid_allocs.clear();
-    const char* ge = std::getenv("RT_GRID");
-    if (!(ge && std::strcmp(ge, "0") == 0) && sm.n_small && d.small_rmax > 0.0f) {
-        rt::BvhNode root;
-        RT_HIP(hipMemcpy(&root, d.nodes_raw, sizeof(root), hipMemcpyDeviceToHost));
-        const float lo[3] = {root.lox, root.loy, root.loz}, hi[3] = {root.hix, root.hiy, root.hiz};
-        const char* gs = std::getenv("RT_GRID_SCALE");
+    ctx->colours_unit = sm.colour_out_of_range == 0u;
+    ctx->scene_radius = rt::summary_float(sm.R_o);
+    ctx->pad_radius = ctx->scene_radius * 1.01f + 100.0f;   // the build padded for this radius
+    ctx->padded_for = ctx->pad_radius;
+    ctx->has_grid = false;
+    if (Tuning::get(ctx->tune.grid, 1) != 0 && sm.n_small && d.small_rmax > 0.0f) {
         rt::GridInfo gi;
         uint64_t bound = 0;
-        if (rt::grid_layout(lo, hi, sm.n_small, d.small_rmax, 64.0f * 0x1p-24f * ctx->pad_radius,
-                            gs ? float(std::atof(gs)) : rt::kGridCellScale, gi, &bound) && bound <= (1u << 26)) {
-            uint32_t* cursor = nullptr;
-            void* tmp = nullptr;
-            const size_t tb = rt::grid_scan_bytes(gi.n_cells);
-            if (int rc = scene_alloc(ctx, &d.cell_start, size_t(gi.n_cells) + 1, true)) return rc;
-            if (int rc = scene_alloc(ctx, &cursor, size_t(gi.n_cells) + 1, true)) return rc;
-            if (int rc = scene_alloc(ctx, &d.grid_rec, size_t(bound), true)) return rc;
-            if (int rc = scene_alloc(ctx, &d.grid_ids, size_t(bound), true)) return rc;
-            if (int rc = scene_alloc(ctx, reinterpret_cast<uint8_t**>(&tmp), tb, true)) return rc;
-            RT_HIP(rt::build_grid_gpu(ctx->ws, d_sph, count, gi, cursor, d.cell_start, d.grid_rec, d.grid_ids, tmp,
-                                      tb, st));
+        if (rt::grid_layout(sm.root_lo, sm.root_hi, sm.n_small, d.small_rmax, 64.0f * 0x1p-24f * ctx->pad_radius,
+                            float(Tuning::get(ctx->tune.grid_scale, rt::kGridCellScale)), gi, &bound) &&
+            bound <= (1u << 26)) {
+            const size_t nc1 = size_t(gi.n_cells) + 1, tb = rt::grid_scan_bytes(gi.n_cells);
+            const size_t off_cur = round256(nc1 * 4), off_rec = off_cur + round256(nc1 * 4),
+                         off_ids = off_rec + round256(size_t(bound) * sizeof(rt::GeomRec)),
+                         off_tmp = off_ids + round256(size_t(bound) * 4), total = off_tmp + round256(tb);
+            if (s.grid_cap < total) {
+                if (int rc = retire_slot_memory(ctx, s, s.grid_mem)) return rc;
+                s.grid_cap = 0;
+                RT_HIP(hipMalloc(&s.grid_mem, total + total / 8));
+                s.grid_cap = total + total / 8;
+            }
+            char* g = static_cast<char*>(s.grid_mem);
+            d.cell_start = reinterpret_cast<uint32_t*>(g);
+            d.grid_rec = reinterpret_cast<rt::GeomRec*>(g + off_rec);
+            d.grid_ids = reinterpret_cast<uint32_t*>(g + off_ids);
+            RT_HIP(rt::build_grid_gpu(ctx->ws, ctx->d_spheres, d.n_spheres, gi, reinterpret_cast<uint32_t*>(g + off_cur),
+                                      d.cell_start, d.grid_rec, d.grid_ids, g + off_tmp, tb, bs));
             gi.n_refs = 0;   // exact count left on the device: the grid is walked from L2
             d.grid = gi;
             ctx->has_grid = true;
             ctx->grid_pad_radius = ctx->pad_radius;
         }
     }
+    ctx->scene = d;
+    ctx->slot_cur = k;
+    ctx->gpu_tree = true;
+    ctx->treelet_stale = true;
     ctx->nodes_host.clear();
     size_lds_forms(ctx);
     return RT_OK;
@@ -646,23 +816,6 @@ Builder pick_builder(uint32_t count) {
     return count <= kHostSahMaxSpheres ? Builder::HOST_SAH : Builder::GPU;
 }
 
-int stage_spheres(rt_context* ctx, const Sphere* spheres, uint32_t count, hipStream_t st) {
-    if (count > ctx->d_spheres_cap) {
-        if (ctx->d_spheres) {
-            RT_HIP(hipDeviceSynchronize());
-            (void)hipFree(ctx->d_spheres);
-        }
-        ctx->d_spheres = nullptr;
-        ctx->d_spheres_cap = 0;
-        void* p = nullptr;
-        RT_HIP(hipMalloc(&p, size_t(count) * sizeof(Sphere)));
-        ctx->d_spheres = static_cast<Sphere*>(p);
-        ctx->d_spheres_cap = count;
-    }
-    if (count) RT_HIP(hipMemcpyAsync(ctx->d_spheres, spheres, size_t(count) * sizeof(Sphere), hipMemcpyHostToDevice, st));
-    return RT_OK;
-}
-
 int check_scene_args(rt_context* ctx, const Sphere* spheres, uint32_t count) {
     if (!ctx) return fail(RT_ERR_INVALID_ARGUMENT, "ctx is NULL");
     if (!spheres && count) return fail(RT_ERR_INVALID_ARGUMENT, "spheres is NULL");
@@ -670,19 +823,125 @@ int check_scene_args(rt_context* ctx, const Sphere* spheres, uint32_t count) {
     return RT_OK;
 }
 
-// Scene calls: ordered after the context's previous operation, and before its next one.
-template <typename F>
-int scene_op(rt_context* ctx, hipStream_t st, F&& body) {
+// Bookkeeping after a scene call: the scene is usable (or not, RT_ERR_NO_SCENE), launch info
+// reports its default form until it renders.
+int scene_done(rt_context* ctx, int rc) {
+    ctx->scene_set = rc == RT_OK;
+    ctx->last_accel = 0;
+    return rc;
+}
+
+// First half of every scene call. Host-built scenes are built (or taken from *shared, built by an
+// earlier context of the same rt_multi frame) and uploaded in order on `st` after the context's
+// previous operations; device-built scenes start their build on the context's build stream.
+int scene_begin(rt_context* ctx, const Sphere* spheres, uint32_t count, bool device_ptr, hipStream_t st, bool refit,
+                rt::HostPackagePtr* shared) {
     DeviceGuard g(ctx->device);
-    if (int rc = order_on(ctx, st)) return rc;
-    const int rc = body();
-    if (rc != RT_OK) {
-        ctx->scene_set = false;
-        return rc;
+    if (int rc = device_build_end(ctx)) return rc;   // a begin without its end (never in this library)
+    const Builder b = device_ptr ? Builder::GPU : pick_builder(count);
+    if (b != Builder::GPU) {
+        try {
+            if (int rc = order_on(ctx, st)) return rc;
+            rt::HostPackagePtr own;
+            rt::HostPackagePtr& pk = shared ? *shared : own;
+            if (!pk || pk->count != count) pk = build_host_package(ctx, spheres, count, b == Builder::HOST_SAH);
+            if (int rc = commit_host_package(ctx, *pk, st)) return rc;
+            return mark_issued(ctx, st);
+        } catch (const std::exception& e) {
+            return fail(RT_ERR_OUT_OF_MEMORY, e.what());
+        }
     }
-    ctx->scene_set = true;
-    ctx->last_accel = 0;   // launch info reports the new scene's default form until it renders
-    return mark_issued(ctx, st);
+    return device_build_begin(ctx, spheres, count, device_ptr, st, refit && ctx->gpu_tree && ctx->slot_cur >= 0 &&
+                                                                       count == ctx->scene.n_spheres &&
+                                                                       ctx->ws.topo_n == count);
+}
+
+int scene_end(rt_context* ctx) {
+    if (!ctx->pending) return RT_OK;
+    DeviceGuard g(ctx->device);
+    if (int rc = device_build_end(ctx)) return rc;
+    return mark_issued(ctx, ctx->build_stream);   // the next operation waits for the build
+}
+
+}  // namespace
+
+namespace rt {
+int set_scene_begin(rt_context* ctx, const Sphere* spheres, uint32_t count, void* stream, HostPackagePtr* shared) {
+    if (int rc = check_scene_args(ctx, spheres, count)) return rc;
+    const int rc = scene_begin(ctx, spheres, count, false, static_cast<hipStream_t>(stream), false, shared);
+    if (rc != RT_OK) {
+        ctx->pending = false;
+        return scene_done(ctx, rc);
+    }
+    return RT_OK;
+}
+
+int set_scene_end(rt_context* ctx) {
+    const int rc = scene_end(ctx);
+    ctx->pending = false;
+    return scene_done(ctx, rc);
+}
+}  // namespace rt
+
+namespace {
+
+int scene_call(rt_context* ctx, const Sphere* spheres, uint32_t count, bool device_ptr, void* stream, bool refit) {
+    if (int rc = check_scene_args(ctx, spheres, count)) return rc;
+    int rc = scene_begin(ctx, spheres, count, device_ptr, static_cast<hipStream_t>(stream), refit, nullptr);
+    if (rc == RT_OK) rc = scene_end(ctx);
+    ctx->pending = false;
+    return scene_done(ctx, rc);
+}
+
+// Kernel form of a launch (rt_internal.h ACCEL_*) and its dynamic LDS bytes. form =
+// options.reserved[1] (A/B and tests, 0 = automatic): 6 one LDS node copy, 8 octant copies, 10
+// every node from L2, 12 the grid, 14 the grid with the wave-cooperative walk; cam_r = the camera's
+// distance from the origin (the grid's margin covers cameras within its pad radius).
+uint32_t choose_accel(const rt_context* ctx, bool brute, uint32_t form, float cam_r, size_t* lds_out) {
+    const rt::DeviceScene& d = ctx->scene;
+    const Tuning& tu = ctx->tune;
+    uint32_t accel;
+    size_t lds = 0;
+    if (brute) {
+        accel = rt::ACCEL_BRUTE;
+    } else if (ctx->has_grid && cam_r <= ctx->grid_pad_radius &&
+               (form == 12u || form == 14u || (form == 0u && (ctx->grid_bytes || !ctx->oct_bytes)))) {
+        // the grid (DESIGN.md §4.6): staged in LDS when it fits (config 3: 1 % faster than the
+        // octant tree), else the octant tree when that fits LDS (a device-built scene of ~1000
+        // spheres, whose grid would be read from L2), else the grid from L2
+        accel = ctx->grid_bytes ? rt::ACCEL_GRID : rt::ACCEL_GRID_GLOBAL;
+        lds = ctx->grid_bytes;   // 0: the grid from L2
+        // the wave-cooperative walk: form 14, or tuning grid_coop = 1
+        const bool coop = form == 14u || (form == 0u && Tuning::get(tu.grid_coop, 0) == 1);
+        if (coop && accel == rt::ACCEL_GRID &&
+            ctx->grid_bytes + rt::kLaneSumLdsBytes + rt::kCoopLdsBytes <= kMaxLdsBytes)
+            accel = rt::ACCEL_GRID_COOP;
+        else if (coop && accel == rt::ACCEL_GRID_GLOBAL)
+            accel = rt::ACCEL_GRID_GLOBAL_COOP;
+        // the LDS grid kernel also stages the winner's gate and shading records ({c, r} + the
+        // material record, 48 B per sphere) when two blocks per CU still fit (DESIGN.md §4.8);
+        // tuning grid_rec = 0: not (A/B)
+        const size_t rec_bytes = size_t(d.n_spheres) * 48u;
+        if (accel == rt::ACCEL_GRID && Tuning::get(tu.grid_rec, 1) != 0 &&
+            ctx->grid_bytes + rec_bytes + rt::kLaneSumLdsBytes <= kTwoBlockLdsBytes) {
+            accel = rt::ACCEL_GRID_REC;
+            lds = ctx->grid_bytes + rec_bytes;
+        }
+    } else if (ctx->oct_bytes && (form == 0u || form == 8u)) {
+        accel = rt::ACCEL_LBVH_OCT;
+        lds = ctx->oct_bytes;
+    } else if (ctx->lds1_bytes && (form == 0u || form == 6u || form == 8u)) {
+        accel = rt::ACCEL_LBVH_LDS;
+        lds = ctx->lds1_bytes;
+    } else if (ctx->gpu_tree && d.treelet && d.n_nodes && d.n_leaf < (1u << 26) && form != 10u) {
+        // (treelet leaf words carry first_count in 30 bits)
+        accel = rt::ACCEL_LBVH_TOP;
+        lds = size_t(rt::kTreeletCap) * 32u;
+    } else {
+        accel = rt::ACCEL_LBVH_GLOBAL;
+    }
+    *lds_out = lds;
+    return accel;
 }
 
 }  // namespace
@@ -690,53 +949,27 @@ int scene_op(rt_context* ctx, hipStream_t st, F&& body) {
 extern "C" {
 
 int rt_set_scene(rt_context* ctx, const Sphere* spheres, uint32_t count, void* stream) {
-    if (int rc = check_scene_args(ctx, spheres, count)) return rc;
-    hipStream_t st = static_cast<hipStream_t>(stream);
-    return scene_op(ctx, st, [&]() -> int {
-        const Builder b = pick_builder(count);
-        if (b != Builder::GPU) return set_scene_host(ctx, spheres, count, st, b == Builder::HOST_SAH);
-        RT_HIP(hipStreamSynchronize(st));  // the device builder frees and rebuilds in place
-        if (int rc = stage_spheres(ctx, spheres, count, st)) return rc;
-        return set_scene_gpu(ctx, ctx->d_spheres, count, st, false);
-    });
+    return scene_call(ctx, spheres, count, false, stream, false);
 }
 
 int rt_set_scene_device(rt_context* ctx, const Sphere* d_spheres, uint32_t count, void* stream) {
-    if (int rc = check_scene_args(ctx, d_spheres, count)) return rc;
-    hipStream_t st = static_cast<hipStream_t>(stream);
-    return scene_op(ctx, st, [&]() -> int {
-        RT_HIP(hipStreamSynchronize(st));
-        return set_scene_gpu(ctx, d_spheres, count, st, false);
-    });
+    return scene_call(ctx, d_spheres, count, true, stream, false);
 }
 
 int rt_refit_scene(rt_context* ctx, const Sphere* spheres, uint32_t count, void* stream) {
-    if (int rc = check_scene_args(ctx, spheres, count)) return rc;
-    if (!ctx->gpu_tree || count != ctx->scene.n_spheres || ctx->ws.topo_n != count)
-        return rt_set_scene(ctx, spheres, count, stream);   // no topology to reuse: full build
-    hipStream_t st = static_cast<hipStream_t>(stream);
-    return scene_op(ctx, st, [&]() -> int {
-        RT_HIP(hipStreamSynchronize(st));
-        if (int rc = stage_spheres(ctx, spheres, count, st)) return rc;
-        return set_scene_gpu(ctx, ctx->d_spheres, count, st, true);
-    });
+    // without a device-built tree of this count there is no topology to reuse: a full build
+    return scene_call(ctx, spheres, count, false, stream, true);
 }
 
 int rt_refit_scene_device(rt_context* ctx, const Sphere* d_spheres, uint32_t count, void* stream) {
-    if (int rc = check_scene_args(ctx, d_spheres, count)) return rc;
-    if (!ctx->gpu_tree || count != ctx->scene.n_spheres || ctx->ws.topo_n != count)
-        return rt_set_scene_device(ctx, d_spheres, count, stream);
-    hipStream_t st = static_cast<hipStream_t>(stream);
-    return scene_op(ctx, st, [&]() -> int {
-        RT_HIP(hipStreamSynchronize(st));
-        return set_scene_gpu(ctx, d_spheres, count, st, true);
-    });
+    return scene_call(ctx, d_spheres, count, true, stream, true);
 }
 
 int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t* rows,
                      uint32_t band_width, uint32_t band_height, float* accum, uint8_t* out,
                      const rt_options* opt, void* stream) {
     if (!ctx || !rci) return fail(RT_ERR_INVALID_ARGUMENT, "ctx or rci is NULL");
+    if (ctx->pending) return fail(RT_ERR_INVALID_ARGUMENT, "rt_render_device between the halves of a scene build");
     if (!ctx->scene_set) return fail(RT_ERR_NO_SCENE, "rt_render_device before rt_set_scene");
     if (band_width == 0 || band_height == 0) return RT_OK;
     if (!accum || !out) return fail(RT_ERR_INVALID_ARGUMENT, "accum or out is NULL");
@@ -764,57 +997,12 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
                     "checkered spheres); this scene has one outside: render it with RT_RNG_PIXEL_STREAM");
     const uint64_t tiles_x = (band_width + 7u) / 8u, tiles_y = (band_height + 7u) / 8u;
     const uint64_t n_tiles = tiles_x * tiles_y;
-    // reserved[1] (internal, A/B only): LBVH walk form, 0 = automatic (octant node copies in LDS
-    // when they fit, else one copy in LDS, else an LDS treelet over L2), 6 = one LDS node copy,
-    // 8 = octant copies, 10 = every node from L2.
-    const uint32_t form = o.reserved[1];
+    // reserved[1] (internal, A/B only): walk form, 0 = automatic (choose_accel)
     const rt::DeviceScene& d = ctx->scene;
-    uint32_t accel;
-    size_t lds = 0;
     const float cam_r = std::sqrt(rci->camera_pos.x * rci->camera_pos.x + rci->camera_pos.y * rci->camera_pos.y +
                                   rci->camera_pos.z * rci->camera_pos.z);
-    if (o.accel == RT_ACCEL_BRUTE) {
-        accel = rt::ACCEL_BRUTE;
-    } else if (ctx->has_grid && cam_r <= ctx->grid_pad_radius &&
-               (form == 12u || form == 14u || (form == 0u && (ctx->grid_bytes || !ctx->oct_bytes)))) {
-        // the grid (DESIGN.md §4.6): staged in LDS when it fits (config 3: 1 % faster than the
-        // octant tree), else the octant tree when that fits LDS (a device-built scene of ~1000
-        // spheres, whose grid would be read from L2), else the grid from L2; its margin covers
-        // cameras within its pad radius
-        accel = ctx->grid_bytes ? rt::ACCEL_GRID : rt::ACCEL_GRID_GLOBAL;
-        lds = ctx->grid_bytes ? ctx->grid_bytes : rt::kBigLdsBytes;
-        // the wave-cooperative walk: form 14, or RT_GRID_COOP=1
-        const char* ce = std::getenv("RT_GRID_COOP");
-        const bool coop = form == 14u || (form == 0u && ce && std::strcmp(ce, "1") == 0);
-        if (coop && accel == rt::ACCEL_GRID &&
-            ctx->grid_bytes + rt::kLaneSumLdsBytes + rt::kCoopLdsBytes <= kMaxLdsBytes)
-            accel = rt::ACCEL_GRID_COOP;
-        else if (coop && accel == rt::ACCEL_GRID_GLOBAL)
-            accel = rt::ACCEL_GRID_GLOBAL_COOP;
-        // the LDS grid kernel also stages the winner's gate and shading records ({c, r} + the
-        // material record, 48 B per sphere) when two blocks per CU still fit (DESIGN.md §4.2);
-        // RT_GRID_REC=0: not (A/B)
-        const size_t rec_bytes = size_t(d.n_spheres) * 48u;
-        const char* re = std::getenv("RT_GRID_REC");
-        if (accel == rt::ACCEL_GRID && !(re && std::strcmp(re, "0") == 0) &&
-            ctx->grid_bytes + rec_bytes + rt::kLaneSumLdsBytes <= kTwoBlockLdsBytes) {
-            accel = rt::ACCEL_GRID_REC;
-            lds = ctx->grid_bytes + rec_bytes;
-        }
-    } else if (ctx->oct_bytes && (form == 0u || form == 8u)) {
-        accel = rt::ACCEL_LBVH_OCT;
-        lds = ctx->oct_bytes;
-    } else if (ctx->lds1_bytes && (form == 0u || form == 6u || form == 8u)) {
-        accel = rt::ACCEL_LBVH_LDS;
-        lds = ctx->lds1_bytes;
-    } else if (ctx->gpu_tree && d.treelet && d.n_nodes && d.n_leaf < (1u << 26) && form != 10u) {
-        // (treelet leaf words carry first_count in 30 bits)
-        accel = rt::ACCEL_LBVH_TOP;
-        lds = size_t(rt::kTreeletCap) * 32u + rt::kBigLdsBytes;
-    } else {
-        accel = rt::ACCEL_LBVH_GLOBAL;
-        lds = rt::kBigLdsBytes;
-    }
+    size_t lds = 0;
+    const uint32_t accel = choose_accel(ctx, o.accel == RT_ACCEL_BRUTE, o.reserved[1], cam_r, &lds);
     const bool count = (o.reserved[0] & 1u) != 0;  // internal: count box / sphere tests
     DeviceGuard g(ctx->device);
     hipStream_t st = static_cast<hipStream_t>(stream);
@@ -882,7 +1070,7 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
         const double T = std::sqrt(0.75 * m * double(d.small_rmin) / (7.0 * 0x1p-24));
         const double tn = 0.95 * T - double(d.small_rmax) - m;
         const bool start_ok = 9.1e-4 * (double(d.small_rmax) + 1e-3) <= 0.25 * m;
-        if (tn > 0.0 && start_ok && !std::getenv("RT_GRID_FULL_SLACK")) {   // RT_GRID_FULL_SLACK: A/B only
+        if (tn > 0.0 && start_ok && Tuning::get(ctx->tune.grid_full_slack, 0) == 0) {   // grid_full_slack: A/B only
             P.cull_near_t = float(tn);
             P.cull_near_abs = 1e-3f + 1e-3f * d.small_rmax;   // covers 9.1e-4 (r + eps_d) of |oc| - t
         }
@@ -943,8 +1131,8 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     // throughput-bound and its tail (the units running when the queue runs dry, about one unit
     // long) short, without paying a unit's start and flush too often (config 3,
     // 10 000 spp, 4 -> 25 chunks -2.0 %; config 5, 1000 spp 4K: 1 / 3 / 7 / 14 chunks 658.6 /
-    // 655.3 / 666.0 / 685.9 ms). RT_SAMPLE_CHUNKS forces a count, RT_UNITS_PER_LANE /
-    // RT_UNIT_MIN_SAMPLES the targets. The brute-force walk's samples cost ~n/10 times a grid
+    // 655.3 / 666.0 / 685.9 ms). Tuning sample_chunks forces a count, units_per_lane /
+    // unit_min_samples set the targets. The brute-force walk's samples cost ~n/10 times a grid
     // sample, so its floor scales down with n (488 spheres: 5 samples; config 2, 100 spp: 1 -> 20
     // chunks).
     uint64_t chunks = 1;
@@ -952,12 +1140,12 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     if (mode == rt::MODE_HASH && spp > 1) {
         uint64_t per_lane = 128, min_samples = 256;
         if (accel == rt::ACCEL_BRUTE) min_samples = std::min<uint64_t>(256, std::max<uint64_t>(4, 2560 / std::max(1u, d.n_spheres)));
-        if (const char* e = std::getenv("RT_UNITS_PER_LANE")) per_lane = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
-        if (const char* e = std::getenv("RT_UNIT_MIN_SAMPLES")) min_samples = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));
+        per_lane = std::max<uint64_t>(1, uint64_t(Tuning::get(ctx->tune.units_per_lane, double(per_lane))));
+        min_samples = std::max<uint64_t>(1, uint64_t(Tuning::get(ctx->tune.unit_min_samples, double(min_samples))));
         const uint64_t pixels = uint64_t(band_width) * band_height;
         chunks = std::min<uint64_t>((lanes * per_lane + pixels - 1) / pixels, std::max<uint64_t>(1, spp / min_samples));
-        if (const char* e = std::getenv("RT_SAMPLE_CHUNKS")) {
-            chunks = std::strtoull(e, nullptr, 10);
+        if (ctx->tune.sample_chunks != Tuning::kUnset) {
+            chunks = uint64_t(ctx->tune.sample_chunks);
             chunks_forced = true;
         }
         chunks = std::max<uint64_t>(1, std::min<uint64_t>({chunks, spp, 4096}));
@@ -985,20 +1173,20 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
         P.fixed = ctx->fixed;
     }
     // Longest-processing-time-first hand-out from the last launch of this band geometry: tiles
-    // in descending order of their longest unit chain (RT_SCHEDULE=rowmajor | sum: A/B only);
-    // this launch records the next costs.
+    // in descending order of their longest unit chain (tuning schedule 1 = row-major, 2 = by the
+    // tile's summed chains: A/B only); this launch records the next costs.
     if (accel != rt::ACCEL_BRUTE) {
         rt::TileSchedule& sc = ctx->sched;
         RT_HIP(rt::schedule_reserve(sc, uint32_t(n_tiles), st));
-        const char* e = std::getenv("RT_SCHEDULE");
-        const bool lpt = !(e && std::strcmp(e, "rowmajor") == 0);
+        const double sched = Tuning::get(ctx->tune.schedule, 0);
+        const bool lpt = sched != 1;
         if (lpt && sc.valid) {
             RT_HIP(rt::schedule_order(sc, st));
             P.tile_order = sc.order;
         }
         RT_HIP(hipMemsetAsync(sc.cost[sc.cur], 0, size_t(sc.n) * 4, st));
         P.tile_cost = sc.cost[sc.cur];
-        P.tile_cost_sum = (e && std::strcmp(e, "sum") == 0) ? 1u : 0u;
+        P.tile_cost_sum = sched == 2 ? 1u : 0u;
     }
     // Head and tail of the LPT order (HASH): the frame's tail is made of the units
     // still running when the queue runs dry, so only the last ranks (the shortest fifth of the
@@ -1009,8 +1197,8 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     // 25 -> 3 head / 10 tail chunks, config 5: 3 -> 1 / 3. A sixth of the units at config 3, so
     // fewer unit starts and flushes, and fewer 64-bit fixed-point atomics, whose memory-side requests are most of the
     // kernel's HBM traffic: 6.6 -> 0.98 GB per frame at -0.6 % frame time (10 tail chunks; 25:
-    // 1.6 GB at -0.9 %; profiles/r03_tail_chunks_traffic.txt). RT_HEAD_CHUNKS / RT_TAIL_TILES_PM
-    // (tail tiles per mille) override; RT_SAMPLE_CHUNKS sets the tail count itself.
+    // 1.6 GB at -0.9 %; profiles/r03_tail_chunks_traffic.txt). Tuning head_chunks / tail_tiles_pm
+    // (tail tiles per mille) override; sample_chunks sets the tail count itself.
     uint64_t head_tiles = 0, head_chunks = chunks;
     if (mode == rt::MODE_HASH && chunks > 1 && P.tile_order) {
         const uint64_t pixels = uint64_t(band_width) * band_height;
@@ -1018,9 +1206,8 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
         // tail units: at most 2.5x the uniform ones, and at least 3x shorter than the head's
         const uint64_t tail_chunks =
             chunks_forced ? chunks : std::max<uint64_t>((chunks * 2 + 4) / 5, std::min<uint64_t>(chunks, 3 * head_chunks));
-        uint64_t tail_pm = 200;
-        if (const char* e = std::getenv("RT_HEAD_CHUNKS")) head_chunks = std::strtoull(e, nullptr, 10);
-        if (const char* e = std::getenv("RT_TAIL_TILES_PM")) tail_pm = std::strtoull(e, nullptr, 10);
+        head_chunks = uint64_t(Tuning::get(ctx->tune.head_chunks, double(head_chunks)));
+        const uint64_t tail_pm = uint64_t(Tuning::get(ctx->tune.tail_tiles_pm, 200));
         head_chunks = std::max<uint64_t>(1, std::min<uint64_t>(head_chunks, tail_chunks));
         const uint64_t tail = std::min<uint64_t>(n_tiles, (n_tiles * std::min<uint64_t>(tail_pm, 1000) + 999) / 1000);
         if (head_chunks < tail_chunks) {
@@ -1048,17 +1235,15 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     {   // Block hand-out: the last `reserve` units go out one by one. Measured
         // (scripts/refill_ab.py, 1080p): 0 to 32 Ki are within 1 %, one pixel per lane of the
         // grid (262 Ki) is 10-15 % slower at 13-50 spp.
-        uint64_t reserve = 8192;
-        if (const char* e = std::getenv("RT_REFILL_RESERVE")) reserve = std::strtoull(e, nullptr, 10);
+        const uint64_t reserve = uint64_t(Tuning::get(ctx->tune.refill_reserve, 8192));
         P.n_block_units = P.n_units > reserve ? uint32_t((P.n_units - reserve) & ~uint64_t(63)) : 0u;
         P.first_blocks = uint32_t(std::min<uint64_t>(uint64_t(grid) * blk / 64u, P.n_block_units / 64u));
         // A STREAM frame is as long as its longest pixel chain; the waves that
         // start on the longest-chain tiles of the LPT order take no further work, so no refill of
         // their other lanes slows the chain down. 1/512 of the waves (32 on a full MI355X):
-        // 12 spp -3.4 %, 50 spp -3 %, 100 spp +-0 (scripts/env_ab.py RT_ISOLATE_TILES). HASH
+        // 12 spp -3.4 %, 50 spp -3 %, 100 spp +-0 (scripts/env_ab.py isolate_tiles). HASH
         // units are short: no isolation.
-        uint64_t iso = uint64_t(grid) * blk / 64u / 512u;
-        if (const char* e = std::getenv("RT_ISOLATE_TILES")) iso = std::strtoull(e, nullptr, 10);
+        const uint64_t iso = uint64_t(Tuning::get(ctx->tune.isolate_tiles, double(uint64_t(grid) * blk / 64u / 512u)));
         P.isolate_blocks = (P.tile_order && mode == rt::MODE_STREAM) ? uint32_t(std::min<uint64_t>(P.first_blocks, iso)) : 0u;
         if (P.first_blocks) RT_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&ctx->counters->work_head),
                                                      int(P.first_blocks * 64u), 1, st));
@@ -1081,6 +1266,11 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     if (P.tile_cost) {
         ctx->sched.cur ^= 1;
         ctx->sched.valid = true;
+    }
+    if (ctx->slot_cur >= 0) {   // the next build into this arena waits for this launch
+        SceneSlot& sl = ctx->slot[ctx->slot_cur];
+        RT_HIP(hipEventRecord(sl.ev_free, st));
+        sl.used = true;
     }
     return mark_issued(ctx, st);
 }
@@ -1217,8 +1407,41 @@ int rt_debug_kernel_times(rt_context* ctx, float* out_ms, uint32_t capacity, uin
     return RT_OK;
 }
 
+#ifndef RT_BUILD_ARCH
+#define RT_BUILD_ARCH "unknown"
+#endif
+#ifndef RT_BUILD_FLAGS
+#define RT_BUILD_FLAGS "unknown"
+#endif
+#ifndef RT_BUILD_VARIANT
+#define RT_BUILD_VARIANT ""
+#endif
+// The Makefile passes the real architecture, device flags and the variant flags of an A/B build
+// (make variant VFLAGS=...), so a variant never reports itself as the shipped build.
 const char* rt_build_info(void) {
-    return "sources_sha256=" RT_SOURCES_SHA256 ";arch=gfx950;flags=-O3 -ffp-contract=off -fno-slp-vectorize";
+    return "sources_sha256=" RT_SOURCES_SHA256 ";arch=" RT_BUILD_ARCH ";flags=" RT_BUILD_FLAGS
+           ";variant=" RT_BUILD_VARIANT;
+}
+
+int rt_debug_tune(rt_context* ctx, const char* key, double value) {
+    if (!ctx || !key) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    static const struct { const char* name; double Tuning::*field; } kKeys[] = {
+        {"grid", &Tuning::grid}, {"grid_scale", &Tuning::grid_scale}, {"grid_coop", &Tuning::grid_coop},
+        {"grid_rec", &Tuning::grid_rec}, {"grid_full_slack", &Tuning::grid_full_slack},
+        {"units_per_lane", &Tuning::units_per_lane}, {"unit_min_samples", &Tuning::unit_min_samples},
+        {"sample_chunks", &Tuning::sample_chunks}, {"head_chunks", &Tuning::head_chunks},
+        {"tail_tiles_pm", &Tuning::tail_tiles_pm}, {"schedule", &Tuning::schedule},
+        {"refill_reserve", &Tuning::refill_reserve}, {"isolate_tiles", &Tuning::isolate_tiles},
+        {"sah_knobs", &Tuning::sah_knobs}};
+    if (!(value >= 0.0 || value == Tuning::kUnset))
+        return fail(RT_ERR_INVALID_ARGUMENT, "tuning values are >= 0 (-1 restores the default)");
+    for (const auto& k : kKeys) {
+        if (std::strcmp(k.name, key) == 0) {
+            ctx->tune.*(k.field) = value;
+            return RT_OK;
+        }
+    }
+    return fail(RT_ERR_INVALID_ARGUMENT, std::string("unknown tuning key ") + key);
 }
 
 int rt_debug_launch_info(rt_context* ctx, uint32_t* out4) {
@@ -1228,10 +1451,9 @@ int rt_debug_launch_info(rt_context* ctx, uint32_t* out4) {
         out4[1] = ctx->last_accel;
         out4[2] = uint32_t(ctx->last_lds);
     } else {   // no launch yet: the default form of the current scene (camera within its pad radius)
-        const bool grid = ctx->has_grid && (ctx->grid_bytes || !ctx->oct_bytes);
-        out4[1] = grid ? (ctx->grid_bytes ? rt::ACCEL_GRID : rt::ACCEL_GRID_GLOBAL) : ctx->oct_bytes ? rt::ACCEL_LBVH_OCT
-                  : ctx->lds1_bytes ? rt::ACCEL_LBVH_LDS : ctx->gpu_tree ? rt::ACCEL_LBVH_TOP : rt::ACCEL_LBVH_GLOBAL;
-        out4[2] = uint32_t(grid ? ctx->grid_bytes : ctx->oct_bytes ? ctx->oct_bytes : ctx->lds1_bytes);
+        size_t lds = 0;
+        out4[1] = choose_accel(ctx, false, 0u, 0.0f, &lds);
+        out4[2] = uint32_t(lds);
     }
     out4[3] = uint32_t(ctx->cu_count);
     return RT_OK;

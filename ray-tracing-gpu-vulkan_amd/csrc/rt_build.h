@@ -18,6 +18,8 @@ struct BuildSummary {
     uint32_t rmin_o;                 // ... and of the smallest small radius
     uint32_t cmin_o[3], cmax_o[3];   // centroid bounds of the small spheres (Morton frame)
     uint32_t colour_out_of_range;    // != 0: some sphere colour leaves [0, 1] (colours_in_unit)
+    float root_lo[3], root_hi[3];    // unpadded root box (the small spheres' AABB union): the grid's
+                                     // bounds, so the host needs no second read-back
 };
 float summary_float(uint32_t ordered);
 
@@ -57,7 +59,8 @@ void build_release(BuildWorkspace& ws);
 
 // Full build (refit = false) or refit of the previous topology (refit = true: same n, same big
 // set and leaf assignment; boxes, records, radii bounds and padding recomputed). Asynchronous on
-// `st` except for the final copy of the summary into *out (synchronous).
+// `st`, the summary included: it is copied into *out (pinned host memory), valid once `st` has
+// reached that point (the caller records an event after this call).
 hipError_t build_scene_gpu(BuildWorkspace& ws, const Sphere* d_spheres, uint32_t n,
                            const BuildOutputs& o, bool refit, hipStream_t st, BuildSummary* out);
 
@@ -73,6 +76,7 @@ struct TileSchedule {
     uint32_t* order = nullptr;     // hand-out rank -> tile
     uint32_t* keys = nullptr;      // sort scratch
     uint32_t* iota = nullptr;
+    uint32_t* norm = nullptr;      // costs scaled by their chunk counts (schedule_order's sort keys)
     void* tmp = nullptr;
     size_t tmp_bytes = 0;
     int cur = 0;                   // table the next launch records into

@@ -323,6 +323,9 @@ __global__ void __launch_bounds__(kBlock) k_emit(const Sphere* __restrict__ sph,
     nd.escape = esc >= total ? kEnd : esc;
     nd.first_count = leafy ? (((kLeafMax * lidx) << 4) | sz) : 0u;
     nodes_raw[pos] = nd;
+    if (pos == 0u) {   // the root: the grid's bounds (read back with the summary)
+        for (int k = 0; k < 3; k++) { S->root_lo[k] = b[k]; S->root_hi[k] = b[k + 3]; }
+    }
     // padding for origins within the scene radius and a nearby camera (rt_api.cpp pad_for)
     const float pad_radius = o2f(S->R_o) * 1.01f + 100.0f;
     const float pad = 18.0f * 5.9604645e-8f * pad_radius;
@@ -557,13 +560,12 @@ hipError_t build_scene_gpu(BuildWorkspace& ws, const Sphere* sph, uint32_t n, co
     }
     if (hipError_t e = hipGetLastError()) return e;
     if (hipError_t e = hipMemcpyAsync(out, ws.S, sizeof(BuildSummary), hipMemcpyDeviceToHost, st)) return e;
-    if (hipError_t e = hipStreamSynchronize(st)) return e;
     if (!refit) ws.topo_n = n;
     return hipSuccess;
 }
 
 void schedule_release(TileSchedule& s) {
-    void* ptrs[] = {s.cost[0], s.cost[1], s.order, s.keys, s.iota, s.tmp};
+    void* ptrs[] = {s.cost[0], s.cost[1], s.order, s.keys, s.iota, s.norm, s.tmp};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     s = TileSchedule{};
@@ -578,6 +580,7 @@ hipError_t schedule_reserve(TileSchedule& s, uint32_t n, hipStream_t st) {
     if (e == hipSuccess) e = alloc(&s.order, n);
     if (e == hipSuccess) e = alloc(&s.keys, n);
     if (e == hipSuccess) e = alloc(&s.iota, n);
+    if (e == hipSuccess) e = alloc(&s.norm, n);
     if (e == hipSuccess)
         e = hipcub::DeviceRadixSort::SortPairsDescending(nullptr, s.tmp_bytes, s.cost[0], s.keys, s.iota, s.order,
                                                          int(n), 0, 32);
@@ -596,25 +599,29 @@ hipError_t schedule_reserve(TileSchedule& s, uint32_t n, hipStream_t st) {
     return hipSuccess;
 }
 
-// cost[order[r]] *= the chunk count of rank r in the launch that recorded it (saturating).
-__global__ void k_cost_norm(uint32_t* __restrict__ cost, const uint32_t* __restrict__ order, uint32_t n,
-                            uint32_t head_tiles, uint32_t head_chunks, uint32_t chunks) {
+// norm[order[r]] = cost[order[r]] x the chunk count of rank r in the launch that recorded it
+// (saturating). Written beside the recorded costs, never over them: schedule_order may run again on
+// the same record (a launch that fails after it), and must not scale it twice.
+__global__ void k_cost_norm(const uint32_t* __restrict__ cost, const uint32_t* __restrict__ order, uint32_t n,
+                            uint32_t head_tiles, uint32_t head_chunks, uint32_t chunks, uint32_t* __restrict__ norm) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
     const uint32_t t = order[r];
     const uint64_t v = uint64_t(cost[t]) * (r < head_tiles ? head_chunks : chunks);
-    cost[t] = uint32_t(v < 0xffffffffull ? v : 0xffffffffull);
+    norm[t] = uint32_t(v < 0xffffffffull ? v : 0xffffffffull);
 }
 
 hipError_t schedule_order(TileSchedule& s, hipStream_t st) {
     const int last = s.cur ^ 1;
+    const uint32_t* key = s.cost[last];
     if (s.rec_head_tiles[last]) {   // `order` still holds the ranks that launch handed out
         k_cost_norm<<<blocks(s.n), kBlock, 0, st>>>(s.cost[last], s.order, s.n, s.rec_head_tiles[last],
-                                                   s.rec_head_chunks[last], s.rec_chunks[last]);
+                                                   s.rec_head_chunks[last], s.rec_chunks[last], s.norm);
         if (hipError_t e = hipGetLastError()) return e;
+        key = s.norm;
     }
     size_t tb = s.tmp_bytes;
-    return hipcub::DeviceRadixSort::SortPairsDescending(s.tmp, tb, s.cost[s.cur ^ 1], s.keys, s.iota, s.order,
+    return hipcub::DeviceRadixSort::SortPairsDescending(s.tmp, tb, key, s.keys, s.iota, s.order,
                                                         int(s.n), 0, 32, st);
 }
 

@@ -265,7 +265,7 @@ struct Builder {
 
 }  // namespace
 
-void build_lbvh_host(const Sphere* sph, uint32_t n, HostBvh& out, bool sah) {
+void build_lbvh_host(const Sphere* sph, uint32_t n, HostBvh& out, bool sah, uint32_t sah_knobs) {
     out = HostBvh{};
     if (n == 0) return;
     if (n >= (1u << 27)) return;   // leaf references hold 28-bit slot indices
@@ -314,11 +314,9 @@ void build_lbvh_host(const Sphere* sph, uint32_t n, HostBvh& out, bool sah) {
     // 3-4. hierarchy in depth-first order
     out.nodes.reserve(2 * prims.size());
     SahKnobs knobs;
-    if (const char* k = std::getenv("RT_SAH_KNOBS")) {   // e.g. "classic,sweep,order1"
-        knobs.classic = std::strstr(k, "classic") != nullptr;
-        knobs.sweep = std::strstr(k, "sweep") != nullptr;
-        knobs.order = std::strstr(k, "order1") ? 1 : std::strstr(k, "order2") ? 2 : 0;
-    }
+    knobs.classic = (sah_knobs & 1u) != 0;
+    knobs.sweep = (sah_knobs & 2u) != 0;
+    knobs.order = int((sah_knobs >> 2) & 3u);
     Builder b{sph, prims, out, sah, knobs};
     b.build(0, uint32_t(prims.size()));
     for (BvhNode& nd : out.nodes)

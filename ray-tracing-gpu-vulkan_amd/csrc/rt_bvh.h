@@ -19,7 +19,9 @@ struct HostBvh {
 };
 
 // sah: binned surface-area splits (the default tree for small scenes); else the Morton radix
-// split that rt_build.hip reproduces on the device.
-void build_lbvh_host(const Sphere* spheres, uint32_t n, HostBvh& out, bool sah);
+// split that rt_build.hip reproduces on the device. sah_knobs (A/B only, rt_debug_tune "sah_knobs";
+// 0 = the measured best): bit 0 classic cost (area x spheres), bit 1 exact sweep, bits 2-3 child
+// order (1 larger-area child first, 2 smaller first).
+void build_lbvh_host(const Sphere* spheres, uint32_t n, HostBvh& out, bool sah, uint32_t sah_knobs = 0);
 
 }  // namespace rt

@@ -4,9 +4,25 @@
 
 #include <hip/hip_runtime.h>
 
+#include <memory>
 #include <string>
 
+#include "../../include/rt_mi355x.h"
+
 namespace rt {
+
+// A host-built scene (tree, grid, records; rt_api.cpp), built once and uploadable to any context:
+// rt_multi_set_scene builds it for the first device and uploads the same package to the others.
+struct HostPackage;
+struct HostPackageDeleter { void operator()(HostPackage* p) const; };
+using HostPackagePtr = std::unique_ptr<HostPackage, HostPackageDeleter>;
+
+// rt_set_scene in two halves, so that rt_multi_set_scene issues every device's build before it
+// waits for any: begin builds a host scene (or takes *shared) and uploads it, or starts a device
+// build on the context's build stream; end waits for the device build's summary and builds its
+// grid. Every begin that succeeds must be followed by end on the same context.
+int set_scene_begin(rt_context* ctx, const Sphere* spheres, uint32_t count, void* stream, HostPackagePtr* shared);
+int set_scene_end(rt_context* ctx);
 
 // Message of the calling thread's last failure (rt_last_error()).
 extern thread_local std::string g_last_error;

@@ -251,12 +251,11 @@ constexpr int kFixedFracBits = 24;
 constexpr uint32_t kFixedFlush = 128;
 
 // "Big" spheres (radius above a scene-relative threshold, e.g. the ground sphere) are tested by
-// every segment before the tree walk; at most kBigMax of them. The LBVH kernels stage their
-// records (center, radius) and ids in LDS once per block: kBigLdsBytes at the end of the block's
-// dynamic LDS.
+// every segment before the tree walk; at most kBigMax of them. A one-wave kernel writes their
+// records (center, radius) and ids into TraceParams::big_tab before each launch; the walk kernels
+// read them through the scalar cache (rt_kernels.hip setup_ray).
 constexpr uint32_t kBigMax = 64;
 constexpr uint32_t kNoRowsLds = 0xffffffffu;
-constexpr uint32_t kBigLdsBytes = kBigMax * 16u + kBigMax * 4u;
 constexpr uint32_t kHashMaxSpp = 1u << 19;
 
 }  // namespace rt

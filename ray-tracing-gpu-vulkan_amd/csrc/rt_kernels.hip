@@ -25,23 +25,6 @@ using namespace rtd;
 
 namespace {
 
-// Code shape switches (1 = shipped; 0 builds the previous form for A/B timing): the winner's
-// shading records loaded with its gate; the LDS grid's reference records read one ahead; tail
-// stealing in the counter-based stream.
-#ifndef RT_LDS_PIPE
-#define RT_LDS_PIPE 1
-#endif
-#ifndef RT_TAIL_STEAL
-#define RT_TAIL_STEAL 1
-#endif
-#ifndef RT_FUSE_GATE_LOADS
-#define RT_FUSE_GATE_LOADS 1
-#endif
-// The big spheres of every segment through the scalar cache (TraceParams::big_tab) instead of an
-// LDS table (config 3 -1.6 %, reference stream -1.7 %, config 5 -2.2 %; 0 builds the LDS form).
-#ifndef RT_SBIG
-#define RT_SBIG 1
-#endif
 constexpr float T_MIN = 0.001f;               // shader.rgen:75
 constexpr float T_MAX_SUCC = 0x1.388002p+13f; // successor of 10000.0f (shader.rgen:26): a report
                                               // at exactly tMax is accepted, so compare with '<'.
@@ -557,9 +540,7 @@ __device__ __forceinline__ void steal_tail(const rt::TraceParams& P, uint32_t la
 template <int MODE, bool COUNT>
 __device__ __forceinline__ void refill(const rt::TraceParams& P, uint32_t lane, uint32_t& st, Path& ps,
                                        WaveBlock& blk, Stamps& stamps) {
-#if RT_TAIL_STEAL
     if (MODE == rt::MODE_HASH && blk.done) steal_tail<COUNT>(P, lane, st, ps);   // wave-uniform condition
-#endif
     const unsigned long long need = __ballot(st == ST_NEED_UNIT);
     if (!need) return;
     STAMP(5);
@@ -1003,28 +984,8 @@ __device__ __forceinline__ uint32_t octant(const V3 d) {
     return (__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 31) << 1) | ((__float_as_uint(d.z) >> 31) << 2);
 }
 
-// Big-sphere table of a block (LDS, rt_internal.h kBigLdsBytes): records {cx, cy, cz, r} and ids,
-// n_big rounded up to a multiple of 4 by repeating the last one (a duplicate of an already tested
-// sphere can never change (best, bi)). Staged once per block, read by every segment with a
-// wave-uniform address (LDS broadcast): one round trip instead of the dependent id -> record ->
-// radius scalar loads per segment.
-struct BigTable { const float4* rec; const uint32_t* id; };
-
-__device__ __forceinline__ BigTable stage_big(const rt::TraceParams& P, float4* lds_at, uint32_t tid, uint32_t nthr) {
-    if (RT_SBIG) return BigTable{nullptr, nullptr};   // setup_ray reads TraceParams::big_tab
-    const uint32_t nb4 = (P.n_big + 3u) & ~3u;
-    uint32_t* ids = reinterpret_cast<uint32_t*>(lds_at + rt::kBigMax);
-    for (uint32_t i = tid; i < nb4; i += nthr) {
-        const uint32_t id = P.big_ids[min(i, P.n_big - 1u)];
-        const rt::GeomRec g = P.geom[id];
-        lds_at[i] = make_float4(g.cx, g.cy, g.cz, P.radius[id]);
-        ids[i] = id;
-    }
-    return BigTable{lds_at, ids};
-}
-
 // New segment: hoisted per-ray terms and the exhaustive big spheres.
-__device__ __forceinline__ void setup_ray(const rt::TraceParams& P, const BigTable& big, Ray& r, uint32_t& n_sph) {
+__device__ __forceinline__ void setup_ray(const rt::TraceParams& P, Ray& r, uint32_t& n_sph) {
     r.a = dot(r.d, r.d);
     r.ia = rcp_cr(r.a);
     r.inv = v3(rcp_cr(r.d.x), rcp_cr(r.d.y), rcp_cr(r.d.z));
@@ -1033,9 +994,9 @@ __device__ __forceinline__ void setup_ray(const rt::TraceParams& P, const BigTab
     // beyond it, and the (t bits, id) keys of the cooperative walk order the same way.
     r.best = 10000.0f;
     r.bi = 0xffffffffu;
-#if RT_SBIG
-    // records and ids through the scalar cache (SGPR operands, no LDS round trip); the four
-    // discriminants stay in registers for the candidate passes, which run per sphere with a
+    // records and ids through the scalar cache (TraceParams::big_tab, SGPR operands, no LDS round
+    // trip: config 3 -1.6 %, reference stream -1.7 %, config 5 -2.2 % against an LDS table); the
+    // four discriminants stay in registers for the candidate passes, which run per sphere with a
     // wave-uniform record (no reload, no per-lane record select)
     typedef const __attribute__((address_space(4))) float* ConstF;
     typedef const __attribute__((address_space(4))) uint32_t* ConstU;
@@ -1070,16 +1031,6 @@ __device__ __forceinline__ void setup_ray(const rt::TraceParams& P, const BigTab
             }
         }
     }
-#else
-    for (uint32_t k0 = 0; k0 < P.n_big; k0 += 4) {   // wave-uniform: LDS broadcast reads
-        const float4 b0 = big.rec[k0], b1 = big.rec[k0 + 1], b2 = big.rec[k0 + 2], b3 = big.rec[k0 + 3];
-        const uint4 id = *reinterpret_cast<const uint4*>(big.id + k0);
-        float unused_limit = 0.0f;
-        test4(b0, b1, b2, b3, [&](uint32_t k) { return lds_reload(big.rec + k0 + k); },
-                    [&](uint32_t k) { return k == 0 ? id.x : k == 1 ? id.y : k == 2 ? id.z : id.w; },
-              r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, unused_limit, P);
-    }
-#endif
     n_sph += P.n_big;
     r.limit = cull_limit(P, r.best);
     r.walk = P.nodes != nullptr || P.cell_start != nullptr;
@@ -1196,8 +1147,7 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
             ++j;
           }
         }
-#if RT_LDS_PIPE
-        if (!PAIRS && j < e) {   // two records in flight, no register copies (unrolled by two)
+        if (!PAIRS && j < e) {   // LDS: two records in flight, no register copies (unrolled by two)
             float4 A = rec[j], B;
             for (;;) {
                 UTIL(1, true);
@@ -1212,13 +1162,6 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
                 if (++j >= e) break;
             }
         }
-#else
-        for (; j < e; ++j) {   // from LDS one at a time (pairs measured 1 % slower there)
-            UTIL(1, true);
-            test1(rec[j], [&] { return ids[j]; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
-            if (COUNT) n_sph++;
-        }
-#endif
         UTIL(0, true);
         const float tm = fminf(fminf(tx, ty), tz);
         if (!(tm <= r.limit)) break;   // the next cell starts beyond every closer candidate
@@ -1558,8 +1501,7 @@ template <bool COUNT, int LAYOUT, int MODE, bool REC = false>
 __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4* __restrict__ nodes4,
                                           const float4* __restrict__ leaf4,
                                           const uint32_t* __restrict__ leaf_ids,
-                                          const float4* __restrict__ geom4, const float4* __restrict__ mat4,
-                                          const BigTable big) {
+                                          const float4* __restrict__ geom4, const float4* __restrict__ mat4) {
     constexpr bool LSUM = MODE == rt::MODE_HASH &&
                           (LAYOUT == LAYOUT_GRID || LAYOUT == LAYOUT_GRID_L2 || LAYOUT == LAYOUT_GRID_COOP);
     const uint32_t lane = lane_id();
@@ -1608,7 +1550,7 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
         STAMP(1);
         UTIL(8, st == ST_TRACING);
         const uint32_t box0 = n_box;
-        if (st == ST_TRACING) setup_ray(P, big, r, n_sph);
+        if (st == ST_TRACING) setup_ray(P, r, n_sph);
         STAMP(2);
         if constexpr (LAYOUT == LAYOUT_GRID_COOP) {   // every lane of the wave takes part (tracing or not)
             grid_walk_coop<COUNT>(P, reinterpret_cast<const uint32_t*>(nodes4), leaf4, leaf_ids, r, st == ST_TRACING,
@@ -1620,7 +1562,6 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
         // get the contract's answer by a wave-cooperative gated brute force. The winner's shading
         // records are loaded with the gate's (one round trip to L2 per segment, not two).
         HitRec hr{};
-#if RT_FUSE_GATE_LOADS
         float rad = 0.0f;
         if (st == ST_TRACING && r.bi != 0xffffffffu) {
             hr = load_hit(geom4, mat4, r.bi);
@@ -1633,13 +1574,6 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
             regate_brute<COUNT>(P, reinterpret_cast<const float4*>(P.geom), lane, regate, r);
             if (((regate >> lane) & 1ull) && r.bi != 0xffffffffu) hr = load_hit(geom4, mat4, r.bi);
         }
-#else
-        const unsigned long long regate =
-            __ballot(st == ST_TRACING && (P.force_regate || !winner_gated<REC>(P, geom4, r)));
-        if (__builtin_expect(regate != 0ull, 0))
-            regate_brute<COUNT>(P, reinterpret_cast<const float4*>(P.geom), lane, regate, r);
-        if (st == ST_TRACING && r.bi != 0xffffffffu) hr = load_hit(geom4, mat4, r.bi);
-#endif
         if (COUNT && st == ST_TRACING) {   // walk-length histogram (diagnostic, COUNT builds only)
             const uint32_t len = min(n_box - box0, 63u);
             atomicAdd(&P.counters->walk_hist[r.bi != 0xffffffffu ? 1 : 0][len], 1ull);
@@ -1682,21 +1616,19 @@ template <bool COUNT, int MODE>
 __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace_global_kernel(const rt::TraceParams P) {
     UTIL_INIT;
     PLACEMENT_RECORD(P);
-    extern __shared__ float4 lds[];   // the big-sphere table only
-    const BigTable big = stage_big(P, lds, threadIdx.x, kTraceBlock);
     stage_walk_params(P, threadIdx.x);
     stage_rows(P, threadIdx.x, kTraceBlock);
     __syncthreads();
     lbvh_loop<COUNT, LAYOUT_GLOBAL, MODE>(P, reinterpret_cast<const float4*>(P.nodes),
                                           reinterpret_cast<const float4*>(P.leaf_geom), P.leaf_ids,
                                           reinterpret_cast<const float4*>(P.geom),
-                                          reinterpret_cast<const float4*>(P.mat), big);
+                                          reinterpret_cast<const float4*>(P.mat));
 }
 
 // LBVH kernel with the whole tree staged in LDS, once per persistent block (one 1024-thread block
 // per CU). Staged nodes use the AB layout (node_hit); NOCT = 8 stages one copy per ray direction
 // octant, each in its own near-child-first order when the host provides one (nodes_oct). LDS:
-// [nodes | leaf spheres | leaf ids | big-sphere table]. The geometry + material records read by
+// [nodes | leaf spheres | leaf ids]. The geometry + material records read by
 // shading stay in HBM: one random record per hit is an L2 hit (staging them in LDS measured the
 // same), and the LDS they would take fits bigger trees as octant copies.
 template <bool COUNT, uint32_t NOCT, int MODE>
@@ -1741,33 +1673,30 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
         lds[n_node4 + n_leaf4 + i] = make_float4(__uint_as_float(v.x), __uint_as_float(v.y),
                                                  __uint_as_float(v.z), __uint_as_float(v.w));
     }
-    const uint32_t base = n_node4 + n_leaf4 + n_id4;
     const float4* geom4 = reinterpret_cast<const float4*>(P.geom);
     const float4* mat4 = reinterpret_cast<const float4*>(P.mat);
-    const BigTable big = stage_big(P, lds + base, threadIdx.x, kTraceBlock);
     stage_walk_params(P, threadIdx.x);
     stage_rows(P, threadIdx.x, kTraceBlock);
     __syncthreads();
     lbvh_loop<COUNT, NOCT == 8 ? LAYOUT_OCT : LAYOUT_LDS1, MODE>(
-        P, lds, lds + n_node4, reinterpret_cast<const uint32_t*>(lds + n_node4 + n_leaf4), geom4, mat4, big);
+        P, lds, lds + n_node4, reinterpret_cast<const uint32_t*>(lds + n_node4 + n_leaf4), geom4, mat4);
 }
 
 // Grid kernel (ACCEL_GRID): the grid's cell offsets and references staged in LDS once per
-// persistent block: [references (float4) | reference ids | cell offsets | big-sphere table].
+// persistent block: [references (float4) | reference ids | cell offsets | shading records (REC)].
 template <bool COUNT, int MODE, bool IN_LDS, bool COOP = false, bool REC = false>
 __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace_grid_kernel(const rt::TraceParams P) {
     UTIL_INIT;
     PLACEMENT_RECORD(P);
     extern __shared__ float4 lds[];
     if (!IN_LDS) {   // grids too big for LDS: offsets and references from L2 / HBM
-        const BigTable big = stage_big(P, lds, threadIdx.x, kTraceBlock);
         stage_walk_params(P, threadIdx.x);
-    stage_rows(P, threadIdx.x, kTraceBlock);
+        stage_rows(P, threadIdx.x, kTraceBlock);
         __syncthreads();
         lbvh_loop<COUNT, COOP ? LAYOUT_GRID_COOP : LAYOUT_GRID_L2, MODE>(P, reinterpret_cast<const float4*>(P.cell_start),
                                             reinterpret_cast<const float4*>(P.grid_rec), P.grid_ids,
                                             reinterpret_cast<const float4*>(P.geom),
-                                            reinterpret_cast<const float4*>(P.mat), big);
+                                            reinterpret_cast<const float4*>(P.mat));
         return;
     }
     const uint32_t nr = P.grid.n_refs, nc1 = P.grid.n_cells + 1u;
@@ -1778,11 +1707,10 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
     for (uint32_t i = threadIdx.x; i < nr; i += kTraceBlock) ids[i] = P.grid_ids[i];
     uint32_t* cst = reinterpret_cast<uint32_t*>(lds + nr + n_id4);
     for (uint32_t i = threadIdx.x; i < nc1; i += kTraceBlock) cst[i] = P.cell_start[i];
-    const BigTable big = stage_big(P, lds + nr + n_id4 + n_cs4, threadIdx.x, kTraceBlock);
     stage_walk_params(P, threadIdx.x);
     stage_rows(P, threadIdx.x, kTraceBlock);
     if (REC) {   // the winner's gate and shading records in LDS too: {cx, cy, cz, r} + 2 x MatRec float4
-        float4* srec = lds + nr + n_id4 + n_cs4 + rt::kBigLdsBytes / 16u;
+        float4* srec = lds + nr + n_id4 + n_cs4;
         float4* smat = srec + P.n_spheres;
         const float4* mat4 = reinterpret_cast<const float4*>(P.mat);
         for (uint32_t i = threadIdx.x; i < P.n_spheres; i += kTraceBlock) {
@@ -1792,13 +1720,13 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
             smat[2 * i + 1] = mat4[2 * i + 1];
         }
         __syncthreads();
-        lbvh_loop<COUNT, LAYOUT_GRID, MODE, true>(P, reinterpret_cast<const float4*>(cst), lds, ids, srec, smat, big);
+        lbvh_loop<COUNT, LAYOUT_GRID, MODE, true>(P, reinterpret_cast<const float4*>(cst), lds, ids, srec, smat);
         return;
     }
     __syncthreads();
     lbvh_loop<COUNT, COOP ? LAYOUT_GRID_COOP : LAYOUT_GRID, MODE>(P, reinterpret_cast<const float4*>(cst), lds, ids,
                                         reinterpret_cast<const float4*>(P.geom),
-                                        reinterpret_cast<const float4*>(P.mat), big);
+                                        reinterpret_cast<const float4*>(P.mat));
 }
 
 // LBVH kernel for trees too big for LDS: the treelet (rt_build.hip build_treelet) is staged in LDS
@@ -1820,13 +1748,12 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
         lds[2 * i + 1] = make_float4(B.x, B.y, __uint_as_float(miss == END ? END : lbase + miss * 32u),
                                      __uint_as_float(int32_t(hit) >= 0 ? lbase + hit * 32u : hit));
     }
-    const BigTable big = stage_big(P, lds + 2u * rt::kTreeletCap, threadIdx.x, kTraceBlock);
     stage_walk_params(P, threadIdx.x);
     stage_rows(P, threadIdx.x, kTraceBlock);
     __syncthreads();
     lbvh_loop<COUNT, LAYOUT_TOP, MODE>(P, lds, reinterpret_cast<const float4*>(P.leaf_geom), P.leaf_ids,
                                        reinterpret_cast<const float4*>(P.geom),
-                                       reinterpret_cast<const float4*>(P.mat), big);
+                                       reinterpret_cast<const float4*>(P.mat));
 }
 
 // HASH-mode resolve (shader.rgen:53-66 for the chunked frame): per texel, the fixed-point sum of

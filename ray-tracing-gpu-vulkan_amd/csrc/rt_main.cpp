@@ -124,6 +124,7 @@ int run_frames(uint32_t samples, uint32_t width, uint32_t height, uint32_t gpu_c
 
 int main(int argc, const char** argv) {
     uint32_t samples = 10, width = 1920, height = 1080, gpu_count = 1, frames = 0, rng_mode = RT_RNG_PIXEL_STREAM;
+    bool rng_explicit = false;
     bool store = false, animate = false;
     for (int i = 1; i < argc; i++) {
         const std::string a = argv[i];
@@ -148,6 +149,7 @@ int main(int argc, const char** argv) {
                 return 2;
             }
             rng_mode = std::strcmp(argv[++i], "hash") == 0 ? RT_RNG_SAMPLE_HASH : RT_RNG_PIXEL_STREAM;
+            rng_explicit = true;
         } else if (a == "--samples" || a == "--width" || a == "--height" || a == "--gpus" || a == "--frames") {
             uint32_t v = 0;
             if (i + 1 >= argc || !parse_u32(argv[i + 1], v)) {
@@ -170,8 +172,9 @@ int main(int argc, const char** argv) {
         return 1;
     }
     if (frames > 0) return run_frames(samples, width, height, gpu_count, frames, animate, store, rng_mode);
-    // ray_trace() keeps the reference's signature; its stream is selected through RT_RNG
-    if (rng_mode == RT_RNG_SAMPLE_HASH) setenv("RT_RNG", "hash", 1);
+    // ray_trace() keeps the reference's signature; its stream is selected through RT_RNG. An
+    // explicit --rng wins over the caller's environment; without it RT_RNG passes through.
+    if (rng_explicit) setenv("RT_RNG", rng_mode == RT_RNG_SAMPLE_HASH ? "hash" : "stream", 1);
     ray_trace(samples, store, width, height, gpu_count);
     return 0;
 }

@@ -92,6 +92,26 @@ void free_launches(rt_multi* m) {
     m->key.clear();
 }
 
+// The scene on every device: each device's build is issued before any is waited for (device-built
+// scenes build on every GPU at once, each beside its previous frame), and a host-built scene is
+// built once and uploaded to every device (rt_api.cpp set_scene_begin / set_scene_end).
+int set_scene_all(rt_multi* m) {
+    rt::HostPackagePtr shared;
+    const uint32_t count = uint32_t(m->spheres.size());
+    int rc = RT_OK;
+    size_t begun = 0;
+    for (; begun < m->launches.size(); begun++) {
+        Launch& l = m->launches[begun];
+        rc = rt::set_scene_begin(l.ctx, m->spheres.data(), count, m->stream[l.dev], &shared);
+        if (rc != RT_OK) break;
+    }
+    for (size_t i = 0; i < begun; i++) {   // every begun build is ended, even after a failure
+        const int e = rt::set_scene_end(m->launches[i].ctx);
+        if (rc == RT_OK) rc = e;
+    }
+    return rc;
+}
+
 // (Re)builds the launch list for `key` (one entry per launch: device + global rows). Buffers of
 // a launch are zeroed (accumulate adds to the previous frame of the same partition).
 int set_partition(rt_multi* m, const std::string& key, uint32_t W, uint32_t H,
@@ -118,10 +138,6 @@ int set_partition(rt_multi* m, const std::string& key, uint32_t W, uint32_t H,
             RT_HIP(hipMemset(l.acc, 0, texels * 16));
             RT_HIP(hipMemset(l.out, 0, texels * 4));
         }
-        if (m->scene_set) {
-            if (int rc = rt_set_scene(l.ctx, m->spheres.data(), uint32_t(m->spheres.size()), m->stream[l.dev]))
-                return rc;
-        }
         DeviceGuard g0(0);
         if (nr) {
             RT_HIP(hipMalloc(&l.rows_root, nr * 4));
@@ -131,7 +147,7 @@ int set_partition(rt_multi* m, const std::string& key, uint32_t W, uint32_t H,
         }
     }
     m->key = key;
-    return RT_OK;
+    return m->scene_set ? set_scene_all(m) : RT_OK;
 }
 
 // Strips k = 0, 1, ... of kStrip rows, strip k on device k % n.
@@ -273,8 +289,7 @@ int rt_multi_set_scene(rt_multi* m, const Sphere* spheres, uint32_t count) {
     } catch (const std::exception& e) {
         return fail(RT_ERR_OUT_OF_MEMORY, e.what());
     }
-    for (Launch& l : m->launches)
-        if (int rc = rt_set_scene(l.ctx, m->spheres.data(), count, m->stream[l.dev])) return rc;
+    if (int rc = set_scene_all(m)) return rc;
     m->scene_set = true;
     return RT_OK;
 }

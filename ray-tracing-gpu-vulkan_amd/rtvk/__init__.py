@@ -149,6 +149,12 @@ class Renderer:
         check(fn(self._ctx, spheres_dev.data_ptr() if n else None, n, st))
         self.sphere_count = n
 
+    def tune(self, **kv) -> None:
+        """Launch-plan parameters of this context (rt_debug_tune; tests and A/B timing only): e.g.
+        ``tune(sample_chunks=7)``; None restores a default. No setting changes an image."""
+        for k, v in kv.items():
+            check(self._lib.rt_debug_tune(self._ctx, k.encode(), -1.0 if v is None else float(v)))
+
     def tile_costs(self) -> np.ndarray:
         """Per 8x8 tile of the last LBVH launch, the traced segments of its most expensive pixel
         (row-major tiles; empty before the first launch): the key the next launch hands tiles out
@@ -220,7 +226,7 @@ class Renderer:
         v = (ctypes.c_uint32 * 4)()
         check(self._lib.rt_debug_launch_info(self._ctx, v))
         forms = {1: "brute", 2: "lbvh-global", 3: "lbvh-lds", 4: "lbvh-octant-lds", 5: "lbvh-treelet", 6: "grid-lds", 7: "grid-global",
-                 8: "grid-lds-coop", 9: "grid-global-coop", 10: "grid-lds"}
+                 8: "grid-lds-coop", 9: "grid-global-coop", 10: "grid-lds-rec"}
         return {"chunks": int(v[0]) & 0xffff, "head_chunks": (int(v[0]) >> 16) or None,
                 "form": forms.get(int(v[1]), str(v[1])), "lds_bytes": int(v[2]), "cus": int(v[3])}
 

@@ -128,6 +128,7 @@ EXPORTS = {
     "rt_debug_launch_info": (_I, [_P, _P]),
     "rt_debug_kernel_times": (_I, [_P, _P, _U32, ctypes.POINTER(_U32)]),
     "rt_build_info": (ctypes.c_char_p, []),
+    "rt_debug_tune": (_I, [_P, ctypes.c_char_p, ctypes.c_double]),
     "rt_debug_walk_hist": (_I, [_P, _P]),
     "rt_debug_walk_split": (_I, [_P, _P]),
     "rt_debug_lane_hist": (_I, [_P, _P]),

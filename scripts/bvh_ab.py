@@ -27,7 +27,8 @@ if len(sys.argv) > 3:
     combos = [tuple((c + ":").split(":")[:2]) for c in sys.argv[3].split("/")]
 for builder, knobs in combos:
     os.environ["RT_BVH_BUILD"] = builder
-    os.environ["RT_SAH_KNOBS"] = knobs
+    r.tune(sah_knobs=(1 if "classic" in knobs else 0) | (2 if "sweep" in knobs else 0)
+           | (4 if "order1" in knobs else 8 if "order2" in knobs else 0))
     r.set_scene(sc)
     torch.cuda.synchronize()
     rci8 = rtvk.canonical_render_call_info(8, W, H)

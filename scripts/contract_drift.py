@@ -9,9 +9,12 @@ The oracle renders the same pixels three ways (oracle/rt_oracle.cpp LIT_*):
 and reports, for contract vs each literal form: the fraction of bit-identical accumulator
 texels, of identical rgba8 pixels, and the PSNR of the rgba8 image.
 
-Workloads: (1) blocks of the BASELINE config 3 frame (1920x1080, 10 000 spp, counter-based
-stream, the bench's pixels), (2) a 320x180 frame at 64 spp in both streams.
-Usage: python scripts/contract_drift.py [--blocks 8 --rows 8 --width 24] [--threads N]
+Workloads: (1) blocks of the BASELINE config 3 frame (1920x1080, 10 000 spp, the bench's pixels)
+in both streams: the counter-based stream and the reference's per-pixel LCG stream at the
+identical seed (the north star's "PSNR >= 50 dB vs reference at identical seed"), (2) a 320x180
+frame at 64 spp in both streams. `noise_floor` compares the two streams' contract renders: two
+independent Monte-Carlo estimates of the same pixels, the PSNR a fully decorrelated stream reaches.
+Usage: python scripts/contract_drift.py [--blocks 8 --rows 8 --width 24] [--threads N] [--out F]
 """
 from __future__ import annotations
 
@@ -59,6 +62,7 @@ def main() -> int:
     ap.add_argument("--width", type=int, default=24)
     ap.add_argument("--spp", type=int, default=10000)
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 1)
+    ap.add_argument("--out", default=None, help="also write the JSON here")
     args = ap.parse_args()
     oracle.build()
     sc = oracle.generate_scene(0.0)
@@ -67,21 +71,28 @@ def main() -> int:
     W, H = 1920, 1080
     ys = np.linspace(0, H - args.rows, args.blocks).round().astype(int)
     xs = np.linspace(0, W - args.width, args.blocks).round().astype(int)[::-1]
-    parts = {k: [] for k in ("contract", "rint", "all")}
-    secs = 0.0
-    for y, x in zip(ys, xs):
-        rows = np.arange(y, y + args.rows, dtype=np.uint32)
-        r = render3(sc, oracle.render_call_info(args.spp, W, H, (int(x), 0)), args.width, args.rows, rows,
-                    2, args.threads)
-        for k in parts:
-            parts[k].append(r[k][:2])
-        secs += sum(v[3] for v in r.values())
-    cat = {k: (np.concatenate([p[0] for p in v]), np.concatenate([p[1] for p in v])) for k, v in parts.items()}
-    res["config3_blocks"] = {
-        "pixels": f"{args.blocks} blocks of {args.rows} rows x {args.width} px of 1920x1080 at {args.spp} spp, hash stream",
-        "rint_literal": compare(*cat["rint"], *cat["contract"]),
-        "all_literal": compare(*cat["all"], *cat["contract"]),
-        "cpu_s": round(secs, 1)}
+    cat_by_stream = {}
+    for rng, sname in ((2, "hash"), (0, "stream")):
+        parts = {k: [] for k in ("contract", "rint", "all")}
+        secs = 0.0
+        for y, x in zip(ys, xs):
+            rows = np.arange(y, y + args.rows, dtype=np.uint32)
+            r = render3(sc, oracle.render_call_info(args.spp, W, H, (int(x), 0)), args.width, args.rows, rows,
+                        rng, args.threads)
+            for k in parts:
+                parts[k].append(r[k][:2])
+            secs += sum(v[3] for v in r.values())
+        cat = {k: (np.concatenate([p[0] for p in v]), np.concatenate([p[1] for p in v])) for k, v in parts.items()}
+        cat_by_stream[sname] = cat
+        res["config3_blocks" if sname == "hash" else "config3_blocks_reference_stream"] = {
+            "pixels": f"{args.blocks} blocks of {args.rows} rows x {args.width} px of 1920x1080 at {args.spp} spp, "
+                      + ("hash stream" if sname == "hash" else "reference per-pixel LCG stream (identical seed)"),
+            "rint_literal": compare(*cat["rint"], *cat["contract"]),
+            "all_literal": compare(*cat["all"], *cat["contract"]),
+            "cpu_s": round(secs, 1)}
+    res["config3_blocks_noise_floor"] = {
+        "what": "contract render, reference stream vs hash stream: two independent estimates of the same pixels",
+        **compare(*cat_by_stream["stream"]["contract"], *cat_by_stream["hash"]["contract"])}
     # (2) 320x180 at 64 spp, both streams
     for rng, name in ((0, "stream"), (2, "hash")):
         r = render3(sc, oracle.render_call_info(64, 320, 180), 320, 180, None, rng, args.threads)
@@ -90,6 +101,8 @@ def main() -> int:
             "all_literal": compare(*r["all"][:2], *r["contract"][:2]),
             "segments": {k: v[2][0] for k, v in r.items()}}
     print(json.dumps(res, indent=1))
+    if args.out:
+        Path(args.out).write_text(json.dumps(res, indent=1) + "\n")
     return 0
 
 

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""A/B of a per-launch environment knob in one process, interleaved rounds, full 1080p frames:
-every setting must render the same image. Usage:
-  python scripts/env_ab.py VAR spp[,spp...] name=value [name=value ...]   (value '-' = unset)"""
+"""A/B of a per-launch tuning knob (rt_debug_tune; names as RT_SAMPLE_CHUNKS or sample_chunks) in one
+process, interleaved rounds, full 1080p frames: every setting must render the same image. Usage:
+  python scripts/env_ab.py KNOB spp[,spp...] name=value [name=value ...]   (value '-' = default)"""
 import os
 import sys
 
@@ -14,6 +14,7 @@ import rtvk  # noqa: E402
 W, H = int(os.environ.get("AB_W", 1920)), int(os.environ.get("AB_H", 1080))   # AB_W / AB_H / AB_K: frame, scene
 RNG = rtvk.HASH if os.environ.get("AB_RNG", "stream") == "hash" else rtvk.STREAM   # AB_RNG=hash
 var = sys.argv[1]
+key = var[3:].lower() if var.startswith("RT_") else var
 spps = [int(x) for x in sys.argv[2].split(",")]
 settings = dict(a.split("=", 1) for a in sys.argv[3:])
 r = rtvk.Renderer(0)
@@ -26,10 +27,7 @@ for spp in spps:
     ref = None
     for rnd in range(6):
         for k, v in settings.items():
-            if v == "-":
-                os.environ.pop(var, None)
-            else:
-                os.environ[var] = v
+            r.tune(**{key: None if v == "-" else float(v)})
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             r.render_device(rci, acc, out, options=rtvk.make_options(rng_mode=RNG))

@@ -28,11 +28,8 @@ times = {k: [] for k in settings}
 ref = None
 for rnd in range(rounds + 1):
     for name, kvs in settings.items():
-        for k in knobs:
-            os.environ.pop(k, None)
-        for k, v in kvs:
-            if v != "-":
-                os.environ[k] = v
+        r.tune(**{(k[3:].lower() if k.startswith("RT_") else k): None for k in knobs})   # rt_debug_tune
+        r.tune(**{(k[3:].lower() if k.startswith("RT_") else k): (None if v == "-" else float(v)) for k, v in kvs})
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         r.render_device(rci, acc, out, options=rtvk.make_options(rng_mode=RNG))

@@ -29,10 +29,7 @@ for spp in spps:
     ref = None
     for rnd in range(5):
         for k, v in settings.items():
-            if v is None:
-                os.environ.pop("RT_REFILL_RESERVE", None)
-            else:
-                os.environ["RT_REFILL_RESERVE"] = v
+            r.tune(refill_reserve=None if v is None else float(v))
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             r.render_device(rci, acc, out, options=rtvk.make_options())

@@ -18,10 +18,9 @@ rci = rtvk.canonical_render_call_info(spp, W, H)
 opt = rtvk.make_options(accel=rtvk.abi.RT_ACCEL_AUTO, rng_mode=rtvk.HASH)
 rs = {}
 for sc in scales:   # one context per scale: the grid is built at set_scene
-    os.environ["RT_GRID_SCALE"] = sc
     rs[sc] = rtvk.Renderer(0)
+    rs[sc].tune(grid_scale=float(sc))
     rs[sc].set_scene(scene)
-os.environ.pop("RT_GRID_SCALE")
 acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
 out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
 times, ref = {s: [] for s in scales}, None

@@ -24,10 +24,7 @@ rci = rtvk.canonical_render_call_info(spp, W, H)
 imgs = {}
 for rep in range(3):
     for mode in ("rowmajor", "sum", "lpt"):
-        if mode == "lpt":
-            os.environ.pop("RT_SCHEDULE", None)
-        else:
-            os.environ["RT_SCHEDULE"] = mode
+        r.tune(schedule={"lpt": 0, "rowmajor": 1, "sum": 2}[mode])
         ts, tails, drys = [], [], []
         for i in range(8):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -13,7 +13,7 @@ ROOT = Path(__file__).resolve().parent.parent
 @pytest.mark.gpu
 def test_bench_json_line_contract():
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--width", "96", "--height", "64", "--spp", "2",
-                        "--steps", "3", "--warmup", "1"],
+                        "--steps", "3", "--warmup", "1", "--no-rebuild-check"],
                        capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -36,8 +36,14 @@ def test_bench_json_line_contract():
     assert d["config"]["rng"] == "hash" and "reference_stream" in d and "brute_force" in d
     assert d["roofline"]["lib_sha256"] and "frac_basis" in d["roofline"]
     assert cb["parity"]["accum_bit_exact"] and cb["parity"]["rgba8_equal"] and cb["parity"]["psnr_db"] == "inf"
+    # both streams' pixels against the oracle, and the reference stream against the literal GLSL
+    ref = cb["parity"]["reference_stream"]
+    assert ref["accum_bit_exact"] and ref["rgba8_equal"], ref
+    assert set(ref["vs_literal_glsl"]) >= {"rint", "all"}
+    assert len(cb["config1_runs"]) == 3 and cb["spp16_msamples_per_s"] > 0
+    assert d["build"]["env"] == {} and d["build"]["rebuild"] == "skipped"
     # honest labels: the accel named in config is the walk that ran (the roofline's kernel)
-    assert d["config"]["path"] == "single" and d["config"]["accel"] in ("grid-lds", "lbvh-octant-lds")
+    assert d["config"]["path"] == "single" and d["config"]["accel"] in ("grid-lds-rec", "grid-lds", "lbvh-octant-lds")
     assert ("grid" in d["roofline"]["kernel"]) == d["config"]["accel"].startswith("grid")
     # the kernel is timed inside the timed region: it cannot outlast the step
     assert 0 < roof["kernel_ms"] <= d["ms_per_step"]
@@ -68,6 +74,17 @@ def test_bench_refuses_more_gpus_than_visible():
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(max(1, n) + 1), "--steps", "1"],
                        capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 2 and "visible" in r.stderr
+
+
+def test_bench_refuses_tuning_environment():
+    """A tuning or library-selecting RT_* variable in the environment would make the line describe
+    something other than the shipped build: bench.py refuses before rendering."""
+    import os
+    for var, val in (("RT_SAMPLE_CHUNKS", "7"), ("RT_LIB", "/tmp/x.so"), ("RT_BVH_BUILD", "gpu")):
+        e = dict(os.environ, **{var: val})
+        r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "1"],
+                           capture_output=True, text=True, timeout=300, cwd=ROOT, env=e)
+        assert r.returncode == 2 and var in r.stderr, (var, r.stderr[-500:])
 
 
 def test_bench_refuses_launcher_mismatch():

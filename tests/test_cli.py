@@ -102,6 +102,20 @@ def test_ray_trace_hash_stream_matches_oracle(tmp_path, oracle, how):
 
 
 @pytest.mark.gpu
+def test_cli_explicit_rng_overrides_environment(tmp_path, oracle):
+    """An explicit --rng stream wins over RT_RNG=hash in the caller's environment (the CLI passes
+    its choice to ray_trace() through RT_RNG, always when --rng is given)."""
+    import os
+    e = dict(os.environ, RT_RNG="hash")
+    r = run("--store", "--samples", "3", "--width", "48", "--height", "24", "--rng", "stream", cwd=tmp_path, env=e)
+    assert r.returncode == 0, r.stderr
+    assert "reference stream" in r.stdout
+    img = np.frombuffer((tmp_path / "render.ppm").read_bytes()[len(b"P6\n48 24\n255\n"):], np.uint8).reshape(24, 48, 3)
+    _, ref, _ = oracle.render(oracle.generate_scene(), oracle.render_call_info(3, 48, 24), 48, 24)
+    np.testing.assert_array_equal(img, ref[..., :3])
+
+
+@pytest.mark.gpu
 def test_ray_trace_rejects_unknown_rng(tmp_path):
     import os
     e = dict(os.environ, RT_RNG="philox")

@@ -122,12 +122,13 @@ def test_device_tree_edge_cases(renderer, oracle, case):
     assert_trees_equal(host, dev)
 
 
-@pytest.mark.parametrize("K,device_built,form", [(11, False, "grid-lds"), (15, False, "grid-lds"),
+@pytest.mark.parametrize("K,device_built,form", [(11, False, "grid-lds-rec"), (15, False, "grid-lds"),
                                                  (16, True, "lbvh-octant-lds"), (40, True, "grid-global"),
                                                  (158, True, "grid-global")])
 def test_auto_builder_policy(renderer, oracle, K, device_built, form):
     """Default: host SAH tree up to 1024 spheres (K = 15 -> 904), device LBVH above (K = 16 ->
-    1028); the walk is the uniform grid over the small spheres staged in LDS (host-built scenes),
+    1028); the walk is the uniform grid over the small spheres staged in LDS (host-built scenes;
+    with the shading records too while two blocks per CU still fit, K = 11),
     else the tree's 8 octant copies in LDS while they fit (K = 16), else the grid from L2
     (device-built scenes, K = 40 -> 6404)."""
     with tree_builder(None):

@@ -4,7 +4,7 @@ in-region kernel timing and build provenance, and what the multi-device path rep
 import numpy as np
 import pytest
 
-from test_gpu_parity import GRID, HASH, LBVH, LBVH_OCT, STREAM, assert_same, gpu_render  # noqa: F401
+from test_gpu_parity import GRID, HASH, LBVH, LBVH_OCT, STREAM, assert_same, gpu_render, tuned  # noqa: F401
 from test_gpu_parity import renderer, rtvk, torch  # noqa: F401  (module fixtures)
 
 pytestmark = pytest.mark.gpu
@@ -19,7 +19,7 @@ def test_config3_full_frame_grid_equals_lbvh(rtvk, renderer, torch, oracle, rng_
     sc = oracle.generate_scene()
     rci = oracle.render_call_info(spp, W, H)
     a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH, rng_mode=rng_mode)
-    assert renderer.launch_info()["form"] == "grid-lds"
+    assert renderer.launch_info()["form"] == "grid-lds-rec"
     a2, o2, st2 = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH_OCT, rng_mode=rng_mode)
     assert renderer.launch_info()["form"] == "lbvh-octant-lds"
     assert_same(a, o, a2, o2)
@@ -46,6 +46,68 @@ def test_kernel_vs_literal_glsl(rtvk, renderer, torch, oracle, rng_mode, min_psn
         psnr = 10 * np.log10(255 ** 2 / mse)
         print(f"rng {rng_mode} lit {lit}: {same:.4f} of accumulator texels bit-identical, rgba8 PSNR {psnr:.2f} dB")
         assert psnr >= min_psnr and same > 0.7
+
+
+def _blocks(W, H, n_blocks, rows, width):
+    """(y, x) corners of n_blocks blocks spread over the frame (bench.py's cpu_baseline layout)."""
+    ys = np.linspace(0, H - rows, n_blocks).round().astype(int)
+    xs = np.linspace(0, W - width, n_blocks).round().astype(int)[::-1]
+    return list(zip(ys, xs))
+
+
+def test_reference_stream_vs_literal_glsl_config3(rtvk, renderer, torch, oracle):
+    """The north star's bar, "PSNR >= 50 dB vs reference at identical seed", on the headline frame:
+    BASELINE config 3 (1920x1080, 10 000 spp) in the reference's own per-pixel LCG stream at the
+    reference's seed. The kernel equals the contract oracle bit for bit on 8 blocks of 16 rows x 12
+    px; against the oracle's literal readings of the GLSL (LIT_RINT: shader.rint:46-55 as written;
+    LIT_ALL: every dot / normalize too) the same pixels stay above 50 dB (measured 58.5 / 57.0 dB
+    on the drift script's blocks, profiles/r04_contract_drift.json; two fully independent
+    10 000-spp estimates of these pixels differ by ~53 dB)."""
+    W, H, spp = 1920, 1080, 10000
+    sc = oracle.generate_scene()
+    a, o, _ = gpu_render(rtvk, renderer, torch, sc, oracle.render_call_info(spp, W, H), W, H, accel=LBVH,
+                         rng_mode=STREAM)
+    got, ref = {}, {k: [] for k in ("contract", "rint", "all")}
+    for y, x in _blocks(W, H, 8, 16, 12):
+        rows = np.arange(y, y + 16, dtype=np.uint32)
+        rci = oracle.render_call_info(spp, W, H, (int(x), 0))
+        got.setdefault("acc", []).append(a[y:y + 16, x:x + 12])
+        got.setdefault("px", []).append(o[y:y + 16, x:x + 12])
+        for name, lit in (("contract", oracle.LIT_CONTRACT), ("rint", oracle.LIT_RINT), ("all", oracle.LIT_ALL)):
+            ra, ro, _ = oracle.render(sc, rci, 12, 16, rows=rows, opts=oracle.options(rng_mode=STREAM, lit=lit),
+                                      threads=16)
+            ref[name].append((ra, ro))
+    ga, go = np.concatenate(got["acc"]), np.concatenate(got["px"])
+    assert_same(ga, go, np.concatenate([r[0] for r in ref["contract"]]), np.concatenate([r[1] for r in ref["contract"]]))
+    for name in ("rint", "all"):
+        lo = np.concatenate([r[1] for r in ref[name]])
+        mse = np.mean((go[..., :3].astype(np.float64) - lo[..., :3]) ** 2)
+        psnr = 10 * np.log10(255 ** 2 / mse)
+        print(f"reference stream, config 3 blocks, literal {name}: rgba8 PSNR {psnr:.2f} dB")
+        assert psnr >= 50.0
+
+
+def test_grid_rec_form_switch(rtvk, renderer, torch, oracle):
+    """The canonical scene's default walk stages the winner's gate and shading records in LDS
+    (form grid-lds-rec, ACCEL_GRID_REC); tuning grid_rec = 0 runs the plain LDS grid kernel
+    (grid-lds) instead. launch_info names each, and both render the oracle's bits in both streams."""
+    W, H, spp = 96, 64, 3
+    sc = oracle.generate_scene()
+    rci = oracle.render_call_info(spp, W, H)
+    for rng in (STREAM, HASH):
+        ra, ro, rs = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=rng))
+        a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH, rng_mode=rng)
+        assert renderer.launch_info()["form"] == "grid-lds-rec"
+        assert_same(a, o, ra, ro)
+        with tuned(renderer, grid_rec=0):
+            a2, o2, st2 = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH, rng_mode=rng)
+            assert renderer.launch_info()["form"] == "grid-lds"
+        assert_same(a2, o2, ra, ro)
+        assert (st.segments, st.samples) == (st2.segments, st2.samples) == rs[:2]
+    with pytest.raises(rtvk.RtError, match="unknown tuning key"):
+        renderer.tune(no_such_knob=1)
+    with pytest.raises(rtvk.RtError):
+        renderer.tune(sample_chunks=-5)
 
 
 def _bright_scene(oracle):

@@ -30,22 +30,14 @@ STREAM, COUNTER, HASH = 0, 1, 2
 
 
 @contextlib.contextmanager
-def env(**kv):
-    """Temporarily set (value str) or clear (None) environment variables read by the library."""
-    prev = {k: os.environ.get(k) for k in kv}
-    for k, v in kv.items():
-        if v is None:
-            os.environ.pop(k, None)
-        else:
-            os.environ[k] = str(v)
+def tuned(renderer, **kv):
+    """Launch-plan parameters of the renderer's context for the block (rt_debug_tune; no setting
+    may change an image), restored to the defaults afterwards."""
+    renderer.tune(**kv)
     try:
         yield
     finally:
-        for k, v in prev.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+        renderer.tune(**{k: None for k in kv})
 
 
 @contextlib.contextmanager
@@ -274,7 +266,7 @@ def test_empty_and_single_sphere(rtvk, renderer, torch, oracle):
 def test_grid_near_cull_slack_mixed_radii(rtvk, renderer, torch, oracle, builder):
     """The grid walks' small cull slack depends on the smallest and largest small
     radius: a scene of 300 spheres with radii 0.06-0.45 (the grid's 8:1 limit), cameras inside and
-    far outside it. The default slack, the full slack (RT_GRID_FULL_SLACK=1) and the oracle agree
+    far outside it. The default slack, the full slack (tuning grid_full_slack = 1) and the oracle agree
     bit for bit, both streams, host (LDS) and device (L2) grids."""
     rng = np.random.default_rng(7)
     base = oracle.generate_scene()[4:5]
@@ -295,7 +287,7 @@ def test_grid_near_cull_slack_mixed_radii(rtvk, renderer, torch, oracle, builder
             ra, ro, _ = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=rng_mode))
             for full in (None, "1"):
                 for accel in (LBVH, GRID_COOP):
-                    with env(RT_GRID_FULL_SLACK=full):
+                    with tuned(renderer, grid_full_slack=full):
                         a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=accel, rng_mode=rng_mode,
                                              builder=builder)
                     assert_same(a, o, ra, ro)
@@ -377,13 +369,13 @@ def test_accumulate_and_counter_rng(rtvk, renderer, torch, oracle, rng_mode, acc
 @pytest.mark.parametrize("chunks", ["1", "2", "3", "7", "13", "4096"])
 def test_hash_chunk_invariance(rtvk, renderer, torch, oracle, chunks):
     """RT_RNG_SAMPLE_HASH: splitting every pixel's 13 samples into 1..13 chunks run by different
-    lanes in any order (RT_SAMPLE_CHUNKS; 4096 is clamped to spp) gives the oracle's bits, with
+    lanes in any order (tuning sample_chunks; 4096 is clamped to spp) gives the oracle's bits, with
     the same segment and sample counts, on a ragged band, twice (the second with the LPT order)."""
     W, H, spp = 77, 45, 13
     sc = oracle.generate_scene()
     rci = oracle.render_call_info(spp, W, H)
     ra, ro, rs = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=HASH))
-    with env(RT_SAMPLE_CHUNKS=chunks):
+    with tuned(renderer, sample_chunks=chunks):
         for accel in (LBVH, LBVH, BRUTE):
             a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, rng_mode=HASH, accel=accel)
             assert_same(a, o, ra, ro)
@@ -394,15 +386,15 @@ def test_hash_chunk_invariance(rtvk, renderer, torch, oracle, chunks):
 
 @pytest.mark.parametrize("head,tail_pm", [("1", "0"), ("2", "300"), ("5", "500"), ("1", "1"), ("3", "1000")])
 def test_hash_head_tail_chunks(rtvk, renderer, torch, oracle, head, tail_pm):
-    """RT_RNG_SAMPLE_HASH with the LPT order split into a head (the longest tiles, RT_HEAD_CHUNKS
-    chunks per pixel) and a tail (RT_TAIL_TILES_PM per mille of the tiles, `chunks` = 7 chunks):
+    """RT_RNG_SAMPLE_HASH with the LPT order split into a head (the longest tiles, head_chunks
+    chunks per pixel) and a tail (tail_tiles_pm per mille of the tiles, `chunks` = 7 chunks):
     the oracle's bits and counts for every split, from all-head (0 per mille) to all-tail (1000,
     no head), on a ragged band; the first launch has no LPT order (no head), the second has."""
     W, H, spp = 77, 45, 13
     sc = oracle.generate_scene()
     rci = oracle.render_call_info(spp, W, H)
     ra, ro, rs = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=HASH))
-    with env(RT_SAMPLE_CHUNKS="7", RT_HEAD_CHUNKS=head, RT_TAIL_TILES_PM=tail_pm):
+    with tuned(renderer, sample_chunks=7, head_chunks=head, tail_tiles_pm=tail_pm):
         for k in range(3):
             a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, rng_mode=HASH, accel=LBVH, count=k == 2)
             assert_same(a, o, ra, ro)
@@ -423,7 +415,7 @@ def test_hash_tail_steals(rtvk, renderer, torch, oracle):
     sc = oracle.generate_scene()
     rci = oracle.render_call_info(spp, W, H)
     ra, ro, rs = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=HASH), threads=16)
-    with env(RT_SAMPLE_CHUNKS=1):
+    with tuned(renderer, sample_chunks=1):
         for accel in (LBVH, BRUTE):
             for count in (False, True):
                 a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, rng_mode=HASH, accel=accel, count=count)
@@ -622,7 +614,7 @@ def test_resolve_rgba8_edge_values(rtvk, renderer, torch, oracle):
 
 @pytest.mark.parametrize("reserve", ["0", "100", str(1 << 40)])
 def test_chunked_refill_same_image(rtvk, renderer, torch, oracle, reserve):
-    """Pixel hand-out by whole tiles (RT_REFILL_RESERVE=0), tiles then single pixels (100), and
+    """Pixel hand-out by whole tiles (refill_reserve = 0), tiles then single pixels (100), and
     single pixels only (huge reserve) render the same image as the oracle, on a ragged frame
     (width and height not multiples of 8) so tiles with missing pixels go through the tile path."""
     W, H = 203, 117
@@ -630,7 +622,7 @@ def test_chunked_refill_same_image(rtvk, renderer, torch, oracle, reserve):
     rci = oracle.render_call_info(3, W, H)
     ra, ro, rs = oracle.render(sc, rci, W, H)
     rh, oh, rsh = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=HASH))
-    with env(RT_REFILL_RESERVE=reserve):
+    with tuned(renderer, refill_reserve=reserve):
         for _ in range(2):   # second launch runs with the LPT hand-out order
             a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH)
             assert_same(a, o, ra, ro)
@@ -691,17 +683,14 @@ def test_strips_rccl_world1(rtvk, renderer, torch, oracle, rng_mode):
 
 @pytest.mark.parametrize("isolate", ["0", "3", "1000000"])
 def test_isolated_tiles_same_image(rtvk, renderer, torch, oracle, isolate):
-    """Waves starting on the longest-chain tiles that take no further pixels (RT_ISOLATE_TILES,
+    """Waves starting on the longest-chain tiles that take no further pixels (isolate_tiles,
     including every wave isolated) render the same image as the oracle; the second launch has
     the LPT order the isolation needs."""
     W, H = 136, 72
     sc = oracle.generate_scene()
     rci = oracle.render_call_info(2, W, H)
     ra, ro, _ = oracle.render(sc, rci, W, H)
-    prev = {k: os.environ.get(k) for k in ("RT_ISOLATE_TILES", "RT_REFILL_RESERVE")}
-    os.environ["RT_ISOLATE_TILES"] = isolate
-    os.environ["RT_REFILL_RESERVE"] = "0"
-    try:
+    with tuned(renderer, isolate_tiles=isolate, refill_reserve=0):
         renderer.set_scene(sc)
         rci_c = rtvk.RenderCallInfo.from_buffer_copy(rci.tobytes())
         for _ in range(2):
@@ -710,12 +699,6 @@ def test_isolated_tiles_same_image(rtvk, renderer, torch, oracle, isolate):
             renderer.render_device(rci_c, a, o, options=rtvk.make_options())
             torch.cuda.synchronize()
             assert_same(a.cpu().numpy(), o.cpu().numpy(), ra, ro)
-    finally:
-        for k, v in prev.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
 
 
 
