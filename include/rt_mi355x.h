@@ -284,6 +284,9 @@ int rt_debug_walk_hist(rt_context* ctx, uint64_t* out128);
    max over the wave's tracing lanes [0] and over its bounce (depth > 0) lanes [1], summed over
    passes; the primary (depth 0) lanes' summed work [2] and their count [3]. */
 int rt_debug_walk_split(rt_context* ctx, uint64_t* out4);
+/* Diagnostic: of ctx's last instrumented launch of a grid walk, {cells visited, visited cells that
+ * hold no reference}. */
+int rt_debug_grid_cells(rt_context* ctx, uint64_t* out2);
 /* Diagnostic: segment-loop iterations of the last instrumented launch by the number of lanes
  * (0..64) of the wave tracing in that iteration (the persistent kernel's lane occupancy), then
  * three s_memrealtime stamps (100 MHz): first wave start, pixel queue dry, last wave exit. */

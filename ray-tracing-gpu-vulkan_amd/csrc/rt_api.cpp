@@ -1382,6 +1382,19 @@ int rt_debug_walk_split(rt_context* ctx, uint64_t* out4) {
     return RT_OK;
 }
 
+// Diagnostic export: of the last COUNT launch of a grid walk, {cells visited, visited cells without
+// references} (the decision metric of an occupancy bitmap).
+int rt_debug_grid_cells(rt_context* ctx, uint64_t* out2) {
+    if (!ctx || !out2) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    DeviceGuard g(ctx->device);
+    if (ctx->ev_valid) RT_HIP(hipEventSynchronize(ctx->ev_last));
+    rt::Counters c;
+    RT_HIP(hipMemcpy(&c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
+    out2[0] = c.box_tests;
+    out2[1] = c.cells_empty;
+    return RT_OK;
+}
+
 // Diagnostic export: walk-length histogram of the last COUNT launch (2 x 64 bins: miss, hit).
 int rt_debug_walk_hist(rt_context* ctx, uint64_t* out128) {
     if (!ctx || !out128) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");

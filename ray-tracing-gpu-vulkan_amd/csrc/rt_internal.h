@@ -168,6 +168,7 @@ struct Counters {
     unsigned long long util[2 * 16];   // diagnostic builds only (-DRT_UTIL): per code point k, wave
                                        // passes [2k] and active lanes summed over them [2k + 1]
     unsigned long long steals;     // counter-based stream: tail steals (rt_kernels.hip steal_tail)
+    unsigned long long cells_empty;     // COUNT builds, grid walks: visited cells without references
     unsigned long long walk_split[4];   // COUNT builds: walk work (cells + references) per segment
                                         // pass, max over the wave's tracing lanes [0], over its bounce
                                         // lanes only [1]; primary lanes' summed work [2], count [3]

@@ -1093,7 +1093,7 @@ __device__ __forceinline__ void walk_global_range(const rt::TraceParams& P, cons
 template <bool COUNT, bool PAIRS>
 __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32_t* __restrict__ cstart,
                                           const float4* __restrict__ rec, const uint32_t* __restrict__ ids,
-                                          Ray& r, uint32_t& n_cell, uint32_t& n_sph) {
+                                          Ray& r, uint32_t& n_cell, uint32_t& n_sph, uint32_t& n_empty) {
     const rt::GridInfo& G = P.grid;
     const float x0 = (G.lo_m[0] - r.o.x) * r.inv.x, x1 = (G.hi_m[0] - r.o.x) * r.inv.x;
     const float y0 = (G.lo_m[1] - r.o.y) * r.inv.y, y1 = (G.hi_m[1] - r.o.y) * r.inv.y;
@@ -1125,7 +1125,10 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
     const int dxc = sx, dyc = sy * int(G.n[0]), dzc = sz * int(G.n[0] * G.n[1]);
     for (;;) {
         const uint32_t b = cstart[cell], e = cstart[cell + 1];
-        if (COUNT) n_cell++;
+        if (COUNT) {
+            n_cell++;
+            n_empty += b == e ? 1u : 0u;
+        }
         uint32_t j = b;
         if (PAIRS) {   // references from L2: two at a time (two record loads in flight; config 5 -3.5 %)
           // the ids are loaded with the records (one L2 round trip instead of a second, dependent
@@ -1405,11 +1408,11 @@ __device__ __forceinline__ void regate_brute(const rt::TraceParams& P, const flo
 template <bool COUNT, int LAYOUT>
 __device__ __forceinline__ void walk(const rt::TraceParams& P, const float4* __restrict__ nodes4,
                                      const float4* __restrict__ leaf4, const uint32_t* __restrict__ leaf_ids,
-                                     Ray& r, uint32_t& n_box, uint32_t& n_sph) {
+                                     Ray& r, uint32_t& n_box, uint32_t& n_sph, uint32_t& n_empty) {
     if (LAYOUT == LAYOUT_GRID || LAYOUT == LAYOUT_GRID_L2) {   // nodes4 = cell offsets, leaf4 / leaf_ids = references
         if (r.walk)
             grid_walk<COUNT, LAYOUT == LAYOUT_GRID_L2>(P, reinterpret_cast<const uint32_t*>(nodes4), leaf4, leaf_ids, r,
-                                                       n_box, n_sph);
+                                                       n_box, n_sph, n_empty);
         return;
     }
     const RayBox q = ray_box(r.o, r.inv);
@@ -1515,7 +1518,7 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
     }
     // traced segments and started samples of this wave (wave-uniform: ballot counts, no per-lane
     // registers); per-lane test counters in COUNT builds only
-    uint32_t seg_w = 0, smp_w = 0, n_box = 0, n_sph = 0;
+    uint32_t seg_w = 0, smp_w = 0, n_box = 0, n_sph = 0, n_empty = 0;
     unsigned long long wave_iters = 0;
     bool saw_dry = false;
     WaveBlock blk;
@@ -1556,7 +1559,7 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
             grid_walk_coop<COUNT>(P, reinterpret_cast<const uint32_t*>(nodes4), leaf4, leaf_ids, r, st == ST_TRACING,
                                   n_box, n_sph);
         } else {
-            if (st == ST_TRACING) walk<COUNT, LAYOUT>(P, nodes4, leaf4, leaf_ids, r, n_box, n_sph);
+            if (st == ST_TRACING) walk<COUNT, LAYOUT>(P, nodes4, leaf4, leaf_ids, r, n_box, n_sph, n_empty);
         }
         // the AABB gate of the winner only (winner_gated); the rare lanes whose winner fails it
         // get the contract's answer by a wave-cooperative gated brute force. The winner's shading
@@ -1606,6 +1609,7 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
     if (COUNT) {
         atomicAdd(&P.counters->box_tests, (unsigned long long)n_box);
         atomicAdd(&P.counters->sphere_tests, (unsigned long long)n_sph);
+        if (n_empty) atomicAdd(&P.counters->cells_empty, (unsigned long long)n_empty);
         if (lane == 0) atomicAdd(&P.counters->wave_iters, wave_iters);
     }
     UTIL_FLUSH;

@@ -219,6 +219,13 @@ class Renderer:
         check(self._lib.rt_debug_steals(self._ctx, ctypes.byref(v)))
         return int(v.value)
 
+    def grid_cells(self) -> dict:
+        """Of the last instrumented (count_tests) grid-walk launch: cells visited and visited cells
+        without references (rt_debug_grid_cells)."""
+        v = (ctypes.c_uint64 * 2)()
+        check(self._lib.rt_debug_grid_cells(self._ctx, v))
+        return {"cells": int(v[0]), "empty": int(v[1])}
+
     def launch_info(self) -> dict:
         """Of the last launch: sample chunks per pixel (of the LPT order's tail ranks; head_chunks:
         of its head ranks, None when there is no head), the kernel form it ran, its dynamic LDS

@@ -131,6 +131,7 @@ EXPORTS = {
     "rt_debug_tune": (_I, [_P, ctypes.c_char_p, ctypes.c_double]),
     "rt_debug_walk_hist": (_I, [_P, _P]),
     "rt_debug_walk_split": (_I, [_P, _P]),
+    "rt_debug_grid_cells": (_I, [_P, _P]),
     "rt_debug_lane_hist": (_I, [_P, _P]),
     "rt_debug_steals": (_I, [_P, _P]),
     "rt_debug_tile_cost": (_I, [_P, _P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),

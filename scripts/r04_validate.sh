@@ -18,4 +18,6 @@ timeout -k 10 600 python bench.py --steps $STEPS --warmup 2 > gpurun_out/${TAG}_
 rc=$?; tail -c 600 gpurun_out/${TAG}_bench.json; fatal $rc bench
 timeout -k 10 300 python bench.py --config 5 --path multi --gpus 1 --steps 3 --warmup 2 --no-cpu-baseline --no-rebuild-check > gpurun_out/${TAG}_bench_c5_multi.json 2> gpurun_out/${TAG}_bench_c5_multi.err
 rc=$?; tail -c 300 gpurun_out/${TAG}_bench_c5_multi.json; fatal $rc bench_c5_multi
+timeout -k 10 120 python scripts/grid_cells.py > gpurun_out/${TAG}_grid_cells.json 2>&1
+rc=$?; cat gpurun_out/${TAG}_grid_cells.json; fatal $rc grid_cells
 echo done
