@@ -160,7 +160,7 @@ def cpu_baseline(width: int, height: int, spp: int, grid: int, rng_mode: int, gp
            "config1_frame_s": round(t1, 3), "config1_runs": [round(v, 3) for v in c1],
            "config1_msamples_per_s": round(rate / 1e6, 4), "spp16_frame_s": round(t16, 3),
            "spp16_msamples_per_s": round(rate16 / 1e6, 4),
-           "spp_independent": bool(abs(rate16 / rate - 1.0) < 0.25)}
+           "spp16_over_spp1": round(rate16 / rate, 3)}   # 1 spp carries the per-frame cost (threads, seeds) alone
     if gpu_accum is not None:
         ga, go = gpu_blocks(gpu_accum), gpu_blocks(gpu_rgba8)
         res["parity"] = {"pixels": int(n_blocks * nr * bw), "stream": stream_name,

@@ -112,7 +112,8 @@ typedef struct rt_options {
                              when they fit, else one copy in LDS, else an LDS treelet over L2
                              subtrees), 6 one LDS node copy, 8 octant copies, 10 every node from
                              L2, 12 the uniform grid, 14 the uniform grid in LDS with the
-                             wave-cooperative walk */
+                             wave-cooperative walk, 16 the uniform grid in LDS
+                             with the wave-wide candidate queue */
 } rt_options;
 
 /* Statistics of the last rt_render_device() on a context (valid after its stream completes). */
@@ -260,7 +261,8 @@ int rt_debug_kernel_times(rt_context* ctx, float* out_ms, uint32_t capacity, uin
 const char* rt_build_info(void);
 /* Diagnostic (tests, A/B timing): sets one launch-plan parameter of ctx (value -1 restores the
  * default). None of them changes an image; the defaults are the measured best. Keys: "grid" (0: no
- * uniform grid), "grid_scale", "grid_coop" (1: wave-cooperative grid walk), "grid_rec" (0: no
+ * uniform grid), "grid_scale", "grid_coop" (1: wave-cooperative grid walk), "grid_cq" (1: wave-wide
+ * candidate queue), "grid_rec" (0: no
  * shading records in LDS), "grid_full_slack", "units_per_lane", "unit_min_samples",
  * "sample_chunks", "head_chunks", "tail_tiles_pm", "schedule" (0 LPT, 1 row-major, 2 LPT by tile
  * sum), "refill_reserve", "isolate_tiles", "sah_knobs". Unknown keys: RT_ERR_INVALID_ARGUMENT.

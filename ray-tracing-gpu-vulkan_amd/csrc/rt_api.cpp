@@ -50,6 +50,7 @@ struct Tuning {
     double grid = kUnset;               // 0: no uniform grid (LBVH walks only)
     double grid_scale = kUnset;         // cell size scale (rt_grid.h kGridCellScale)
     double grid_coop = kUnset;          // 1: the wave-cooperative grid walk
+    double grid_cq = kUnset;            // 1: the wave-wide candidate queue in the LDS grid walk (§4.9)
     double grid_rec = kUnset;           // 0: no shading records in the LDS grid kernel's LDS
     double grid_full_slack = kUnset;    // 1: the full cull slack in grid walks
     double units_per_lane = kUnset;     // sample-chunk targets (counter-based stream)
@@ -905,7 +906,7 @@ uint32_t choose_accel(const rt_context* ctx, bool brute, uint32_t form, float ca
     if (brute) {
         accel = rt::ACCEL_BRUTE;
     } else if (ctx->has_grid && cam_r <= ctx->grid_pad_radius &&
-               (form == 12u || form == 14u || (form == 0u && (ctx->grid_bytes || !ctx->oct_bytes)))) {
+               (form == 12u || form == 14u || form == 16u || (form == 0u && (ctx->grid_bytes || !ctx->oct_bytes)))) {
         // the grid: staged in LDS when it fits (config 3: 1 % faster than the
         // octant tree), else the octant tree when that fits LDS (a device-built scene of ~1000
         // spheres, whose grid would be read from L2), else the grid from L2
@@ -922,10 +923,15 @@ uint32_t choose_accel(const rt_context* ctx, bool brute, uint32_t form, float ca
         // material record, 48 B per sphere) when two blocks per CU still fit;
         // tuning grid_rec = 0: not (A/B)
         const size_t rec_bytes = size_t(d.n_spheres) * 48u;
+        // the wave-wide candidate queue: form 16, or tuning grid_cq = 1
+        const bool cq = accel == rt::ACCEL_GRID && (form == 16u || (form == 0u && Tuning::get(tu.grid_cq, 0) == 1));
+        const size_t cq_bytes = cq ? rt::kCqLdsBytes : 0u;
         if (accel == rt::ACCEL_GRID && Tuning::get(tu.grid_rec, 1) != 0 &&
-            ctx->grid_bytes + rec_bytes + rt::kLaneSumLdsBytes <= kTwoBlockLdsBytes) {
-            accel = rt::ACCEL_GRID_REC;
+            ctx->grid_bytes + rec_bytes + rt::kLaneSumLdsBytes + cq_bytes <= kTwoBlockLdsBytes) {
+            accel = cq ? rt::ACCEL_GRID_REC_CQ : rt::ACCEL_GRID_REC;
             lds = ctx->grid_bytes + rec_bytes;
+        } else if (cq && ctx->grid_bytes + rt::kLaneSumLdsBytes + cq_bytes <= kMaxLdsBytes) {
+            accel = rt::ACCEL_GRID_CQ;
         }
     } else if (ctx->oct_bytes && (form == 0u || form == 8u)) {
         accel = rt::ACCEL_LBVH_OCT;
@@ -1037,7 +1043,8 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     P.treelet = d.treelet;
     P.treelet_count = d.treelet_count;
     const bool grid_walk = accel == rt::ACCEL_GRID || accel == rt::ACCEL_GRID_GLOBAL || accel == rt::ACCEL_GRID_COOP ||
-                           accel == rt::ACCEL_GRID_GLOBAL_COOP || accel == rt::ACCEL_GRID_REC;
+                           accel == rt::ACCEL_GRID_GLOBAL_COOP || accel == rt::ACCEL_GRID_REC ||
+                           accel == rt::ACCEL_GRID_CQ || accel == rt::ACCEL_GRID_REC_CQ;
     if (grid_walk) {   // (cell_start also marks a walk)
         P.grid = d.grid;
         P.cell_start = d.cell_start;
@@ -1440,6 +1447,7 @@ int rt_debug_tune(rt_context* ctx, const char* key, double value) {
     if (!ctx || !key) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     static const struct { const char* name; double Tuning::*field; } kKeys[] = {
         {"grid", &Tuning::grid}, {"grid_scale", &Tuning::grid_scale}, {"grid_coop", &Tuning::grid_coop},
+        {"grid_cq", &Tuning::grid_cq},
         {"grid_rec", &Tuning::grid_rec}, {"grid_full_slack", &Tuning::grid_full_slack},
         {"units_per_lane", &Tuning::units_per_lane}, {"unit_min_samples", &Tuning::unit_min_samples},
         {"sample_chunks", &Tuning::sample_chunks}, {"head_chunks", &Tuning::head_chunks},

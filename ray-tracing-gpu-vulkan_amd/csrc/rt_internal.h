@@ -94,6 +94,9 @@ constexpr unsigned kLaneSumLdsBytes = 3u * 8u * RT_TRACE_BLOCK;
 // Wave-cooperative grid walk (ACCEL_GRID_COOP): per thread a ray (2 float4), a key (u64) and a
 // pass marker (u32) in LDS.
 constexpr unsigned kCoopLdsBytes = (2u * 16u + 8u + 4u) * RT_TRACE_BLOCK;
+// Wave-wide candidate queue (ACCEL_GRID_CQ / ACCEL_GRID_REC_CQ): 128 queue entries (u32) and a
+// count per wave, a key (u64) per thread.
+constexpr unsigned kCqLdsBytes = (128u * 4u + 4u) * (RT_TRACE_BLOCK / 64u) + 8u * RT_TRACE_BLOCK;
 
 // Scene as resident in HBM (one allocation per context, rebuilt by rt_set_scene).
 struct DeviceScene {
@@ -129,7 +132,8 @@ struct DeviceScene {
 // L2) is the A/B reference of TOP (options.reserved[1] = 10).
 enum : uint32_t { ACCEL_BRUTE = 1, ACCEL_LBVH_GLOBAL = 2, ACCEL_LBVH_LDS = 3, ACCEL_LBVH_OCT = 4,
                   ACCEL_LBVH_TOP = 5, ACCEL_GRID = 6, ACCEL_GRID_GLOBAL = 7, ACCEL_GRID_COOP = 8,
-                  ACCEL_GRID_GLOBAL_COOP = 9, ACCEL_GRID_REC = 10, ACCEL_COUNT = 11 };
+                  ACCEL_GRID_GLOBAL_COOP = 9, ACCEL_GRID_REC = 10, ACCEL_GRID_CQ = 11, ACCEL_GRID_REC_CQ = 12,
+                  ACCEL_COUNT = 13 };
 
 // Random stream layout of a launch (template parameter of the trace kernels).
 //   STREAM: the reference's per-pixel LCG stream (random.glsl), or with rng_counter the TEA

@@ -931,7 +931,7 @@ constexpr uint32_t END = 0xffffffffu;
 // LDS1 = one node copy in LDS (AB layout), OCT = 8 octant-specialised copies in LDS, TOP = LDS
 // treelet over L2 subtrees.
 enum : int { LAYOUT_GLOBAL = 0, LAYOUT_LDS1 = 1, LAYOUT_OCT = 2, LAYOUT_TOP = 3, LAYOUT_GRID = 4, LAYOUT_GRID_L2 = 5,
-             LAYOUT_GRID_COOP = 6 };
+             LAYOUT_GRID_COOP = 6, LAYOUT_GRID_CQ = 7 };
 
 // Node slab test: one fma per plane, t = fma(plane, inv, -o * inv) (a sub-then-mul form is exact
 // in the gate's own arithmetic but costs twice the issue cycles: packed f32 ops take 4 cycles on
@@ -1185,6 +1185,157 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
     }
 }
 
+// Compiler-only ordering of LDS accesses made by different lanes of one wave: the LDS executes a
+// wave's instructions in issue order, so no wait or barrier is needed, only no reordering.
+__device__ __forceinline__ void lane_order() { asm volatile("" ::: "memory"); }
+
+// ---- wave-wide candidate queue (LAYOUT_GRID_CQ) --------------------------------
+// The LDS grid walk with the candidate tails (sqrt, roots, acceptance) taken out of the divergent
+// reference loop: a reference whose discriminant passes is pushed as (lane, reference) into a
+// per-wave LDS queue (ballot ranks), and at the end of each cell the wave's walking lanes resolve
+// the queue together, every lane taking entries, before any of them takes its DDA step. An entry's
+// ray comes from its owner lane by ds_bpermute (every owner is active at the flush: it pushed in
+// this cell), its candidate lowers the owner's (t bits, id) key by an LDS 64-bit atomic minimum
+// (t >= tmin > 0: the u64 minimum is the walks' (t, lowest id) rule). Per-lane queue overflow
+// (more than kCqCap entries in one cell) falls back to the lane's own tail. The cells visited, the
+// references tested and the closest hit are grid_walk's: bit-exact.
+constexpr uint32_t kCqCap = 128;   // queue entries per wave
+__shared__ uint32_t s_cq_q[kCqCap * (RT_TRACE_BLOCK / 64)];
+__shared__ unsigned long long s_cq_key[RT_TRACE_BLOCK];
+__shared__ uint32_t s_cq_n[RT_TRACE_BLOCK / 64];
+static_assert(sizeof(s_cq_q) + sizeof(s_cq_key) + sizeof(s_cq_n) == rt::kCqLdsBytes, "rt_internal.h");
+
+template <bool COUNT>
+__device__ __forceinline__ void grid_walk_cq(const rt::TraceParams& P, const uint32_t* __restrict__ cstart,
+                                             const float4* __restrict__ rec, const uint32_t* __restrict__ ids,
+                                             Ray& r, uint32_t& n_cell, uint32_t& n_sph, uint32_t& n_empty) {
+    const rt::GridInfo& G = P.grid;
+    const float x0 = (G.lo_m[0] - r.o.x) * r.inv.x, x1 = (G.hi_m[0] - r.o.x) * r.inv.x;
+    const float y0 = (G.lo_m[1] - r.o.y) * r.inv.y, y1 = (G.hi_m[1] - r.o.y) * r.inv.y;
+    const float z0 = (G.lo_m[2] - r.o.z) * r.inv.z, z1 = (G.hi_m[2] - r.o.z) * r.inv.z;
+    const float tn = fmaxf(fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1)), T_MIN);
+    const float tf = fminf(fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1)), r.limit);
+    if (!(tn <= tf)) return;
+    auto cell_of = [&](float p, int k) {
+        const int c = int(floorf((p - G.gmin[k]) * G.inv_cs[k]));
+        return min(max(c, 0), int(G.n[k]) - 1);
+    };
+    int cx = cell_of(__builtin_fmaf(tn, r.d.x, r.o.x), 0);
+    int cy = cell_of(__builtin_fmaf(tn, r.d.y, r.o.y), 1);
+    int cz = cell_of(__builtin_fmaf(tn, r.d.z, r.o.z), 2);
+    const int sx = r.d.x > 0.0f ? 1 : (r.d.x < 0.0f ? -1 : 0);
+    const int sy = r.d.y > 0.0f ? 1 : (r.d.y < 0.0f ? -1 : 0);
+    const int sz = r.d.z > 0.0f ? 1 : (r.d.z < 0.0f ? -1 : 0);
+    auto bound_t = [&](int c, int s, int k, float o, float inv) {
+        const float plane = __builtin_fmaf(float(c + (s > 0 ? 1 : 0)), G.cs[k], G.gmin[k]);
+        return s == 0 ? __builtin_inff() : (plane - o) * inv;
+    };
+    float tx = bound_t(cx, sx, 0, r.o.x, r.inv.x);
+    float ty = bound_t(cy, sy, 1, r.o.y, r.inv.y);
+    float tz = bound_t(cz, sz, 2, r.o.z, r.inv.z);
+    uint32_t cell = (uint32_t(cz) * G.n[1] + uint32_t(cy)) * G.n[0] + uint32_t(cx);
+    const int dxc = sx, dyc = sy * int(G.n[0]), dzc = sz * int(G.n[0] * G.n[1]);
+    const uint32_t lane = lane_id();
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t* const q = s_cq_q + wave * kCqCap;
+    unsigned long long* const key = s_cq_key + wave * 64u;
+    for (;;) {
+        const uint32_t b = cstart[cell], e = cstart[cell + 1];
+        if (COUNT) {
+            n_cell++;
+            n_empty += b == e ? 1u : 0u;
+        }
+        s_cq_n[wave] = 0u;   // every active lane writes the same value
+        lane_order();
+        uint32_t qn = 0u;   // equal on every lane still in the reference loop (they ran the same pushes)
+        for (uint32_t j = b; j < e; ++j) {
+            UTIL(1, true);
+            const float4 sp = rec[j];
+            const float ocx = r.o.x - sp.x, ocy = r.o.y - sp.y, ocz = r.o.z - sp.z;
+            const float bb = __builtin_fmaf(ocz, r.d.z, __builtin_fmaf(ocy, r.d.y, ocx * r.d.x));
+            const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - sp.w;
+            const float D = __builtin_fmaf(bb, bb, -(r.a * c));
+            if (COUNT) n_sph++;
+            const bool cand = D >= 0.0f && !behind(bb, c);
+            const unsigned long long m = __ballot(cand);
+            if (m) {   // wave-uniform
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+                const uint32_t slot = qn + rank;
+                qn = min(qn + uint32_t(__popcll(m)), kCqCap);
+                if (cand) {
+                    if (rank == 0u) s_cq_n[wave] = qn;
+                    if (slot < kCqCap) {
+                        q[slot] = lane | (j << 6);
+                    } else {   // the queue is full: this lane's own tail (rare)
+                        UTIL(2, true);
+                        const float sq = sqrt_cr(D);
+                        float t = (-bb - sq) * r.ia;
+                        if (!(t >= T_MIN)) t = (-bb + sq) * r.ia;
+                        const uint32_t id = ids[j];
+                        if ((t >= T_MIN) & (t <= r.best) & ((t < r.best) | (id < r.bi))) {
+                            r.best = t;
+                            r.bi = id;
+                        }
+                    }
+                }
+            }
+        }
+        lane_order();
+        const uint32_t qtot = __builtin_amdgcn_readfirstlane(s_cq_n[wave]);
+        if (qtot) {   // resolve the cell's candidates with every walking lane
+            key[lane] = (static_cast<unsigned long long>(__float_as_uint(r.best)) << 32) | r.bi;
+            lane_order();
+            const unsigned long long act = __ballot(true);
+            const uint32_t rk = __builtin_amdgcn_mbcnt_hi(uint32_t(act >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(act), 0u));
+            const uint32_t nact = __popcll(act);
+            for (uint32_t base = 0; base < qtot; base += nact) {   // wave-uniform trip count
+                const uint32_t k = base + rk;
+                const bool valid = k < qtot;
+                const uint32_t ent = q[valid ? k : 0u];
+                const int L = int(ent & 63u);
+                const uint32_t jj = ent >> 6;
+                const V3 o = v3(__shfl(r.o.x, L), __shfl(r.o.y, L), __shfl(r.o.z, L));
+                const V3 d = v3(__shfl(r.d.x, L), __shfl(r.d.y, L), __shfl(r.d.z, L));
+                const float a = __shfl(r.a, L), ia = __shfl(r.ia, L);
+                UTIL(2, valid);
+                const float4 sp = rec[jj];
+                const uint32_t id = ids[jj];
+                const float ocx = o.x - sp.x, ocy = o.y - sp.y, ocz = o.z - sp.z;
+                const float bb = __builtin_fmaf(ocz, d.z, __builtin_fmaf(ocy, d.y, ocx * d.x));
+                const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - sp.w;
+                const float D = __builtin_fmaf(bb, bb, -(a * c));   // the push's D: >= 0
+                const float sq = sqrt_cr(D);
+                float t = (-bb - sq) * ia;
+                if (!(t >= T_MIN)) t = (-bb + sq) * ia;   // report t1 if t1 >= tmin, else t2
+                if (valid && t >= T_MIN)
+                    __hip_atomic_fetch_min(&key[L], (static_cast<unsigned long long>(__float_as_uint(t)) << 32) | id,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            }
+            lane_order();
+            const unsigned long long kk = key[lane];
+            r.best = __uint_as_float(uint32_t(kk >> 32));
+            r.bi = uint32_t(kk);
+        }
+        r.limit = cull_limit(P, r.best);
+        UTIL(0, true);
+        const float tm = fminf(fminf(tx, ty), tz);
+        if (!(tm <= r.limit)) break;   // the next cell starts beyond every closer candidate
+        const bool mx = tx == tm, my = !mx && ty == tm, mz = !mx && !my;
+        cx += mx ? sx : 0;
+        cy += my ? sy : 0;
+        cz += mz ? sz : 0;
+        if (uint32_t(cx) >= G.n[0] || uint32_t(cy) >= G.n[1] || uint32_t(cz) >= G.n[2]) break;
+        cell += mx ? dxc : my ? dyc : dzc;
+        const int cc = mx ? cx : my ? cy : cz, s = mx ? sx : my ? sy : sz;
+        const float2 cg = s_walk_par[mx ? 0 : my ? 1 : 2];   // (cs[k], gmin[k])
+        const float ok = mx ? r.o.x : my ? r.o.y : r.o.z, ik = mx ? r.inv.x : my ? r.inv.y : r.inv.z;
+        const float tnew = (__builtin_fmaf(float(cc + (s > 0 ? 1 : 0)), cg.x, cg.y) - ok) * ik;
+        tx = mx ? tnew : tx;
+        ty = my ? tnew : ty;
+        tz = mz ? tnew : tz;
+    }
+}
+
 // ---- wave-cooperative grid walk (LAYOUT_GRID_COOP) ---------------------------
 // Wave64 inclusive scans through DPP: row_shr 1/2/4/8 inside each 16-lane row (zero fill), then
 // row_bcast:15 (lane 15 of rows 0 / 2 into rows 1 / 3) and row_bcast:31 (lane 31 into rows 2, 3).
@@ -1214,10 +1365,6 @@ __shared__ float4 s_coop_ray[2 * RT_TRACE_BLOCK];
 __shared__ unsigned long long s_coop_key[RT_TRACE_BLOCK];
 __shared__ uint32_t s_coop_mark[RT_TRACE_BLOCK];
 static_assert(sizeof(s_coop_ray) + sizeof(s_coop_key) + sizeof(s_coop_mark) == rt::kCoopLdsBytes, "rt_internal.h");
-
-// Compiler-only ordering of LDS accesses made by different lanes of one wave: the LDS executes a
-// wave's instructions in issue order, so no wait or barrier is needed, only no reordering.
-__device__ __forceinline__ void lane_order() { asm volatile("" ::: "memory"); }
 
 // The grid walk of grid_walk with the reference tests of a wave's rays spread over all 64 lanes.
 // Rounds: every walking lane takes its current cell's n references; an exclusive scan of n gives
@@ -1409,6 +1556,11 @@ template <bool COUNT, int LAYOUT>
 __device__ __forceinline__ void walk(const rt::TraceParams& P, const float4* __restrict__ nodes4,
                                      const float4* __restrict__ leaf4, const uint32_t* __restrict__ leaf_ids,
                                      Ray& r, uint32_t& n_box, uint32_t& n_sph, uint32_t& n_empty) {
+    if (LAYOUT == LAYOUT_GRID_CQ) {
+        if (r.walk)
+            grid_walk_cq<COUNT>(P, reinterpret_cast<const uint32_t*>(nodes4), leaf4, leaf_ids, r, n_box, n_sph, n_empty);
+        return;
+    }
     if (LAYOUT == LAYOUT_GRID || LAYOUT == LAYOUT_GRID_L2) {   // nodes4 = cell offsets, leaf4 / leaf_ids = references
         if (r.walk)
             grid_walk<COUNT, LAYOUT == LAYOUT_GRID_L2>(P, reinterpret_cast<const uint32_t*>(nodes4), leaf4, leaf_ids, r,
@@ -1506,7 +1658,8 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
                                           const uint32_t* __restrict__ leaf_ids,
                                           const float4* __restrict__ geom4, const float4* __restrict__ mat4) {
     constexpr bool LSUM = MODE == rt::MODE_HASH &&
-                          (LAYOUT == LAYOUT_GRID || LAYOUT == LAYOUT_GRID_L2 || LAYOUT == LAYOUT_GRID_COOP);
+                          (LAYOUT == LAYOUT_GRID || LAYOUT == LAYOUT_GRID_L2 || LAYOUT == LAYOUT_GRID_COOP ||
+                           LAYOUT == LAYOUT_GRID_CQ);
     const uint32_t lane = lane_id();
     const Camera cam = load_camera(P);
     uint32_t st = ST_NEED_UNIT;
@@ -1688,7 +1841,7 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
 
 // Grid kernel (ACCEL_GRID): the grid's cell offsets and references staged in LDS once per
 // persistent block: [references (float4) | reference ids | cell offsets | shading records (REC)].
-template <bool COUNT, int MODE, bool IN_LDS, bool COOP = false, bool REC = false>
+template <bool COUNT, int MODE, bool IN_LDS, bool COOP = false, bool REC = false, bool CQ = false>
 __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace_grid_kernel(const rt::TraceParams P) {
     UTIL_INIT;
     PLACEMENT_RECORD(P);
@@ -1724,11 +1877,12 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
             smat[2 * i + 1] = mat4[2 * i + 1];
         }
         __syncthreads();
-        lbvh_loop<COUNT, LAYOUT_GRID, MODE, true>(P, reinterpret_cast<const float4*>(cst), lds, ids, srec, smat);
+        lbvh_loop<COUNT, CQ ? LAYOUT_GRID_CQ : LAYOUT_GRID, MODE, true>(P, reinterpret_cast<const float4*>(cst), lds, ids,
+                                                                        srec, smat);
         return;
     }
     __syncthreads();
-    lbvh_loop<COUNT, COOP ? LAYOUT_GRID_COOP : LAYOUT_GRID, MODE>(P, reinterpret_cast<const float4*>(cst), lds, ids,
+    lbvh_loop<COUNT, COOP ? LAYOUT_GRID_COOP : CQ ? LAYOUT_GRID_CQ : LAYOUT_GRID, MODE>(P, reinterpret_cast<const float4*>(cst), lds, ids,
                                         reinterpret_cast<const float4*>(P.geom),
                                         reinterpret_cast<const float4*>(P.mat));
 }
@@ -1899,6 +2053,12 @@ static const void* pick_mode(uint32_t accel, bool count) {
         case ACCEL_GRID_REC:
             return count ? RT_FN(rt_trace_grid_kernel<true, MODE, true, false, true>)
                          : RT_FN(rt_trace_grid_kernel<false, MODE, true, false, true>);
+        case ACCEL_GRID_CQ:
+            return count ? RT_FN(rt_trace_grid_kernel<true, MODE, true, false, false, true>)
+                         : RT_FN(rt_trace_grid_kernel<false, MODE, true, false, false, true>);
+        case ACCEL_GRID_REC_CQ:
+            return count ? RT_FN(rt_trace_grid_kernel<true, MODE, true, false, true, true>)
+                         : RT_FN(rt_trace_grid_kernel<false, MODE, true, false, true, true>);
         case ACCEL_GRID_GLOBAL_COOP:
             return count ? RT_FN(rt_trace_grid_kernel<true, MODE, false, true>)
                          : RT_FN(rt_trace_grid_kernel<false, MODE, false, true>);

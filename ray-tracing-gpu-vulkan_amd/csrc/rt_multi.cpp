@@ -142,8 +142,10 @@ int set_partition(rt_multi* m, const std::string& key, uint32_t W, uint32_t H,
         if (nr) {
             RT_HIP(hipMalloc(&l.rows_root, nr * 4));
             RT_HIP(hipMemcpy(l.rows_root, l.rows.data(), nr * 4, hipMemcpyHostToDevice));
-            RT_HIP(hipMalloc(&l.stage_acc, texels * 16));
-            RT_HIP(hipMalloc(&l.stage_out, texels * 4));
+            if (l.dev != 0) {   // device 0's own bands are scattered in place (gather_to_root)
+                RT_HIP(hipMalloc(&l.stage_acc, texels * 16));
+                RT_HIP(hipMalloc(&l.stage_out, texels * 4));
+            }
         }
     }
     m->key = key;
@@ -158,15 +160,16 @@ std::vector<std::pair<uint32_t, std::vector<uint32_t>>> strip_parts(uint32_t n, 
     return parts;
 }
 
-// One RCCL group moves every launch's band (float4 accumulator, then rgba8 image) to device 0
-// (device 0's own bands included: a send to itself), then one kernel per band puts its rows in
-// place in dst (device 0 pointers, W x H). Everything on stream[0] after the group.
+// One RCCL group moves every other device's bands (float4 accumulator, then rgba8 image) to
+// device 0, then one kernel per band puts its rows in place in dst (device 0 pointers, W x H);
+// device 0's own bands go straight from its render buffers (no send to itself: at N = 1 the frame
+// moves no byte through RCCL). Everything on stream[0] after the group.
 int gather_to_root(rt_multi* m, float* dst_acc, uint8_t* dst_out) {
     const uint32_t W = m->W;
     RT_NCCL(ncclGroupStart());
     for (Launch& l : m->launches) {
         const size_t texels = l.rows.size() * size_t(W);
-        if (!texels) continue;
+        if (!texels || l.dev == 0) continue;
         ncclResult_t e;
         {
             DeviceGuard g(static_cast<int>(l.dev));
@@ -186,8 +189,9 @@ int gather_to_root(rt_multi* m, float* dst_acc, uint8_t* dst_out) {
     RT_NCCL(ncclGroupEnd());
     for (Launch& l : m->launches) {
         if (l.rows.empty()) continue;
-        if (int rc = rt_scatter_rows(m->launches[0].ctx, l.stage_acc, l.stage_out, l.rows_root,
-                                     uint32_t(l.rows.size()), W, m->H, dst_acc, dst_out, m->stream[0]))
+        const bool own = l.dev == 0;   // rendered on stream[0] itself
+        if (int rc = rt_scatter_rows(m->launches[0].ctx, own ? l.acc : l.stage_acc, own ? l.out : l.stage_out,
+                                     l.rows_root, uint32_t(l.rows.size()), W, m->H, dst_acc, dst_out, m->stream[0]))
             return rc;
     }
     return RT_OK;

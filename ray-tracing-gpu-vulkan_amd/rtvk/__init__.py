@@ -233,7 +233,7 @@ class Renderer:
         v = (ctypes.c_uint32 * 4)()
         check(self._lib.rt_debug_launch_info(self._ctx, v))
         forms = {1: "brute", 2: "lbvh-global", 3: "lbvh-lds", 4: "lbvh-octant-lds", 5: "lbvh-treelet", 6: "grid-lds", 7: "grid-global",
-                 8: "grid-lds-coop", 9: "grid-global-coop", 10: "grid-lds-rec"}
+                 8: "grid-lds-coop", 9: "grid-global-coop", 10: "grid-lds-rec", 11: "grid-lds-cq", 12: "grid-lds-rec-cq"}
         return {"chunks": int(v[0]) & 0xffff, "head_chunks": (int(v[0]) >> 16) or None,
                 "form": forms.get(int(v[1]), str(v[1])), "lds_bytes": int(v[2]), "cus": int(v[3])}
 

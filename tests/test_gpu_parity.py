@@ -24,8 +24,9 @@ LBVH_OCT = 8       # test-only alias: accel LBVH, the tree's 8 octant copies in 
                    # treelet (device trees) (options.reserved[1] = 8)
 GRID = 12          # test-only alias: the uniform grid (options.reserved[1] = 12)
 GRID_COOP = 14     # test-only alias: the uniform grid in LDS, wave-cooperative walk (options.reserved[1] = 14)
-WALK_FORM = {LBVH_LDS1: 6, LBVH_GLOBAL: 10, LBVH_OCT: 8, GRID: 12, GRID_COOP: 14}
-FORMS = [BRUTE, LBVH, LBVH_OCT, LBVH_LDS1, LBVH_GLOBAL, GRID_COOP]   # LBVH: the default form (the grid for host scenes)
+GRID_CQ = 16       # test-only alias: the uniform grid in LDS, wave-wide candidate queue (options.reserved[1] = 16)
+WALK_FORM = {LBVH_LDS1: 6, LBVH_GLOBAL: 10, LBVH_OCT: 8, GRID: 12, GRID_COOP: 14, GRID_CQ: 16}
+FORMS = [BRUTE, LBVH, LBVH_OCT, LBVH_LDS1, LBVH_GLOBAL, GRID_COOP, GRID_CQ]   # LBVH: the default form (the grid for host scenes)
 STREAM, COUNTER, HASH = 0, 1, 2
 
 
@@ -286,7 +287,7 @@ def test_grid_near_cull_slack_mixed_radii(rtvk, renderer, torch, oracle, builder
         for rng_mode in (STREAM, HASH):
             ra, ro, _ = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=rng_mode))
             for full in (None, "1"):
-                for accel in (LBVH, GRID_COOP):
+                for accel in (LBVH, GRID_COOP, GRID_CQ):
                     with tuned(renderer, grid_full_slack=full):
                         a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=accel, rng_mode=rng_mode,
                                              builder=builder)
@@ -316,7 +317,7 @@ def test_grid_lattice_axis_rays(rtvk, renderer, torch, oracle, builder):
         f[8:11] = cam
         f[12:15] = [look[k] - cam[k] for k in range(3)]
         ra, ro, _ = oracle.render(sc, rci, W, H)
-        for accel in (BRUTE, LBVH, GRID, GRID_COOP, LBVH_OCT, LBVH_GLOBAL):
+        for accel in (BRUTE, LBVH, GRID, GRID_COOP, GRID_CQ, LBVH_OCT, LBVH_GLOBAL):
             a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=accel, builder=builder)
             assert_same(a, o, ra, ro)
 
