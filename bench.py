@@ -635,6 +635,18 @@ def main() -> int:
             cs = rtvk.Stats(segments=0, samples=0, box_tests=int(t[0].item()), sphere_tests=int(t[1].item()))
             st = rtvk.Stats(segments=int(t[2].item()), samples=int(t[3].item()), box_tests=0, sphere_tests=0)
     form = "brute" if accel == abi.RT_ACCEL_BRUTE else info["form"]
+    # host cost of one per-frame scene call with the GPU idle (host build + upload issue for host
+    # scenes; for device builds it includes the build, which in the timed loop overlaps the
+    # previous frame): the per-frame setup a rank pays outside the kernel
+    sync_all()
+    t_sc = time.perf_counter()
+    for _ in range(5):
+        if mode == "multi":
+            mr.set_scene(scene)
+        else:
+            renderer.set_scene(scene)
+    scene_call_ms = (time.perf_counter() - t_sc) / 5 * 1e3
+    sync_all()
 
     samples_per_step = W * H * spp
     value = samples_per_step * args.steps / elapsed / 1e6
@@ -694,6 +706,7 @@ def main() -> int:
                        "frames_in_flight": 1 if mode == "multi" else len(slots)},
             "segments_per_sample": round(st.segments / max(1, st.samples), 4),
             "scene_setup_ms": round(t_scene * 1e3, 2),
+            "scene_call_ms": round(scene_call_ms, 3),
             "msegments_per_s": round(st.segments / max(1, st.samples) * value, 2),
             "roofline": roof,
             "build": {**abi.build_info(), "env": knobs,

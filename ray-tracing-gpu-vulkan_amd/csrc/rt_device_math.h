@@ -27,28 +27,16 @@ __device__ __forceinline__ V3 neg(V3 a) { return v3(-a.x, -a.y, -a.z); }
 // e = 1 - x r is exact in an fma; the result is the correctly rounded quotient. Other inputs (0,
 // inf, NaN, denormal and huge x) take the division. Bit-identical to 1.0f / x for all 2^32 inputs
 // (scripts/exact_math_exhaustive.hip, run on the GPU; profiles/r02_exact_math_exhaustive.log).
-// RT_FLAT_CR 1 (shipped): rcp_cr / sqrt_cr compute the fast form for every lane and redo only the
-// out-of-range lanes in a rarely entered branch, one exec-mask region instead of an if / else pair
-// per call (config 3 -2.0 %, config 5 -1.9 %; 0 builds the if / else form for A/B).
-#ifndef RT_FLAT_CR
-#define RT_FLAT_CR 1
-#endif
+// Both compute the fast form for every lane and redo only the out-of-range lanes in a rarely
+// entered branch: one exec-mask region per call instead of an if / else pair (config 3 -2.0 %,
+// config 5 -1.9 % against the if / else form).
 __device__ __forceinline__ float rcp_cr(float x) {
     const uint32_t ax = __float_as_uint(x) & 0x7fffffffu;
-#if RT_FLAT_CR   // the fast form for every lane, the library form only where it is out of range
     const float r = __builtin_amdgcn_rcpf(x);
     const float e = __builtin_fmaf(-x, r, 1.0f);
     float q = __builtin_fmaf(e, r, r);
-    if (__builtin_expect(ax - 0x01000000u > 0x7e000000u - 0x01000000u, 0)) q = 1.0f / x;
+    if (__builtin_expect(ax - 0x01000000u > 0x7e000000u - 0x01000000u, 0)) q = 1.0f / x;   // outside [2^-125, 2^125]
     return q;
-#else
-    if (ax - 0x01000000u <= 0x7e000000u - 0x01000000u) {   // 2^-125 <= |x| <= 2^125
-        const float r = __builtin_amdgcn_rcpf(x);
-        const float e = __builtin_fmaf(-x, r, 1.0f);
-        return __builtin_fmaf(e, r, r);
-    }
-    return 1.0f / x;
-#endif
 }
 
 // Correctly rounded sqrt(x), cheaper than hipcc's general sequence: for x in [2^-100, 2^100] the
@@ -58,30 +46,15 @@ __device__ __forceinline__ float rcp_cr(float x) {
 // to it for all 2^32 inputs (scripts/exact_math_exhaustive.hip).
 __device__ __forceinline__ float sqrt_cr(float x) {
     const uint32_t ux = __float_as_uint(x);
-#if RT_FLAT_CR   // the fast form for every lane, the library form only where it is out of range
-    {
-        const float s = __builtin_amdgcn_sqrtf(x);
-        const float sm = __uint_as_float(__float_as_uint(s) - 1u);
-        const float sp = __uint_as_float(__float_as_uint(s) + 1u);
-        const float rm = __builtin_fmaf(-sm, s, x);
-        const float rp = __builtin_fmaf(-sp, s, x);
-        float t = rm <= 0.0f ? sm : s;
-        t = rp > 0.0f ? sp : t;
-        if (__builtin_expect(ux - 0x0d800000u > 0x71800000u - 0x0d800000u, 0)) t = __builtin_sqrtf(x);
-        return t;
-    }
-#endif
-    if (ux - 0x0d800000u <= 0x71800000u - 0x0d800000u) {   // 2^-100 <= x <= 2^100 (x > 0)
-        const float s = __builtin_amdgcn_sqrtf(x);
-        const float sm = __uint_as_float(__float_as_uint(s) - 1u);
-        const float sp = __uint_as_float(__float_as_uint(s) + 1u);
-        const float rm = __builtin_fmaf(-sm, s, x);
-        const float rp = __builtin_fmaf(-sp, s, x);
-        float t = rm <= 0.0f ? sm : s;
-        t = rp > 0.0f ? sp : t;
-        return t;
-    }
-    return __builtin_sqrtf(x);
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = __uint_as_float(__float_as_uint(s) - 1u);
+    const float sp = __uint_as_float(__float_as_uint(s) + 1u);
+    const float rm = __builtin_fmaf(-sm, s, x);
+    const float rp = __builtin_fmaf(-sp, s, x);
+    float t = rm <= 0.0f ? sm : s;
+    t = rp > 0.0f ? sp : t;
+    if (__builtin_expect(ux - 0x0d800000u > 0x71800000u - 0x0d800000u, 0)) t = __builtin_sqrtf(x);   // outside [2^-100, 2^100]
+    return t;
 }
 
 // dot(a,b) = fma(a.z,b.z, fma(a.y,b.y, a.x*b.x))

@@ -1150,6 +1150,29 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
             ++j;
           }
         }
+#ifndef RT_LDS_IDPRE
+#define RT_LDS_IDPRE 0
+#endif
+#if RT_LDS_IDPRE
+        if (!PAIRS && j < e) {   // LDS: records and ids one ahead (past the run: the next cell's, or LDS beyond)
+            float4 A = rec[j], B;
+            uint32_t iA = ids[j], iB;
+            for (;;) {
+                UTIL(1, true);
+                B = rec[j + 1];
+                iB = ids[j + 1];
+                test1<true>(A, [&] { return iA; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
+                if (COUNT) n_sph++;
+                if (++j >= e) break;
+                UTIL(1, true);
+                A = rec[j + 1];
+                iA = ids[j + 1];
+                test1<true>(B, [&] { return iB; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
+                if (COUNT) n_sph++;
+                if (++j >= e) break;
+            }
+        }
+#else
         if (!PAIRS && j < e) {   // LDS: two records in flight, no register copies (unrolled by two)
             float4 A = rec[j], B;
             for (;;) {
@@ -1165,6 +1188,7 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
                 if (++j >= e) break;
             }
         }
+#endif
         UTIL(0, true);
         const float tm = fminf(fminf(tx, ty), tz);
         if (!(tm <= r.limit)) break;   // the next cell starts beyond every closer candidate

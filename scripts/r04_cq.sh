@@ -9,7 +9,8 @@ TAG=${TAG:-r04b}
 fatal() { [ "$1" -ge 124 ] && { echo "fatal rc=$1 in $2: stopping"; exit "$1"; }; return 0; }
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > gpurun_out/${TAG}_pytest_gpu.log 2>&1
 rc=$?; tail -4 gpurun_out/${TAG}_pytest_gpu.log; fatal $rc pytest; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 python scripts/perf_variants.py --spp 1000 --rounds 4 --accels 2 --rng 2,0 --walk 0,16 > gpurun_out/${TAG}_ab_cq.log 2>&1
+V=$(ls ray-tracing-gpu-vulkan_amd/lib/variants/*.so 2>/dev/null | grep -v util)
+timeout -k 10 400 python scripts/perf_variants.py --spp 1000 --rounds 4 --accels 2 --rng 2,0 --walk 0,16 $V > gpurun_out/${TAG}_ab_cq.log 2>&1
 rc=$?; grep -v amdgpu.ids gpurun_out/${TAG}_ab_cq.log; fatal $rc ab_cq
 for w in 0 16; do
   RT_LIB=ray-tracing-gpu-vulkan_amd/lib/variants/librt_util.so RT_WALK=$w timeout -k 10 200 python scripts/lane_util.py 100 > gpurun_out/${TAG}_util_walk$w.log 2>&1
