@@ -12,6 +12,8 @@ rc=$?; tail -4 gpurun_out/${TAG}_pytest_gpu.log; fatal $rc pytest; [ $rc -eq 0 ]
 V=$(ls ray-tracing-gpu-vulkan_amd/lib/variants/*.so 2>/dev/null | grep -v util)
 timeout -k 10 400 python scripts/perf_variants.py --spp 1000 --rounds 4 --accels 2 --rng 2,0 --walk 0,16 $V > gpurun_out/${TAG}_ab_cq.log 2>&1
 rc=$?; grep -v amdgpu.ids gpurun_out/${TAG}_ab_cq.log; fatal $rc ab_cq
+timeout -k 10 400 python scripts/perf_variants.py --spp 100 --rounds 4 --accels 2 --rng 2 --width 3840 --height 2160 --grid 158 $V > gpurun_out/${TAG}_ab_c5.log 2>&1
+rc=$?; grep -v amdgpu.ids gpurun_out/${TAG}_ab_c5.log; fatal $rc ab_c5
 for w in 0 16; do
   RT_LIB=ray-tracing-gpu-vulkan_amd/lib/variants/librt_util.so RT_WALK=$w timeout -k 10 200 python scripts/lane_util.py 100 > gpurun_out/${TAG}_util_walk$w.log 2>&1
   rc=$?; grep -v amdgpu.ids gpurun_out/${TAG}_util_walk$w.log; fatal $rc util$w
