@@ -108,3 +108,18 @@ def test_store_ppm(rtvk, tmp_path):
     np.testing.assert_array_equal(px, img[..., :3])
     with pytest.raises(rtvk.RtError):
         rtvk.store_ppm(str(tmp_path / "no" / "such" / "dir.ppm"), img)
+
+
+def test_library_reads_only_documented_environment():
+    """The shipped library reads exactly the two environment variables INTEGRATION.md §5 lists
+    (RT_RNG in ray_trace(), RT_BVH_BUILD in the builder choice); every other launch-plan parameter
+    goes through rt_debug_tune."""
+    import re
+    from pathlib import Path
+    csrc = Path(__file__).resolve().parent.parent / "ray-tracing-gpu-vulkan_amd" / "csrc"
+    text = "".join(p.read_text() for p in sorted(csrc.iterdir()) if p.suffix in (".cpp", ".hip", ".h"))
+    read = set(re.findall(r'getenv\("([A-Z_]+)"\)', text))
+    assert read == {"RT_RNG", "RT_BVH_BUILD"}, read
+    integ = (Path(__file__).resolve().parent.parent / "INTEGRATION.md").read_text()
+    for var in read:
+        assert f"`{var}" in integ, var
