@@ -20,4 +20,11 @@ for w in 0 16; do
 done
 timeout -k 10 300 python bench.py --config 5 --path multi --gpus 1 --steps 3 --warmup 2 --no-cpu-baseline --no-rebuild-check > gpurun_out/${TAG}_bench_c5_multi.json 2> gpurun_out/${TAG}_bench_c5_multi.err
 rc=$?; tail -c 300 gpurun_out/${TAG}_bench_c5_multi.json; fatal $rc bench_c5_multi
+RT_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+    --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 2 --warmup 1 --spp 1000 \
+    > gpurun_out/${TAG}_rehearsal_n2_gloo.json 2> gpurun_out/${TAG}_rehearsal_n2_gloo.err
+rc=$?; echo "gloo n2 rc=$rc"; tail -c 600 gpurun_out/${TAG}_rehearsal_n2_gloo.json; fatal $rc gloo_n2
+timeout -k 10 300 python bench.py --path multi --gpus 1 --steps 5 --warmup 2 --no-cpu-baseline --no-rebuild-check \
+    > gpurun_out/${TAG}_bench_multi_n1.json 2> gpurun_out/${TAG}_bench_multi_n1.err
+rc=$?; echo "multi n1 rc=$rc"; tail -c 400 gpurun_out/${TAG}_bench_multi_n1.json; fatal $rc multi_n1
 echo done
