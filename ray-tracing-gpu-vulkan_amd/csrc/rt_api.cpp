@@ -32,7 +32,7 @@ hipError_t trace_occupancy(uint32_t accel, bool count, int mode, size_t lds_byte
 hipError_t launch_resolve_fixed(unsigned long long* fixed, uint64_t n_texels, uint32_t accumulate, uint32_t spp,
                                 float* accum, uint8_t* out, hipStream_t st);
 hipError_t launch_tonemap(const float* accum, uint64_t n_texels, uint32_t spp, uint8_t* out, hipStream_t st);
-hipError_t launch_big_table(const TraceParams& P, float* tab, hipStream_t st);
+hipError_t launch_prep(const TraceParams& P, uint32_t work_head, float* tab, uint32_t n_cost, hipStream_t st);
 uint32_t block_size(uint32_t accel);
 hipError_t launch_scatter_rows(const float* src_acc, const uint8_t* src_px, const uint32_t* rows,
                                uint32_t n_rows, uint32_t width, uint32_t dst_rows, float* dst_acc, uint8_t* dst_px,
@@ -1191,8 +1191,7 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
             RT_HIP(rt::schedule_order(sc, st));
             P.tile_order = sc.order;
         }
-        RT_HIP(hipMemsetAsync(sc.cost[sc.cur], 0, size_t(sc.n) * 4, st));
-        P.tile_cost = sc.cost[sc.cur];
+        P.tile_cost = sc.cost[sc.cur];   // zeroed by the launch's prep kernel
         P.tile_cost_sum = sched == 2 ? 1u : 0u;
     }
     // Head and tail of the LPT order (HASH): the frame's tail is made of the units
@@ -1233,9 +1232,6 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
         sc.rec_head_chunks[sc.cur] = P.head_chunks;
         sc.rec_chunks[sc.cur] = P.chunks;
     }
-    RT_HIP(hipMemsetAsync(ctx->counters, 0, sizeof(rt::Counters), st));
-    // first-time stamps start at the maximum (atomicMin); 0xff bytes = ~0ull
-    RT_HIP(hipMemsetAsync(&ctx->counters->t_first, 0xff, 2 * sizeof(unsigned long long), st));
     const uint64_t full = uint64_t(ctx->cu_count) * ctx->occ[accel][ci][mode];
     const uint64_t by_work = (uint64_t(P.n_units) + blk - 1) / blk;
     const int grid = int(std::max<uint64_t>(1, std::min(full, by_work)));
@@ -1252,8 +1248,6 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
         // units are short: no isolation.
         const uint64_t iso = uint64_t(Tuning::get(ctx->tune.isolate_tiles, double(uint64_t(grid) * blk / 64u / 512u)));
         P.isolate_blocks = (P.tile_order && mode == rt::MODE_STREAM) ? uint32_t(std::min<uint64_t>(P.first_blocks, iso)) : 0u;
-        if (P.first_blocks) RT_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&ctx->counters->work_head),
-                                                     int(P.first_blocks * 64u), 1, st));
     }
     if (accel == rt::ACCEL_LBVH_TOP && ctx->treelet_stale) {   // after a build, refit or re-pad
         RT_HIP(rt::build_treelet(d.nodes, d.n_nodes, d.treelet, d.treelet_count, st));
@@ -1262,7 +1256,8 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     hipEvent_t* kev = ctx->kev[ctx->kev_count % rt_context::kKernelEvents];
     for (int k = 0; k < 2; k++)
         if (!kev[k]) RT_HIP(hipEventCreate(&kev[k]));
-    if (P.n_big) RT_HIP(rt::launch_big_table(P, ctx->big_tab, st));
+    // counters zeroed, work counter past the first blocks, big-sphere table, tile-cost table zeroed
+    RT_HIP(rt::launch_prep(P, P.first_blocks * 64u, ctx->big_tab, P.tile_cost ? uint32_t(n_tiles) : 0u, st));
     P.big_tab = ctx->big_tab;
     RT_HIP(hipEventRecord(kev[0], st));
     RT_HIP(rt::launch_trace(P, accel, count, mode, grid, lds, st));

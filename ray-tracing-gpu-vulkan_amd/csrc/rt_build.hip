@@ -583,7 +583,7 @@ hipError_t schedule_reserve(TileSchedule& s, uint32_t n, hipStream_t st) {
     if (e == hipSuccess) e = alloc(&s.norm, n);
     if (e == hipSuccess)
         e = hipcub::DeviceRadixSort::SortPairsDescending(nullptr, s.tmp_bytes, s.cost[0], s.keys, s.iota, s.order,
-                                                         int(n), 0, 32);
+                                                         int(n), 0, 16);
     if (e == hipSuccess) e = hipMalloc(&s.tmp, s.tmp_bytes + 16);
     if (e == hipSuccess) e = hipMemsetAsync(s.cost[0], 0, size_t(n) * 4, st);
     if (e == hipSuccess) e = hipMemsetAsync(s.cost[1], 0, size_t(n) * 4, st);
@@ -599,30 +599,29 @@ hipError_t schedule_reserve(TileSchedule& s, uint32_t n, hipStream_t st) {
     return hipSuccess;
 }
 
-// norm[order[r]] = cost[order[r]] x the chunk count of rank r in the launch that recorded it
-// (saturating). Written beside the recorded costs, never over them: schedule_order may run again on
-// the same record (a launch that fails after it), and must not scale it twice.
+// The sort key of tile order[r]: its recorded cost x the chunk count of rank r in the launch that
+// recorded it (head_tiles 0: x 1), as the top 16 bits of its binary32 value (8 exponent + 7
+// mantissa bits: monotonic in the cost, 2 radix passes instead of 4; the order is a scheduling
+// heuristic, any order renders the same image). Written beside the recorded costs, never over
+// them: schedule_order may run again on the same record (a launch that fails after it).
 __global__ void k_cost_norm(const uint32_t* __restrict__ cost, const uint32_t* __restrict__ order, uint32_t n,
                             uint32_t head_tiles, uint32_t head_chunks, uint32_t chunks, uint32_t* __restrict__ norm) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= n) return;
-    const uint32_t t = order[r];
-    const uint64_t v = uint64_t(cost[t]) * (r < head_tiles ? head_chunks : chunks);
-    norm[t] = uint32_t(v < 0xffffffffull ? v : 0xffffffffull);
+    const uint32_t t = head_tiles ? order[r] : r;
+    const float v = float(cost[t]) * float(head_tiles ? (r < head_tiles ? head_chunks : chunks) : 1u);
+    norm[t] = __float_as_uint(v) >> 16;
 }
 
 hipError_t schedule_order(TileSchedule& s, hipStream_t st) {
     const int last = s.cur ^ 1;
-    const uint32_t* key = s.cost[last];
-    if (s.rec_head_tiles[last]) {   // `order` still holds the ranks that launch handed out
-        k_cost_norm<<<blocks(s.n), kBlock, 0, st>>>(s.cost[last], s.order, s.n, s.rec_head_tiles[last],
-                                                   s.rec_head_chunks[last], s.rec_chunks[last], s.norm);
-        if (hipError_t e = hipGetLastError()) return e;
-        key = s.norm;
-    }
+    // head_tiles != 0: `order` still holds the ranks that launch handed out
+    k_cost_norm<<<blocks(s.n), kBlock, 0, st>>>(s.cost[last], s.order, s.n, s.rec_head_tiles[last],
+                                               s.rec_head_chunks[last], s.rec_chunks[last], s.norm);
+    if (hipError_t e = hipGetLastError()) return e;
     size_t tb = s.tmp_bytes;
-    return hipcub::DeviceRadixSort::SortPairsDescending(s.tmp, tb, key, s.keys, s.iota, s.order,
-                                                        int(s.n), 0, 32, st);
+    return hipcub::DeviceRadixSort::SortPairsDescending(s.tmp, tb, s.norm, s.keys, s.iota, s.order,
+                                                        int(s.n), 0, 16, st);
 }
 
 hipError_t build_treelet(const BvhNode* nodes, uint32_t n_nodes, float* out, uint32_t* out_count, hipStream_t st) {

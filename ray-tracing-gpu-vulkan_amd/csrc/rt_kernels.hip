@@ -2002,16 +2002,34 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
 // The big-sphere table of a launch (TraceParams::big_tab): records {cx, cy, cz, r} of the n_big
 // spheres, padded to a multiple of 4 by repeating the last (a duplicate never changes (best, bi)),
 // then their ids. One wave, before the trace kernel on the same stream.
-__global__ __launch_bounds__(64) void rt_big_table_kernel(const rt::GeomRec* __restrict__ geom,
-                                                          const float* __restrict__ radius,
-                                                          const uint32_t* __restrict__ big_ids, uint32_t n_big,
-                                                          float4* __restrict__ tab) {
-    const uint32_t i = threadIdx.x, nb4 = (n_big + 3u) & ~3u;
-    if (i >= nb4 || n_big == 0u) return;
-    const uint32_t id = big_ids[min(i, n_big - 1u)];
-    const rt::GeomRec g = geom[id];
-    tab[i] = make_float4(g.cx, g.cy, g.cz, radius[id]);
-    reinterpret_cast<uint32_t*>(tab + rt::kBigMax)[i] = id;
+// Per-launch preparation in one kernel instead of five stream operations: block 0
+// zeroes the counters, starts the first-time stamps at the maximum (atomicMin), sets the work
+// counter past the blocks the waves take by wave id, and fills the big-sphere table; every block
+// zeroes its share of the tile-cost table this launch records into.
+__global__ __launch_bounds__(256) void rt_launch_prep_kernel(rt::Counters* __restrict__ counters, uint32_t work_head,
+                                                             const rt::GeomRec* __restrict__ geom,
+                                                             const float* __restrict__ radius,
+                                                             const uint32_t* __restrict__ big_ids, uint32_t n_big,
+                                                             float4* __restrict__ tab, uint32_t* __restrict__ cost,
+                                                             uint32_t n_cost) {
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n_cost; i += gridDim.x * 256u) cost[i] = 0u;
+    if (blockIdx.x != 0) return;
+    static_assert(sizeof(rt::Counters) % 8 == 0, "counters are zeroed as u64 words");
+    unsigned long long* w = reinterpret_cast<unsigned long long*>(counters);
+    for (uint32_t i = threadIdx.x; i < sizeof(rt::Counters) / 8u; i += 256u) w[i] = 0ull;
+    const uint32_t nb4 = (n_big + 3u) & ~3u;
+    if (threadIdx.x < nb4 && n_big != 0u) {
+        const uint32_t id = big_ids[min(threadIdx.x, n_big - 1u)];
+        const rt::GeomRec g = geom[id];
+        tab[threadIdx.x] = make_float4(g.cx, g.cy, g.cz, radius[id]);
+        reinterpret_cast<uint32_t*>(tab + rt::kBigMax)[threadIdx.x] = id;
+    }
+    __syncthreads();   // the words below were zeroed by other threads of the block
+    if (threadIdx.x == 0) {
+        counters->t_first = ~0ull;
+        counters->t_dry = ~0ull;
+        counters->work_head = work_head;
+    }
 }
 
 __global__ __launch_bounds__(256) void rt_resolve_fixed_kernel(unsigned long long* __restrict__ fixed, uint64_t n,
@@ -2174,9 +2192,10 @@ static uint32_t stream_blocks(uint64_t n) {
     return uint32_t(need < 8192 ? need : 8192);
 }
 
-hipError_t launch_big_table(const TraceParams& P, float* tab, hipStream_t st) {
-    hipLaunchKernelGGL(rt_big_table_kernel, dim3(1), dim3(rt::kBigMax), 0, st, P.geom, P.radius, P.big_ids, P.n_big,
-                       reinterpret_cast<float4*>(tab));
+hipError_t launch_prep(const TraceParams& P, uint32_t work_head, float* tab, uint32_t n_cost, hipStream_t st) {
+    const uint32_t blocks = n_cost > 4096u ? min(64u, (n_cost + 4095u) / 4096u) : 1u;
+    hipLaunchKernelGGL(rt_launch_prep_kernel, dim3(blocks), dim3(256), 0, st, P.counters, work_head, P.geom, P.radius,
+                       P.big_ids, P.n_big, reinterpret_cast<float4*>(tab), P.tile_cost, n_cost);
     return hipGetLastError();
 }
 
