@@ -564,10 +564,12 @@ def main() -> int:
     # trace-kernel durations inside the timed region (HIP events the library records around the
     # kernel on its launch stream; rt_debug_kernel_times)
     if mode == "multi":
-        per_dev = mr.kernel_times()   # last frame, each device
-        kernel_ms = max(per_dev) if per_dev else 0.0
-        k_basis = (f"last timed frame, slowest of {len(per_dev)} devices' trace kernels (HIP events on each "
-                   f"launch stream): {', '.join(f'{v:.2f}' for v in per_dev)} ms")
+        frames = mr.kernel_times(min(64, args.steps))   # per timed frame, each device
+        per_frame = [max(f) for f in frames if f]
+        kernel_ms = sum(per_frame) / max(1, len(per_frame))
+        last = frames[-1] if frames else []
+        k_basis = (f"mean over the {len(per_frame)} timed frames of the slowest device's trace kernel (HIP events "
+                   f"on each launch stream); last frame per device: {', '.join(f'{v:.2f}' for v in last)} ms")
     else:
         ks = []
         for sl in slots:

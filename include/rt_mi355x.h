@@ -225,6 +225,9 @@ int rt_multi_info(const rt_multi* m, uint32_t* out4);
 /* Trace-kernel duration (ms, HIP events on the launch stream) of the last frame on each device
  * that rendered rows, in device order; *count = devices written (synchronises). */
 int rt_multi_kernel_times(rt_multi* m, float* out_ms, uint32_t capacity, uint32_t* count);
+/* The same for each of the last `frames` frames (at most 64): out_ms[f * devices + d], oldest frame
+ * first; *count = frames x devices that rendered rows (synchronises). */
+int rt_multi_kernel_times_frames(rt_multi* m, uint32_t frames, float* out_ms, uint32_t capacity, uint32_t* count);
 
 /* ---- host-pointer convenience ------------------------------------------------------ */
 /*

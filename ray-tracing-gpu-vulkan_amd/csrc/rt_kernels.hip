@@ -1123,63 +1123,6 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
     // linear cell index and its per-axis steps (no multiplies in the loop)
     uint32_t cell = (uint32_t(cz) * G.n[1] + uint32_t(cy)) * G.n[0] + uint32_t(cx);
     const int dxc = sx, dyc = sy * int(G.n[0]), dzc = sz * int(G.n[0] * G.n[1]);
-#ifndef RT_L2_PREFETCH
-#define RT_L2_PREFETCH 0
-#endif
-    if constexpr (PAIRS && RT_L2_PREFETCH) {
-        // L2 grid: the next cell's offsets are loaded before this cell's references are tested
-        // (the DDA step does not depend on them; only whether it is taken does), so one dependent
-        // L2 round trip per cell step overlaps the reference tests
-        uint32_t b = cstart[cell], e = cstart[cell + 1];
-        for (;;) {
-            if (COUNT) {
-                n_cell++;
-                n_empty += b == e ? 1u : 0u;
-            }
-            const float tm = fminf(fminf(tx, ty), tz);
-            const bool mx = tx == tm, my = !mx && ty == tm, mz = !mx && !my;
-            const int ncx = cx + (mx ? sx : 0), ncy = cy + (my ? sy : 0), ncz = cz + (mz ? sz : 0);
-            const bool inside = uint32_t(ncx) < G.n[0] && uint32_t(ncy) < G.n[1] && uint32_t(ncz) < G.n[2];
-            const uint32_t ncell = cell + (mx ? dxc : my ? dyc : dzc);
-            uint32_t nb = 0u, ne = 0u;
-            if (inside) {
-                nb = cstart[ncell];
-                ne = cstart[ncell + 1];
-            }
-            uint32_t j = b;
-            for (; j + 1 < e; j += 2) {
-                UTIL(1, true);
-                const float4 s0 = rec[j], s1 = rec[j + 1];
-                const uint32_t i0 = ids[j], i1 = ids[j + 1];
-                test1<true>(s0, [&] { return i0; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
-                test1<true>(s1, [&] { return i1; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
-                if (COUNT) n_sph += 2;
-            }
-            if (j < e) {
-                UTIL(1, true);
-                const float4 s0 = rec[j];
-                const uint32_t i0 = ids[j];
-                test1<true>(s0, [&] { return i0; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
-                if (COUNT) n_sph++;
-            }
-            UTIL(0, true);
-            if (!(tm <= r.limit) || !inside) break;
-            cx = ncx;
-            cy = ncy;
-            cz = ncz;
-            cell = ncell;
-            b = nb;
-            e = ne;
-            const int c = mx ? cx : my ? cy : cz, sg = mx ? sx : my ? sy : sz;
-            const float2 cg = s_walk_par[mx ? 0 : my ? 1 : 2];   // (cs[k], gmin[k])
-            const float ok = mx ? r.o.x : my ? r.o.y : r.o.z, ik = mx ? r.inv.x : my ? r.inv.y : r.inv.z;
-            const float tnew = (__builtin_fmaf(float(c + (sg > 0 ? 1 : 0)), cg.x, cg.y) - ok) * ik;
-            tx = mx ? tnew : tx;
-            ty = my ? tnew : ty;
-            tz = mz ? tnew : tz;
-        }
-        return;
-    }
     for (;;) {
         const uint32_t b = cstart[cell], e = cstart[cell + 1];
         if (COUNT) {
@@ -1207,29 +1150,6 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
             ++j;
           }
         }
-#ifndef RT_LDS_IDPRE
-#define RT_LDS_IDPRE 0
-#endif
-#if RT_LDS_IDPRE
-        if (!PAIRS && j < e) {   // LDS: records and ids one ahead (past the run: the next cell's, or LDS beyond)
-            float4 A = rec[j], B;
-            uint32_t iA = ids[j], iB;
-            for (;;) {
-                UTIL(1, true);
-                B = rec[j + 1];
-                iB = ids[j + 1];
-                test1<true>(A, [&] { return iA; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
-                if (COUNT) n_sph++;
-                if (++j >= e) break;
-                UTIL(1, true);
-                A = rec[j + 1];
-                iA = ids[j + 1];
-                test1<true>(B, [&] { return iB; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
-                if (COUNT) n_sph++;
-                if (++j >= e) break;
-            }
-        }
-#else
         if (!PAIRS && j < e) {   // LDS: two records in flight, no register copies (unrolled by two)
             float4 A = rec[j], B;
             for (;;) {
@@ -1245,7 +1165,6 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
                 if (++j >= e) break;
             }
         }
-#endif
         UTIL(0, true);
         const float tm = fminf(fminf(tx, ty), tz);
         if (!(tm <= r.limit)) break;   // the next cell starts beyond every closer candidate

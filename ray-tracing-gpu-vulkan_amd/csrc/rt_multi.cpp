@@ -352,6 +352,24 @@ int rt_multi_kernel_times(rt_multi* m, float* out_ms, uint32_t capacity, uint32_
     return RT_OK;
 }
 
+int rt_multi_kernel_times_frames(rt_multi* m, uint32_t frames, float* out_ms, uint32_t capacity, uint32_t* count) {
+    if (!m || !count || (!out_ms && capacity)) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    std::vector<Launch*> ls;
+    for (Launch& l : m->launches)
+        if (!l.rows.empty()) ls.push_back(&l);
+    const uint32_t n = uint32_t(ls.size());
+    if (uint64_t(frames) * n > capacity) return fail(RT_ERR_INVALID_ARGUMENT, "capacity below frames x devices");
+    std::vector<float> t(frames);
+    for (uint32_t d = 0; d < n; d++) {
+        uint32_t got = 0;
+        if (int rc = rt_debug_kernel_times(ls[d]->ctx, t.data(), frames, &got)) return rc;
+        if (got < frames) return fail(RT_ERR_INVALID_ARGUMENT, "fewer launches recorded than frames asked");
+        for (uint32_t f = 0; f < frames; f++) out_ms[size_t(f) * n + d] = t[f];
+    }
+    *count = frames * n;
+    return RT_OK;
+}
+
 int rt_multi_stats(rt_multi* m, rt_stats* out) {
     if (!m || !out) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     std::memset(out, 0, sizeof(*out));

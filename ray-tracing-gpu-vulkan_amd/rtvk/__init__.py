@@ -327,12 +327,20 @@ class MultiRenderer:
         check(self._lib.rt_multi_info(self._m, v))
         return {"devices": int(v[0]), "rccl_ranks": int(v[1]), "strip_rows": int(v[2]), "launches": int(v[3])}
 
-    def kernel_times(self) -> list:
-        """Trace-kernel ms of the last frame on each device that rendered rows (device order)."""
-        buf = (ctypes.c_float * max(1, self.device_count))()
+    def kernel_times(self, frames: Optional[int] = None) -> list:
+        """Trace-kernel ms of the last frame on each device that rendered rows (device order); with
+        `frames`, a list of such lists for each of the last `frames` frames, oldest first."""
+        if frames is None:
+            buf = (ctypes.c_float * max(1, self.device_count))()
+            got = ctypes.c_uint32(0)
+            check(self._lib.rt_multi_kernel_times(self._m, buf, self.device_count, ctypes.byref(got)))
+            return [float(buf[i]) for i in range(got.value)]
+        cap = frames * self.device_count
+        buf = (ctypes.c_float * max(1, cap))()
         got = ctypes.c_uint32(0)
-        check(self._lib.rt_multi_kernel_times(self._m, buf, self.device_count, ctypes.byref(got)))
-        return [float(buf[i]) for i in range(got.value)]
+        check(self._lib.rt_multi_kernel_times_frames(self._m, frames, buf, cap, ctypes.byref(got)))
+        n = got.value // max(1, frames)
+        return [[float(buf[f * n + d]) for d in range(n)] for f in range(frames)]
 
     def stats(self) -> Stats:
         st = Stats()

@@ -119,6 +119,7 @@ EXPORTS = {
     "rt_multi_stats": (_I, [_P, ctypes.POINTER(Stats)]),
     "rt_multi_info": (_I, [_P, _P]),
     "rt_multi_kernel_times": (_I, [_P, _P, _U32, ctypes.POINTER(_U32)]),
+    "rt_multi_kernel_times_frames": (_I, [_P, _U32, _P, _U32, ctypes.POINTER(_U32)]),
     "rt_render": (_I, [_P, _U32, _P, _U32, _P, _P, ctypes.POINTER(Options), ctypes.POINTER(Stats)]),
     "rt_store_ppm": (_I, [ctypes.c_char_p, _P, _U32, _U32]),
     "rt_debug_math": (_I, [_I, _I, _P, _P, _U32]),

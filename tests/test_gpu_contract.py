@@ -189,6 +189,10 @@ def test_multi_renderer_reports_communicator(rtvk, torch, oracle):
         assert info["launches"] == min(n, (H + 7) // 8)
         kt = m.kernel_times()
         assert len(kt) == info["launches"] and all(k > 0 for k in kt)
+        m.render(rtvk.canonical_render_call_info(2, W, H), acc, out, options=rtvk.make_options(rng_mode=HASH))
+        kf = m.kernel_times(frames=2)   # per frame, per device, oldest first
+        assert len(kf) == 2 and all(len(f) == info["launches"] and all(k > 0 for k in f) for f in kf)
+        assert kf[0] == kt
         with pytest.raises((TypeError, ValueError)):
             bad = torch.zeros((H, W, 4), dtype=torch.float32, device="cpu")
             m.render(rtvk.canonical_render_call_info(2, W, H), bad, out)
