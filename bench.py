@@ -567,9 +567,9 @@ def main() -> int:
         frames = mr.kernel_times(min(64, args.steps))   # per timed frame, each device
         per_frame = [max(f) for f in frames if f]
         kernel_ms = sum(per_frame) / max(1, len(per_frame))
-        last = frames[-1] if frames else []
+        last_k = frames[-1] if frames else []
         k_basis = (f"mean over the {len(per_frame)} timed frames of the slowest device's trace kernel (HIP events "
-                   f"on each launch stream); last frame per device: {', '.join(f'{v:.2f}' for v in last)} ms")
+                   f"on each launch stream); last frame per device: {', '.join(f'{v:.2f}' for v in last_k)} ms")
     else:
         ks = []
         for sl in slots:
