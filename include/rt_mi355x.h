@@ -214,6 +214,9 @@ int rt_multi_set_scene(rt_multi* m, const Sphere* spheres, uint32_t count);
  * W*H texels. Asynchronous on `stream` (a hipStream_t of device 0; NULL = the legacy stream): the
  * call returns once everything is queued. The image equals the one-device image bit for bit.
  * With opt->accumulate each device adds to its own strips of the previous frame of the same size.
+ * One device holding every row renders straight into accum_rgba32f / out_rgba8 (no strip copy,
+ * no reorder); its running sum is then read back from the accum buffer the previous frame went
+ * to, which the caller leaves unchanged between the two frames.
  */
 int rt_multi_render(rt_multi* m, const RenderCallInfo* rci, const rt_options* opt,
                     float* accum_rgba32f, uint8_t* out_rgba8, void* stream);

@@ -7,8 +7,9 @@
 // round robin over the devices (interleaving balances sky-heavy and sphere-heavy rows without a
 // tuner), each device renders its strips through a rows map (global pixel seeds, so the image
 // does not depend on the device count), and one RCCL group moves every device's float4 + rgba8
-// strips to device 0 over xGMI (ncclSend / ncclRecv, device 0 to itself included), where one
-// kernel per source puts them in place (rt_scatter_rows). SURVEY.md §8(e).
+// strips to device 0 over xGMI (ncclSend / ncclRecv; device 0's own strips are not sent), where
+// one kernel per source puts them in place (rt_scatter_rows); a single device holding every row
+// renders straight into the caller's buffers. SURVEY.md §8(e).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -46,6 +47,10 @@ constexpr uint32_t kStrip = 8;   // rows per strip: one 8x8 pixel tile high, the
 struct Launch {
     uint32_t dev = 0;
     std::vector<uint32_t> rows;          // global rows, band order
+    bool whole = false;                  // device 0, every row in order (one device): may render
+                                         // straight into the caller's buffers
+    float* sum_at = nullptr;             // whole: the caller's accum buffer holding the running sum
+                                         // (last frame rendered straight into it), else the band
     rt_context* ctx = nullptr;           // on dev
     uint32_t* rows_dev = nullptr;        // rows on dev (the kernel's map)
     uint32_t* rows_root = nullptr;       // rows on device 0 (the scatter's map)
@@ -124,6 +129,8 @@ int set_partition(rt_multi* m, const std::string& key, uint32_t W, uint32_t H,
         Launch l;
         l.dev = p.first;
         l.rows = std::move(p.second);
+        l.whole = l.dev == 0 && l.rows.size() == H;
+        for (uint32_t y = 0; l.whole && y < H; y++) l.whole = l.rows[y] == y;
         m->launches.push_back(std::move(l));
     }
     for (Launch& l : m->launches) {
@@ -163,8 +170,9 @@ std::vector<std::pair<uint32_t, std::vector<uint32_t>>> strip_parts(uint32_t n, 
 // One RCCL group moves every other device's bands (float4 accumulator, then rgba8 image) to
 // device 0, then one kernel per band puts its rows in place in dst (device 0 pointers, W x H);
 // device 0's own bands go straight from its render buffers (no send to itself: at N = 1 the frame
-// moves no byte through RCCL). Everything on stream[0] after the group.
-int gather_to_root(rt_multi* m, float* dst_acc, uint8_t* dst_out) {
+// moves no byte through RCCL), and a band rendered into dst itself (`direct`) not at all.
+// Everything on stream[0] after the group.
+int gather_to_root(rt_multi* m, float* dst_acc, uint8_t* dst_out, bool direct) {
     const uint32_t W = m->W;
     RT_NCCL(ncclGroupStart());
     for (Launch& l : m->launches) {
@@ -188,7 +196,7 @@ int gather_to_root(rt_multi* m, float* dst_acc, uint8_t* dst_out) {
     }
     RT_NCCL(ncclGroupEnd());
     for (Launch& l : m->launches) {
-        if (l.rows.empty()) continue;
+        if (l.rows.empty() || (direct && l.whole)) continue;
         const bool own = l.dev == 0;   // rendered on stream[0] itself
         if (int rc = rt_scatter_rows(m->launches[0].ctx, own ? l.acc : l.stage_acc, own ? l.out : l.stage_out,
                                      l.rows_root, uint32_t(l.rows.size()), W, m->H, dst_acc, dst_out, m->stream[0]))
@@ -198,14 +206,17 @@ int gather_to_root(rt_multi* m, float* dst_acc, uint8_t* dst_out) {
 }
 
 // Launch i renders its rows with rcis[i] (offset replaced by the rows map) on its device's stream.
-int render_bands(rt_multi* m, const RenderCallInfo* rcis, size_t n_rci, const rt_options* opt) {
+// direct (dst_acc / dst_out on device 0, W x H): a `whole` launch renders into them, no map.
+int render_bands(rt_multi* m, const RenderCallInfo* rcis, size_t n_rci, const rt_options* opt, bool direct,
+                 float* dst_acc, uint8_t* dst_out) {
     for (size_t i = 0; i < m->launches.size(); i++) {
         Launch& l = m->launches[i];
         if (l.rows.empty()) continue;
         RenderCallInfo r = rcis[n_rci == 1 ? 0 : i];
         r.offset = rt_uvec2{0, 0};   // the rows map carries the global rows
-        if (int rc = rt_render_device(l.ctx, &r, l.rows_dev, m->W, uint32_t(l.rows.size()), l.acc, l.out, opt,
-                                      m->stream[l.dev]))
+        const bool d = direct && l.whole;
+        if (int rc = rt_render_device(l.ctx, &r, d ? nullptr : l.rows_dev, m->W, uint32_t(l.rows.size()),
+                                      d ? dst_acc : l.acc, d ? dst_out : l.out, opt, m->stream[l.dev]))
             return rc;
     }
     return RT_OK;
@@ -316,8 +327,20 @@ int rt_multi_render(rt_multi* m, const RenderCallInfo* rci, const rt_options* op
         RT_HIP(hipEventRecord(m->ev_in, st));
         for (uint32_t d = 0; d < m->n; d++) RT_HIP(hipStreamWaitEvent(m->stream[d], m->ev_in, 0));
     }
-    if (int rc = render_bands(m, rci, 1, opt)) return rc;
-    if (int rc = gather_to_root(m, accum, out)) return rc;
+    // One device holding every row renders straight into the caller's buffers (no band, no
+    // reorder). Its running sum then lives in that accum buffer: an accumulating frame into the
+    // same buffer adds to it there; into another buffer, the sum is copied into the band first.
+    Launch* w = m->launches.size() == 1 && m->launches[0].whole ? &m->launches[0] : nullptr;
+    const bool acc_mode = opt && opt->accumulate;
+    const bool direct = w && (!acc_mode || w->sum_at == accum);
+    if (w && !direct && w->sum_at) {
+        DeviceGuard g0(0);
+        RT_HIP(hipMemcpyAsync(w->acc, w->sum_at, w->rows.size() * size_t(W) * 16, hipMemcpyDeviceToDevice,
+                              m->stream[0]));
+    }
+    if (int rc = render_bands(m, rci, 1, opt, direct, accum, out)) return rc;
+    if (int rc = gather_to_root(m, accum, out, direct)) return rc;
+    if (w) w->sum_at = direct ? accum : nullptr;
     DeviceGuard g0(0);
     RT_HIP(hipEventRecord(m->ev_out, m->stream[0]));   // the caller's later work waits for it
     RT_HIP(hipStreamWaitEvent(st, m->ev_out, 0));
@@ -424,8 +447,8 @@ int rt_render(const Sphere* spheres, uint32_t sphere_count, const RenderCallInfo
         DeviceGuard g0(0);
         RT_HIP(hipMalloc(&dacc, size_t(W) * H * 16));
         RT_HIP(hipMalloc(&dout, size_t(W) * H * 4));
-        if (int rc = render_bands(m, rci, rci_count, opt)) return rc;   // each band its own RenderCallInfo
-        if (int rc = gather_to_root(m, dacc, dout)) return rc;
+        if (int rc = render_bands(m, rci, rci_count, opt, false, nullptr, nullptr)) return rc;   // each band its own RenderCallInfo
+        if (int rc = gather_to_root(m, dacc, dout, false)) return rc;
         RT_HIP(hipStreamSynchronize(m->stream[0]));
         RT_HIP(hipMemcpy(accum, dacc, size_t(W) * H * 16, hipMemcpyDeviceToHost));
         RT_HIP(hipMemcpy(out, dout, size_t(W) * H * 4, hipMemcpyDeviceToHost));

@@ -475,6 +475,32 @@ def test_multi_renderer_rccl(rtvk, torch, oracle, rng_mode):
             assert (st.segments, st.samples) == rs[:2]
 
 
+@pytest.mark.parametrize("rng_mode", [COUNTER, HASH])
+def test_multi_renderer_accumulate(rtvk, torch, oracle, rng_mode):
+    """rt_multi accumulation: each frame adds its samples (sample_base) to the previous frame's sum,
+    whether the previous frame went straight into the caller's buffer (one device holding every
+    row), the next one accumulates into that buffer or into another one (the sum then continues
+    from the launch's band), and again into the other one: every frame equals the oracle's."""
+    W, H = 40, 27
+    sc = oracle.generate_scene()
+    rci_np = oracle.render_call_info(2, W, H)
+    rci = rtvk.RenderCallInfo.from_buffer_copy(rci_np.tobytes())
+    bufs = [(torch.zeros((H, W, 4), dtype=torch.float32, device="cuda:0"),
+             torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda:0")) for _ in range(2)]
+    prev = None
+    with rtvk.MultiRenderer(8) as m:
+        m.set_scene(sc)
+        for k, b in enumerate([0, 0, 1, 1]):   # frame k into buffer pair b
+            acc, out = bufs[b]
+            m.render(rci, acc, out, options=rtvk.make_options(rng_mode=rng_mode, accumulate=k > 0,
+                                                               sample_base=2 * k))
+            torch.cuda.synchronize()
+            ra, ro, _ = oracle.render(sc, rci_np, W, H, accum=prev, opts=oracle.options(
+                rng_mode=rng_mode, accumulate=int(k > 0), sample_base=2 * k))
+            assert_same(acc.cpu().numpy(), out.cpu().numpy(), ra, ro)
+            prev = ra
+
+
 # ---- full size --------------------------------------------------------------------------------
 def test_full_frame_1spp_vs_oracle(rtvk, renderer, torch, oracle):
     """Config 1 frame (1920x1080, 1 spp) against the oracle: bit-exact => PSNR = inf >= 50 dB."""
