@@ -268,7 +268,8 @@ def config5_line(dev, steps: int, warmup: int, sha: str, count_spp: int = 20, or
     """BASELINE config 5 on this GPU: 3840x2160, 99 860 spheres (generateRandomScene grid 316x316),
     1 000 spp, the counter-based stream; every frame rebuilds the scene on the device (Morton LBVH +
     grid, rt_build.hip) as the reference rebuilds BLAS/TLAS, then renders it (grid walked from L2).
-    Timed like the headline (frames back to back between syncs); the trace kernel from the
+    Timed like the headline (frames back to back between syncs, after two untimed frames that
+    allocate both scene arenas); the trace kernel from the
     library's HIP events; image checks: a 64-row band through the default walk equals the LDS
     treelet walk bit for bit, and 4 blocks of the timed frame equal the CPU oracle bit for bit."""
     import numpy as np
@@ -799,7 +800,7 @@ def main() -> int:
                              "peak": VALU_FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                              "frac": round(bflops / (bms * 1e-3) / 1e12 / VALU_FP32_PEAK_TFLOPS, 4)}}
         if args.config == 3 and not args.no_config5 and (W, H, spp, grid) == CONFIGS[3][:4]:
-            result["config5"] = config5_line(dev, steps=3, warmup=1, sha=result["roofline"]["lib_sha256"])
+            result["config5"] = config5_line(dev, steps=5, warmup=2, sha=result["roofline"]["lib_sha256"])
     if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline and not args.profile:
         result["cpu_baseline"] = cpu_baseline(W, H, spp, grid, rng_mode, frame_np[0], frame_np[1], other=other_frame)
     if rank == 0:

@@ -48,8 +48,9 @@ struct BuildWorkspace {
     uint32_t* par_i = nullptr; uint32_t* par_l = nullptr;
     uint32_t* left = nullptr;  uint32_t* right = nullptr;
     uint32_t* lo = nullptr;    uint32_t* hi = nullptr;
-    uint32_t* flags = nullptr; uint32_t* cnt = nullptr; uint32_t* lcnt = nullptr;
+    uint32_t* cnt = nullptr; uint32_t* lcnt = nullptr;
     float4* bnd = nullptr;   // 2 per inner node: lo.xyz, hi.xyz
+    float4* pyr = nullptr;   // box pyramid over the sorted spheres (rt_build.hip k_leafbox / k_level)
     void* tmp = nullptr;     size_t tmp_bytes = 0;
     BuildSummary* S = nullptr;
 };

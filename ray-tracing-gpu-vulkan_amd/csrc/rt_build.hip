@@ -18,10 +18,14 @@
 //   karras    binary radix tree over the keys augmented by their position (Karras 2012,
 //             "Maximizing parallelism in the construction of BVHs, octrees, and k-d trees"):
 //             one thread per inner node finds its range and split by binary search
-//   bottomup  one thread per leaf climbs to the root; the second arrival at a node (agent-scope
-//             acq_rel counter: the 8 XCD L2s are not coherent) unions its children's boxes
-//             (exact float min/max) and counts emitted nodes / leaves of the cut tree (subtrees of
-//             <= 4 spheres become leaves)
+//   boxes     an inner node covers the sorted range [lo, hi], so its box is the union (exact
+//             float min / max) of the range's sphere boxes: a pyramid of unions over 64-sphere
+//             groups (leafbox + level), then 8 lanes per node read at most 2 x 63 entries per
+//             pyramid level. The cut tree (subtrees of <= 4 spheres become leaves) is counted the
+//             same way: each cut leaf marks its first sphere, a node's leaves are the marks in its
+//             range and its emitted nodes 2 leaves - 1. No atomics: the climb with an agent-scope
+//             counter per node it replaced paid an L2 writeback + invalidate per level (364 us at
+//             99 860 spheres; now 41 us: leafbox 6, levels 3 x 5, nodebox 20)
 //   emit      one thread per radix-tree node that survives the cut: depth-first position and leaf
 //             index by climbing to the root, then the padded + raw 32-B node (escape link) and
 //             its 4 dummy-padded leaf slots
@@ -59,6 +63,25 @@ __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
     return v;
 }
 
+// Block-wide max / min (kBlock threads, every thread calls): wave results through LDS, so a block
+// makes one device-scope atomic per summary field instead of one per wave. The summary fields are
+// single addresses every block updates; memory-side atomics on one address serialise (99 860
+// spheres: 1 560 waves x 8 fields took 143 us).
+template <bool MAX>
+__device__ __forceinline__ uint32_t block_reduce(uint32_t v) {
+    __shared__ uint32_t part[kBlock / 64];
+    v = MAX ? wave_max(v) : wave_min(v);
+    __syncthreads();   // part[] may still be read by the previous call
+    if (__lane_id() == 0) part[threadIdx.x >> 6] = v;
+    __syncthreads();
+    v = part[0];
+#pragma unroll
+    for (uint32_t w = 1; w < kBlock / 64; w++) v = MAX ? max(v, part[w]) : min(v, part[w]);
+    return v;
+}
+__device__ __forceinline__ uint32_t block_max(uint32_t v) { return block_reduce<true>(v); }
+__device__ __forceinline__ uint32_t block_min(uint32_t v) { return block_reduce<false>(v); }
+
 __global__ void k_init(BuildSummary* S, bool refit) {
     if (threadIdx.x) return;
     if (!refit) {
@@ -90,8 +113,8 @@ __global__ void __launch_bounds__(kBlock) k_prep(const Sphere* __restrict__ sph,
     } else if (i < n_geom) {   // brute-force pad record: never hit (rt_api.cpp)
         geom[i] = GeomRec{0.0f, 1e19f, 0.0f, -1e38f};
     }
-    Ro = wave_max(Ro);
-    if (__lane_id() == 0) atomicMax(&S->R_o, Ro);
+    Ro = block_max(Ro);
+    if (threadIdx.x == 0) atomicMax(&S->R_o, Ro);
 }
 
 // One wave: threshold and the big set from the descending radius order.
@@ -119,31 +142,33 @@ __global__ void k_select(const float* __restrict__ rdesc, const uint32_t* __rest
     }
 }
 
-// Centroid bounds (Morton frame) and largest radius of the spheres in the tree.
+// Centroid bounds (Morton frame) and largest / smallest radius of the spheres in the tree: a
+// grid-stride loop over kReduceBlocks blocks, block reductions, one atomic per field per block.
+constexpr uint32_t kReduceBlocks = 96;
 __global__ void __launch_bounds__(kBlock) k_reduce(const Sphere* __restrict__ sph, uint32_t n,
                                                    const uint8_t* __restrict__ is_big, bool refit,
                                                    BuildSummary* S) {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    const bool small = i < n && !is_big[i];
-    float c[3] = {0.0f, 0.0f, 0.0f};
-    float r = 0.0f;
-    if (small) {
+    uint32_t rmax = f2o(0.0f), rmin = f2o(INFINITY);
+    uint32_t cmin[3], cmax[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) { cmin[k] = f2o(INFINITY); cmax[k] = f2o(-INFINITY); }
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+        if (is_big[i]) continue;
         const rt_vec4 g = sph[i].geometry;
-        c[0] = g.x; c[1] = g.y; c[2] = g.z; r = g.w;
+        rmax = max(rmax, f2o(g.w));
+        rmin = min(rmin, f2o(g.w));
+        const float c[3] = {g.x, g.y, g.z};
+#pragma unroll
+        for (int k = 0; k < 3; k++) { cmin[k] = min(cmin[k], f2o(c[k])); cmax[k] = max(cmax[k], f2o(c[k])); }
     }
-    const uint32_t ro = wave_max(small ? f2o(r) : f2o(0.0f));
-    if (__lane_id() == 0) atomicMax(&S->rmax_o, ro);
-    const uint32_t rmo = wave_min(small ? f2o(r) : f2o(INFINITY));
-    if (__lane_id() == 0) atomicMin(&S->rmin_o, rmo);
+    rmax = block_max(rmax);
+    rmin = block_min(rmin);
+    if (threadIdx.x == 0) { atomicMax(&S->rmax_o, rmax); atomicMin(&S->rmin_o, rmin); }
     if (refit) return;   // the Morton frame belongs to the stored topology
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-        const uint32_t mn = wave_min(small ? f2o(c[k]) : f2o(INFINITY));
-        const uint32_t mx = wave_max(small ? f2o(c[k]) : f2o(-INFINITY));
-        if (__lane_id() == 0) {
-            atomicMin(&S->cmin_o[k], mn);
-            atomicMax(&S->cmax_o[k], mx);
-        }
+        const uint32_t mn = block_min(cmin[k]), mx = block_max(cmax[k]);
+        if (threadIdx.x == 0) { atomicMin(&S->cmin_o[k], mn); atomicMax(&S->cmax_o[k], mx); }
     }
 }
 
@@ -228,48 +253,126 @@ __device__ __forceinline__ void prim_box(const Sphere* __restrict__ sph, uint32_
     b[3] = g.x + g.w; b[4] = g.y + g.w; b[5] = g.z + g.w;   // traversal's gate computes it
 }
 
-__global__ void __launch_bounds__(kBlock) k_bottomup(const Sphere* __restrict__ sph,
-                                                     const uint32_t* __restrict__ sids, const BuildSummary* S,
-                                                     const uint32_t* __restrict__ par_i,
-                                                     const uint32_t* __restrict__ par_l,
-                                                     const uint32_t* __restrict__ left,
-                                                     const uint32_t* __restrict__ right,
-                                                     const uint32_t* __restrict__ lo,
-                                                     const uint32_t* __restrict__ hi, uint32_t* flags,
-                                                     float4* bnd, uint32_t* cnt, uint32_t* lcnt) {
+// Box pyramid over the m sorted spheres: level 0 = each sphere's box (lo.w = 1 when the sphere is
+// the first of its cut leaf, as uint bits), level k + 1 entry j = union of level-k entries
+// [64 j, 64 j + 64) (lo.w = their marks summed). kLevels levels hold up to 64^kLevels ... spheres
+// per top entry; a node reads the top level whole.
+constexpr uint32_t kLevels = 4;
+__host__ __device__ __forceinline__ uint32_t level_size(uint32_t n, uint32_t k) {
+    for (uint32_t i = 0; i < k; i++) n = (n + 63u) / 64u;
+    return n;
+}
+__host__ __device__ __forceinline__ size_t level_offset(uint32_t cap, uint32_t k) {   // in PBox (2 float4)
+    size_t off = 0;
+    for (uint32_t i = 0; i < k; i++) off += level_size(cap, i);
+    return off;
+}
+
+__global__ void __launch_bounds__(kBlock) k_leafbox(const Sphere* __restrict__ sph,
+                                                    const uint32_t* __restrict__ sids, const BuildSummary* S,
+                                                    const uint32_t* __restrict__ par_i,
+                                                    const uint32_t* __restrict__ par_l,
+                                                    const uint32_t* __restrict__ lo,
+                                                    const uint32_t* __restrict__ hi, float4* pyr) {
     const uint32_t m = S->n_small;
     const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
     if (m < 2 || p >= m) return;
-    uint32_t node = par_l[p];
-    for (uint32_t guard = 0; guard < kMaxDepth; guard++) {   // radix-tree depth <= 32 + 27
-        // Release this thread's writes (the child it finished) and acquire the sibling's.
-        const uint32_t old = __hip_atomic_fetch_add(&flags[node], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == 0u) return;
-        float b[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
-        uint32_t c = 1u, lc = 0u;
-        const uint32_t ch[2] = {left[node], right[node]};
+    float b[6];
+    prim_box(sph, sids[p], b);
+    // the cut leaf holding sphere p: its highest ancestor of <= kLeafMax spheres (the root has none)
+    uint32_t c = kPrim | p;
+    for (uint32_t guard = 0; guard < kMaxDepth; guard++) {
+        const uint32_t up = (c & kPrim) ? par_l[c & ~kPrim] : par_i[c];
+        if (hi[up] - lo[up] + 1u > kLeafMax) break;
+        c = up;
+        if (c == 0u) break;
+    }
+    const uint32_t first = (c & kPrim) ? (c & ~kPrim) : lo[c];
+    pyr[2 * size_t(p)] = make_float4(b[0], b[1], b[2], __uint_as_float(first == p ? 1u : 0u));
+    pyr[2 * size_t(p) + 1] = make_float4(b[3], b[4], b[5], 0.0f);
+}
+
+struct BoxAcc {
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+    uint32_t marks = 0;
+    __device__ __forceinline__ void add(const float4* __restrict__ e) {
+        const float4 a = e[0], z = e[1];
+        mn[0] = fminf(mn[0], a.x); mn[1] = fminf(mn[1], a.y); mn[2] = fminf(mn[2], a.z);
+        mx[0] = fmaxf(mx[0], z.x); mx[1] = fmaxf(mx[1], z.y); mx[2] = fmaxf(mx[2], z.z);
+        marks += __float_as_uint(a.w);
+    }
+    template <int LANES = 64>   // over aligned groups of LANES lanes
+    __device__ __forceinline__ void wave_reduce() {
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
-            float cb[6];
-            uint32_t cc, cl;
-            if (ch[k] & kPrim) {
-                prim_box(sph, sids[ch[k] & ~kPrim], cb);
-                cc = 1u; cl = 1u;
-            } else {
-                const float4 a = bnd[2 * ch[k]], e = bnd[2 * ch[k] + 1];
-                cb[0] = a.x; cb[1] = a.y; cb[2] = a.z; cb[3] = e.x; cb[4] = e.y; cb[5] = e.z;
-                cc = cnt[ch[k]]; cl = lcnt[ch[k]];
+        for (int s = LANES / 2; s >= 1; s >>= 1) {
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                mn[k] = fminf(mn[k], __shfl_xor(mn[k], s));
+                mx[k] = fmaxf(mx[k], __shfl_xor(mx[k], s));
             }
-            for (int q = 0; q < 3; q++) { b[q] = fminf(b[q], cb[q]); b[q + 3] = fmaxf(b[q + 3], cb[q + 3]); }
-            c += cc; lc += cl;
+            marks += (uint32_t)__shfl_xor((int)marks, s);
         }
-        const bool leafy = hi[node] - lo[node] + 1u <= kLeafMax;
-        bnd[2 * node] = make_float4(b[0], b[1], b[2], 0.0f);
-        bnd[2 * node + 1] = make_float4(b[3], b[4], b[5], 0.0f);
-        cnt[node] = leafy ? 1u : c;
-        lcnt[node] = leafy ? 1u : lc;
-        if (node == 0u) return;
-        node = par_i[node];
+    }
+};
+
+// Level k + 1 of the pyramid from level k: one wave per entry.
+__global__ void __launch_bounds__(kBlock) k_level(const BuildSummary* S, uint32_t cap, uint32_t k, float4* pyr) {
+    const uint32_t m = S->n_small;
+    const uint32_t j = (blockIdx.x * kBlock + threadIdx.x) >> 6, lane = __lane_id();
+    if (m < 2 || j >= level_size(m, k + 1)) return;   // wave-uniform
+    const float4* src = pyr + 2 * level_offset(cap, k);
+    const uint32_t n_src = level_size(m, k), e = 64u * j + lane;
+    BoxAcc acc;
+    if (e < n_src) acc.add(src + 2 * size_t(e));
+    acc.wave_reduce();
+    if (lane == 0) {
+        float4* dst = pyr + 2 * (level_offset(cap, k + 1) + j);
+        dst[0] = make_float4(acc.mn[0], acc.mn[1], acc.mn[2], __uint_as_float(acc.marks));
+        dst[1] = make_float4(acc.mx[0], acc.mx[1], acc.mx[2], 0.0f);
+    }
+}
+
+// Inner node i (kNodeLanes lanes): box = union over its sorted range, cut-tree counts from the
+// marks. The range [a, b) at level L splits into the entries before the next multiple of 64 and
+// after the last one (read here) and the 64-aligned middle, which is [a / 64, b / 64) at level
+// L + 1; at most 2 x 63 entries per level, the top level read whole. Most nodes span a few spheres:
+// 8 lanes per node (a wave per node took 104 us at 99 860 spheres, mostly idle lanes).
+constexpr uint32_t kNodeLanes = 8;
+__global__ void __launch_bounds__(kBlock) k_nodebox(const BuildSummary* S, uint32_t cap,
+                                                    const uint32_t* __restrict__ lo,
+                                                    const uint32_t* __restrict__ hi,
+                                                    const float4* __restrict__ pyr, float4* bnd, uint32_t* cnt,
+                                                    uint32_t* lcnt) {
+    const uint32_t m = S->n_small;
+    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t i = t / kNodeLanes, sub = t % kNodeLanes;
+    const bool live = m >= 2 && i < m - 1u;
+    BoxAcc acc;
+    uint32_t l0 = 0, h0 = 0;
+    if (live) {
+        l0 = lo[i];
+        h0 = hi[i];
+        uint32_t a = l0, b = h0 + 1u;
+        for (uint32_t L = 0; L < kLevels; L++) {
+            const float4* P = pyr + 2 * level_offset(cap, L);
+            if (b - a <= 128u || L + 1 == kLevels) {
+                for (uint32_t e = a + sub; e < b; e += kNodeLanes) acc.add(P + 2 * size_t(e));
+                break;
+            }
+            const uint32_t a1 = (a + 63u) & ~63u, b1 = b & ~63u;   // a1 < b1: b - a > 128
+            for (uint32_t e = a + sub; e < a1; e += kNodeLanes) acc.add(P + 2 * size_t(e));
+            for (uint32_t e = b1 + sub; e < b; e += kNodeLanes) acc.add(P + 2 * size_t(e));
+            a = a1 >> 6;
+            b = b1 >> 6;
+        }
+    }
+    acc.wave_reduce<kNodeLanes>();   // every lane: the groups' shuffles stay inside the group
+    if (live && sub == 0) {
+        const bool leafy = h0 - l0 + 1u <= kLeafMax;
+        bnd[2 * size_t(i)] = make_float4(acc.mn[0], acc.mn[1], acc.mn[2], 0.0f);
+        bnd[2 * size_t(i) + 1] = make_float4(acc.mx[0], acc.mx[1], acc.mx[2], 0.0f);
+        cnt[i] = leafy ? 1u : 2u * acc.marks - 1u;   // the cut subtree is a full binary tree
+        lcnt[i] = leafy ? 1u : acc.marks;
     }
 }
 
@@ -483,8 +586,8 @@ float summary_float(uint32_t o) {
 
 void build_release(BuildWorkspace& ws) {
     void* ptrs[] = {ws.rkeys, ws.rkeys_s, ws.ids, ws.ids_s, ws.keys, ws.keys_s, ws.sids, ws.is_big,
-                    ws.par_i, ws.par_l, ws.left, ws.right, ws.lo, ws.hi, ws.flags, ws.cnt, ws.lcnt,
-                    ws.bnd, ws.tmp, ws.S};
+                    ws.par_i, ws.par_l, ws.left, ws.right, ws.lo, ws.hi, ws.cnt, ws.lcnt,
+                    ws.bnd, ws.pyr, ws.tmp, ws.S};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     ws = BuildWorkspace{};
@@ -499,8 +602,8 @@ hipError_t build_reserve(BuildWorkspace& ws, uint32_t n) {
     RT_ALLOC(rkeys, c); RT_ALLOC(rkeys_s, c); RT_ALLOC(ids, c); RT_ALLOC(ids_s, c);
     RT_ALLOC(keys, c); RT_ALLOC(keys_s, c); RT_ALLOC(sids, c); RT_ALLOC(is_big, c);
     RT_ALLOC(par_i, c); RT_ALLOC(par_l, c); RT_ALLOC(left, c); RT_ALLOC(right, c);
-    RT_ALLOC(lo, c); RT_ALLOC(hi, c); RT_ALLOC(flags, c); RT_ALLOC(cnt, c); RT_ALLOC(lcnt, c);
-    RT_ALLOC(bnd, 2 * size_t(c)); RT_ALLOC(S, 1);
+    RT_ALLOC(lo, c); RT_ALLOC(hi, c); RT_ALLOC(cnt, c); RT_ALLOC(lcnt, c);
+    RT_ALLOC(bnd, 2 * size_t(c)); RT_ALLOC(pyr, 2 * level_offset(c, kLevels)); RT_ALLOC(S, 1);
 #undef RT_ALLOC
     if (e == hipSuccess) {
         size_t b1 = 0, b2 = 0;
@@ -541,7 +644,7 @@ hipError_t build_scene_gpu(BuildWorkspace& ws, const Sphere* sph, uint32_t n, co
             if (hipError_t e = hipMemsetAsync(ws.is_big, 0, n, st)) return e;
             k_select<<<1, 64, 0, st>>>(ws.rkeys_s, ws.ids_s, n, o.big_ids, ws.is_big, ws.S);
         }
-        k_reduce<<<blocks(n), kBlock, 0, st>>>(sph, n, ws.is_big, refit, ws.S);
+        k_reduce<<<std::min(blocks(n), kReduceBlocks), kBlock, 0, st>>>(sph, n, ws.is_big, refit, ws.S);
         if (!refit) {
             k_morton<<<blocks(n), kBlock, 0, st>>>(sph, n, ws.is_big, ws.S, ws.keys, ws.ids);
             size_t tb = ws.tmp_bytes;
@@ -551,9 +654,14 @@ hipError_t build_scene_gpu(BuildWorkspace& ws, const Sphere* sph, uint32_t n, co
             k_karras<<<blocks(n), kBlock, 0, st>>>(ws.keys_s, ws.S, ws.par_i, ws.par_l, ws.left, ws.right, ws.lo,
                                                   ws.hi);
         }
-        if (hipError_t e = hipMemsetAsync(ws.flags, 0, size_t(n) * 4, st)) return e;
-        k_bottomup<<<blocks(n), kBlock, 0, st>>>(sph, ws.sids, ws.S, ws.par_i, ws.par_l, ws.left, ws.right, ws.lo,
-                                                ws.hi, ws.flags, ws.bnd, ws.cnt, ws.lcnt);
+        // node boxes and cut-tree counts (kernels read the small count from the summary; grids
+        // sized for n, the excess exits)
+        k_leafbox<<<blocks(n), kBlock, 0, st>>>(sph, ws.sids, ws.S, ws.par_i, ws.par_l, ws.lo, ws.hi, ws.pyr);
+        constexpr uint32_t kWaves = kBlock / 64u;   // one wave per entry / node
+        for (uint32_t k = 0; k + 1 < kLevels; k++)
+            k_level<<<(level_size(n, k + 1) + kWaves - 1) / kWaves, kBlock, 0, st>>>(ws.S, ws.cap, k, ws.pyr);
+        k_nodebox<<<(uint64_t(n) * kNodeLanes + kBlock - 1) / kBlock, kBlock, 0, st>>>(ws.S, ws.cap, ws.lo, ws.hi,
+                                                                                      ws.pyr, ws.bnd, ws.cnt, ws.lcnt);
         k_emit<<<blocks(2 * n), kBlock, 0, st>>>(sph, ws.sids, ws.S, ws.par_i, ws.par_l, ws.left, ws.lo, ws.hi,
                                                 ws.bnd, ws.cnt, ws.lcnt, o.nodes, o.nodes_raw, o.leaf_geom,
                                                 o.leaf_ids);
