@@ -87,7 +87,7 @@ def records(oracle, centers, radii, t=0.0):
     return rec
 
 
-@pytest.mark.parametrize("t,K", [(0.0, 11), (1.3, 11), (0.0, 1), (0.0, 2), (0.5, 40), (0.0, 158)])
+@pytest.mark.parametrize("t,K", [(0.0, 11), (1.3, 11), (0.0, 1), (0.0, 2), (0.5, 40), (0.0, 158), (0.0, 363)])
 def test_device_tree_equals_host_tree(renderer, oracle, t, K):
     sc = oracle.generate_scene(t, K)
     host, dev = build_both(renderer, sc)
@@ -118,6 +118,20 @@ def test_device_tree_edge_cases(renderer, oracle, case):
         c = np.zeros((129, 3), np.float32)
         c[:, 0] = np.linspace(-10, 10, 129)
         r = np.full(129, 0.05, np.float32)
+    host, dev = build_both(renderer, records(oracle, c, r))
+    assert_trees_equal(host, dev)
+
+
+@pytest.mark.parametrize("n", [126, 127, 128, 129, 130, 4095, 4097, 8193, 8320])
+def test_device_tree_box_pyramid_sizes(renderer, oracle, n):
+    """Node boxes and cut-tree counts come from a pyramid of 64-sphere unions (rt_build.hip
+    k_nodebox): scenes whose small-sphere counts straddle the pyramid's group and range limits
+    (128 entries read whole, 64-aligned splits, 64^2 groups) build the host tree bit for bit. K = 363
+    above (527 080 spheres) reaches the pyramid's top level."""
+    rng = np.random.default_rng(n)
+    c = rng.uniform(-20, 20, (n, 3)).astype(np.float32)
+    c[:, 1] = rng.uniform(0, 0.5, n)
+    r = rng.uniform(0.05, 0.25, n).astype(np.float32)
     host, dev = build_both(renderer, records(oracle, c, r))
     assert_trees_equal(host, dev)
 
