@@ -432,8 +432,9 @@ def test_hash_tail_steals(rtvk, renderer, torch, oracle):
 @pytest.mark.parametrize("rng_mode", [STREAM, HASH])
 def test_host_rt_render_bands(rtvk, oracle, rng_mode):
     """rt_render with 3 contiguous bands (one per GPU in the reference, src/ray_trace.cpp:74-93;
-    here band i on device i % n), gathered to device 0 by one RCCL group (sends to itself on a
-    one-GPU box) and copied to the host: equals the one-device frame; then accumulate on top."""
+    here band i on device i % n), gathered to device 0 by one RCCL group (device 0's bands go
+    straight from its buffers) and copied to the host: equals the one-device frame; then
+    accumulate on top."""
     W, H = 32, 20
     sc = oracle.generate_scene()
     rcis = [rtvk.canonical_render_call_info(2, W, H) for _ in range(3)]
@@ -454,9 +455,10 @@ def test_host_rt_render_bands(rtvk, oracle, rng_mode):
 @pytest.mark.parametrize("rng_mode", [STREAM, HASH])
 def test_multi_renderer_rccl(rtvk, torch, oracle, rng_mode):
     """rt_multi (one process, every visible GPU up to 8, one RCCL communicator): 8-row strips
-    dealt round robin, each device's strips sent to device 0 (itself included) in one RCCL group
-    and reordered there; two frames (the second with the LPT order) equal the one-device oracle
-    frame bit for bit, and the statistics are summed over the devices."""
+    dealt round robin, every other device's strips sent to device 0 in one RCCL group and
+    reordered there (one device holding every row renders straight into the caller's buffers);
+    two frames (the second with the LPT order) equal the one-device oracle frame bit for bit, and
+    the statistics are summed over the devices."""
     W, H, spp = 72, 43, 3
     sc = oracle.generate_scene()
     rci_np = oracle.render_call_info(spp, W, H)
