@@ -173,20 +173,56 @@ __device__ __forceinline__ float4 lds_reload(const float4* p) {
 }
 
 // Launch parameters that a lane selects per lane, staged in LDS by every walk kernel before its
-// first barrier (stage_walk_params): the grid's (cell size, origin) per axis for the DDA step and
-// the two absolute cull slacks. Read with a per-lane LDS address (lgkmcnt wait only) instead of
-// the compiler's per-lane select of kernel-argument addresses and a global load, whose
-// vmcnt(0) wait also waited for every store and atomic the wave had in flight.
-__shared__ float2 s_walk_par[4];   // (cs[k], gmin[k]) k = 0..2, (cull_near_abs, cull_abs)
+// first barrier (stage_walk_params): per grid axis the DDA step's (cell size, origin, linear cell
+// stride, cell count), one 16-B load per step, and the two absolute cull slacks. Read with a
+// per-lane LDS address (lgkmcnt wait only) instead of the compiler's per-lane select of
+// kernel-argument addresses and a global load, whose vmcnt(0) wait also waited for every store
+// and atomic the wave had in flight; and the stride and count from the table instead of per-step
+// integer multiplies and a scalar reload of a kernel argument that the SGPR budget evicted
+// (config 3 -3.1 %, reference stream -2.9 %, config 5 -1.3 %).
+__shared__ float4 s_walk_axis[3];   // (cs[k], gmin[k], stride[k], n[k]): stride and n as uint bits
+__shared__ float2 s_walk_slack;     // (cull_near_abs, cull_abs)
+#ifdef RT_CAM_LDS
+__shared__ float s_cam[18];          // lf, hor, ver, ulc, cup, crt (camera_ray)
+#endif
 __device__ __forceinline__ void stage_walk_params(const rt::TraceParams& P, uint32_t tid) {
-    if (tid < 3u) s_walk_par[tid] = make_float2(P.grid.cs[tid], P.grid.gmin[tid]);
-    if (tid == 3u) s_walk_par[3] = make_float2(P.cull_near_abs, P.cull_abs);
+#ifdef RT_CAM_LDS
+    if (tid >= 32u && tid < 50u) s_cam[tid - 32u] = P.lf[tid - 32u];   // the six vectors are contiguous
+#endif
+    if (tid < 3u) {
+        const uint32_t stride = tid == 0u ? 1u : tid == 1u ? P.grid.n[0] : P.grid.n[0] * P.grid.n[1];
+        s_walk_axis[tid] = make_float4(P.grid.cs[tid], P.grid.gmin[tid], __uint_as_float(stride),
+                                       __uint_as_float(P.grid.n[tid]));
+    }
+    if (tid == 3u) s_walk_slack = make_float2(P.cull_near_abs, P.cull_abs);
+}
+
+// One DDA step of the grid walks: the axis whose boundary comes first (x before y before z on
+// ties; tm = the smallest boundary t). Only the stepped coordinate can leave the grid (false:
+// the ray left). The new boundary's t is recomputed from the cell coordinate, never accumulated.
+__device__ __forceinline__ bool dda_step(float tm, float& tx, float& ty, float& tz, int& cx, int& cy, int& cz,
+                                         int sx, int sy, int sz, uint32_t& cell, V3 o, V3 inv) {
+    const bool mx = tx == tm, my = !mx && ty == tm, mz = !mx && !my;
+    const float4 ax = s_walk_axis[mx ? 0 : my ? 1 : 2];
+    const int s = mx ? sx : my ? sy : sz;
+    const int c = (mx ? cx : my ? cy : cz) + s;
+    if (uint32_t(c) >= __float_as_uint(ax.w)) return false;
+    cx = mx ? c : cx;
+    cy = my ? c : cy;
+    cz = mz ? c : cz;
+    cell = s > 0 ? cell + __float_as_uint(ax.z) : cell - __float_as_uint(ax.z);
+    const float ok = mx ? o.x : my ? o.y : o.z, ik = mx ? inv.x : my ? inv.y : inv.z;
+    const float tnew = (__builtin_fmaf(float(c + (s > 0 ? 1 : 0)), ax.x, ax.y) - ok) * ik;
+    tx = mx ? tnew : tx;
+    ty = my ? tnew : ty;
+    tz = mz ? tnew : tz;
+    return true;
 }
 
 // Cull limit of a closest-so-far t: best + cull_abs + cull_rel best, with
 // the smaller absolute slack of grid walks for t <= cull_near_t (rt_api.cpp; -1 elsewhere).
 __device__ __forceinline__ float cull_limit(const rt::TraceParams& P, float t) {
-    const float* slack = reinterpret_cast<const float*>(&s_walk_par[3]);
+    const float* slack = reinterpret_cast<const float*>(&s_walk_slack);
     const float abs_slack = slack[t <= P.cull_near_t ? 0 : 1];
     return fminf(__builtin_fmaf(t, P.cull_rel, t + abs_slack), 10000.0f);
 }
@@ -674,8 +710,21 @@ __device__ __forceinline__ void camera_ray(const rt::TraceParams& P, const Camer
         rx = nan ? __builtin_nanf("") : __uint_as_float(sa ^ (__float_as_uint(lxr) & 0x80000000u));
         ry = nan ? __builtin_nanf("") : __uint_as_float(sa ^ (__float_as_uint(lyr) & 0x80000000u));
     }
+#ifdef RT_CAM_LDS
+    (void)cam;
+    auto cv = [](int i) { return v3(s_cam[3 * i], s_cam[3 * i + 1], s_cam[3 * i + 2]); };
+    V3 from;
+    if (P.pinhole_lf) {   // wave-uniform: lf + (+-0 + +-0) = lf, or NaN when the lens sample was (0, 0)
+        const float nanf = __builtin_nanf("");
+        from = (rx != rx) ? v3(nanf, nanf, nanf) : cv(0);
+    } else {
+        from = add(cv(0), add(scale(rx, cv(5)), scale(ry, cv(4))));
+    }
+    const V3 to = sub(add(cv(3), scale(ux, cv(1))), scale(uy, cv(2)));
+#else
     const V3 from = add(cam.lf, add(scale(rx, cam.crt), scale(ry, cam.cup)));
     const V3 to = sub(add(cam.ulc, scale(ux, cam.hor)), scale(uy, cam.ver));
+#endif
     o = from;
     v = sub(to, from);
     ps.thr = v3(1.0f, 1.0f, 1.0f);
@@ -864,7 +913,13 @@ constexpr uint32_t kTraceBlock = RT_TRACE_BLOCK;   // one block per CU shares on
 template <bool COUNT, int MODE>
 __global__ __launch_bounds__(kBruteBlock, RT_BRUTE_WAVES_PER_SIMD) void rt_trace_brute_kernel(const rt::TraceParams P) {
     const uint32_t lane = lane_id();
+#ifdef RT_CAM_LDS
+    stage_walk_params(P, threadIdx.x);
+    __syncthreads();
+    const Camera cam{};
+#else
     const Camera cam = load_camera(P);
+#endif
     uint32_t st = ST_NEED_UNIT;
     Path ps{};
     V3 o = v3(0, 0, 0), d = v3(0, 0, 1);
@@ -1120,9 +1175,8 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
     float tx = bound_t(cx, sx, 0, r.o.x, r.inv.x);
     float ty = bound_t(cy, sy, 1, r.o.y, r.inv.y);
     float tz = bound_t(cz, sz, 2, r.o.z, r.inv.z);
-    // linear cell index and its per-axis steps (no multiplies in the loop)
+    // linear cell index (a step adds the stepped axis's stride, dda_step)
     uint32_t cell = (uint32_t(cz) * G.n[1] + uint32_t(cy)) * G.n[0] + uint32_t(cx);
-    const int dxc = sx, dyc = sy * int(G.n[0]), dzc = sz * int(G.n[0] * G.n[1]);
     for (;;) {
         const uint32_t b = cstart[cell], e = cstart[cell + 1];
         if (COUNT) {
@@ -1168,20 +1222,7 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
         UTIL(0, true);
         const float tm = fminf(fminf(tx, ty), tz);
         if (!(tm <= r.limit)) break;   // the next cell starts beyond every closer candidate
-        // step the axis whose boundary comes first (x before y before z on ties), branch-free
-        const bool mx = tx == tm, my = !mx && ty == tm, mz = !mx && !my;
-        cx += mx ? sx : 0;
-        cy += my ? sy : 0;
-        cz += mz ? sz : 0;
-        if (uint32_t(cx) >= G.n[0] || uint32_t(cy) >= G.n[1] || uint32_t(cz) >= G.n[2]) break;
-        cell += mx ? dxc : my ? dyc : dzc;
-        const int c = mx ? cx : my ? cy : cz, s = mx ? sx : my ? sy : sz;
-        const float2 cg = s_walk_par[mx ? 0 : my ? 1 : 2];   // (cs[k], gmin[k])
-        const float ok = mx ? r.o.x : my ? r.o.y : r.o.z, ik = mx ? r.inv.x : my ? r.inv.y : r.inv.z;
-        const float tnew = (__builtin_fmaf(float(c + (s > 0 ? 1 : 0)), cg.x, cg.y) - ok) * ik;
-        tx = mx ? tnew : tx;
-        ty = my ? tnew : ty;
-        tz = mz ? tnew : tz;
+        if (!dda_step(tm, tx, ty, tz, cx, cy, cz, sx, sy, sz, cell, r.o, r.inv)) break;
     }
 }
 
@@ -1234,7 +1275,6 @@ __device__ __forceinline__ void grid_walk_cq(const rt::TraceParams& P, const uin
     float ty = bound_t(cy, sy, 1, r.o.y, r.inv.y);
     float tz = bound_t(cz, sz, 2, r.o.z, r.inv.z);
     uint32_t cell = (uint32_t(cz) * G.n[1] + uint32_t(cy)) * G.n[0] + uint32_t(cx);
-    const int dxc = sx, dyc = sy * int(G.n[0]), dzc = sz * int(G.n[0] * G.n[1]);
     const uint32_t lane = lane_id();
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     uint32_t* const q = s_cq_q + wave * kCqCap;
@@ -1320,19 +1360,7 @@ __device__ __forceinline__ void grid_walk_cq(const rt::TraceParams& P, const uin
         UTIL(0, true);
         const float tm = fminf(fminf(tx, ty), tz);
         if (!(tm <= r.limit)) break;   // the next cell starts beyond every closer candidate
-        const bool mx = tx == tm, my = !mx && ty == tm, mz = !mx && !my;
-        cx += mx ? sx : 0;
-        cy += my ? sy : 0;
-        cz += mz ? sz : 0;
-        if (uint32_t(cx) >= G.n[0] || uint32_t(cy) >= G.n[1] || uint32_t(cz) >= G.n[2]) break;
-        cell += mx ? dxc : my ? dyc : dzc;
-        const int cc = mx ? cx : my ? cy : cz, s = mx ? sx : my ? sy : sz;
-        const float2 cg = s_walk_par[mx ? 0 : my ? 1 : 2];   // (cs[k], gmin[k])
-        const float ok = mx ? r.o.x : my ? r.o.y : r.o.z, ik = mx ? r.inv.x : my ? r.inv.y : r.inv.z;
-        const float tnew = (__builtin_fmaf(float(cc + (s > 0 ? 1 : 0)), cg.x, cg.y) - ok) * ik;
-        tx = mx ? tnew : tx;
-        ty = my ? tnew : ty;
-        tz = mz ? tnew : tz;
+        if (!dda_step(tm, tx, ty, tz, cx, cy, cz, sx, sy, sz, cell, r.o, r.inv)) break;
     }
 }
 
@@ -1478,22 +1506,7 @@ __device__ __forceinline__ void grid_walk_coop(const rt::TraceParams& P, const u
             if (!(tm <= r.limit)) {
                 walking = false;   // the next cell starts beyond every closer candidate
             } else {
-                const bool mx = tx == tm, my = !mx && ty == tm, mz = !mx && !my;
-                cx += mx ? sx : 0;
-                cy += my ? sy : 0;
-                cz += mz ? sz : 0;
-                if (uint32_t(cx) >= G.n[0] || uint32_t(cy) >= G.n[1] || uint32_t(cz) >= G.n[2]) {
-                    walking = false;
-                } else {
-                    cell += mx ? sx : my ? sy * int(G.n[0]) : sz * int(G.n[0] * G.n[1]);
-                    const int c = mx ? cx : my ? cy : cz, sg = mx ? sx : my ? sy : sz;
-                    const float2 cg = s_walk_par[mx ? 0 : my ? 1 : 2];   // (cs[k], gmin[k])
-                    const float ok = mx ? r.o.x : my ? r.o.y : r.o.z, ik = mx ? r.inv.x : my ? r.inv.y : r.inv.z;
-                    const float tnew = (__builtin_fmaf(float(c + (sg > 0 ? 1 : 0)), cg.x, cg.y) - ok) * ik;
-                    tx = mx ? tnew : tx;
-                    ty = my ? tnew : ty;
-                    tz = mz ? tnew : tz;
-                }
+                walking = dda_step(tm, tx, ty, tz, cx, cy, cz, sx, sy, sz, cell, r.o, r.inv);
             }
         }
     }
@@ -1661,7 +1674,11 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
                           (LAYOUT == LAYOUT_GRID || LAYOUT == LAYOUT_GRID_L2 || LAYOUT == LAYOUT_GRID_COOP ||
                            LAYOUT == LAYOUT_GRID_CQ);
     const uint32_t lane = lane_id();
+#ifdef RT_CAM_LDS
+    const Camera cam{};   // camera_ray reads the LDS copy
+#else
     const Camera cam = load_camera(P);
+#endif
     uint32_t st = ST_NEED_UNIT;
     Path ps{};
     Ray r{};
