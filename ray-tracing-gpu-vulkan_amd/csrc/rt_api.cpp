@@ -325,11 +325,6 @@ void fill_camera(const RenderCallInfo& rci, rt::TraceParams& P) {
     auto put = [](float* d, F3 v) { d[0] = v.x; d[1] = v.y; d[2] = v.z; };
     put(P.lf, from); put(P.hor, hor); put(P.ver, ver); put(P.ulc, ulc); put(P.cup, cup); put(P.crt, right);
     P.half_aperture = aperture / 2.0f;
-    // Pinhole: the lens offsets are +-0 (or NaN, rt_kernels.hip camera_ray), so the origin is lf
-    // exactly when every lf component is nonzero and finite and crt, cup are finite
-    auto fin = [](F3 v) { return std::isfinite(v.x) && std::isfinite(v.y) && std::isfinite(v.z); };
-    P.pinhole_lf = (P.half_aperture == 0.0f && fin(from) && from.x != 0.0f && from.y != 0.0f && from.z != 0.0f &&
-                    fin(right) && fin(cup)) ? 1u : 0u;
     P.size_x = sx;
     P.size_y = sy;
     P.inv_size_x = 1.0 / double(sx);

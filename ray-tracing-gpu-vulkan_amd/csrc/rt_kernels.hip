@@ -182,13 +182,7 @@ __device__ __forceinline__ float4 lds_reload(const float4* p) {
 // (config 3 -3.1 %, reference stream -2.9 %, config 5 -1.3 %).
 __shared__ float4 s_walk_axis[3];   // (cs[k], gmin[k], stride[k], n[k]): stride and n as uint bits
 __shared__ float2 s_walk_slack;     // (cull_near_abs, cull_abs)
-#ifdef RT_CAM_LDS
-__shared__ float s_cam[18];          // lf, hor, ver, ulc, cup, crt (camera_ray)
-#endif
 __device__ __forceinline__ void stage_walk_params(const rt::TraceParams& P, uint32_t tid) {
-#ifdef RT_CAM_LDS
-    if (tid >= 32u && tid < 50u) s_cam[tid - 32u] = P.lf[tid - 32u];   // the six vectors are contiguous
-#endif
     if (tid < 3u) {
         const uint32_t stride = tid == 0u ? 1u : tid == 1u ? P.grid.n[0] : P.grid.n[0] * P.grid.n[1];
         s_walk_axis[tid] = make_float4(P.grid.cs[tid], P.grid.gmin[tid], __uint_as_float(stride),
@@ -710,21 +704,8 @@ __device__ __forceinline__ void camera_ray(const rt::TraceParams& P, const Camer
         rx = nan ? __builtin_nanf("") : __uint_as_float(sa ^ (__float_as_uint(lxr) & 0x80000000u));
         ry = nan ? __builtin_nanf("") : __uint_as_float(sa ^ (__float_as_uint(lyr) & 0x80000000u));
     }
-#ifdef RT_CAM_LDS
-    (void)cam;
-    auto cv = [](int i) { return v3(s_cam[3 * i], s_cam[3 * i + 1], s_cam[3 * i + 2]); };
-    V3 from;
-    if (P.pinhole_lf) {   // wave-uniform: lf + (+-0 + +-0) = lf, or NaN when the lens sample was (0, 0)
-        const float nanf = __builtin_nanf("");
-        from = (rx != rx) ? v3(nanf, nanf, nanf) : cv(0);
-    } else {
-        from = add(cv(0), add(scale(rx, cv(5)), scale(ry, cv(4))));
-    }
-    const V3 to = sub(add(cv(3), scale(ux, cv(1))), scale(uy, cv(2)));
-#else
     const V3 from = add(cam.lf, add(scale(rx, cam.crt), scale(ry, cam.cup)));
     const V3 to = sub(add(cam.ulc, scale(ux, cam.hor)), scale(uy, cam.ver));
-#endif
     o = from;
     v = sub(to, from);
     ps.thr = v3(1.0f, 1.0f, 1.0f);
@@ -913,13 +894,7 @@ constexpr uint32_t kTraceBlock = RT_TRACE_BLOCK;   // one block per CU shares on
 template <bool COUNT, int MODE>
 __global__ __launch_bounds__(kBruteBlock, RT_BRUTE_WAVES_PER_SIMD) void rt_trace_brute_kernel(const rt::TraceParams P) {
     const uint32_t lane = lane_id();
-#ifdef RT_CAM_LDS
-    stage_walk_params(P, threadIdx.x);
-    __syncthreads();
-    const Camera cam{};
-#else
     const Camera cam = load_camera(P);
-#endif
     uint32_t st = ST_NEED_UNIT;
     Path ps{};
     V3 o = v3(0, 0, 0), d = v3(0, 0, 1);
@@ -1674,11 +1649,7 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
                           (LAYOUT == LAYOUT_GRID || LAYOUT == LAYOUT_GRID_L2 || LAYOUT == LAYOUT_GRID_COOP ||
                            LAYOUT == LAYOUT_GRID_CQ);
     const uint32_t lane = lane_id();
-#ifdef RT_CAM_LDS
-    const Camera cam{};   // camera_ray reads the LDS copy
-#else
     const Camera cam = load_camera(P);
-#endif
     uint32_t st = ST_NEED_UNIT;
     Path ps{};
     Ray r{};
