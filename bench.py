@@ -359,6 +359,99 @@ def config5_line(dev, steps: int, warmup: int, sha: str, count_spp: int = 20, or
     return res
 
 
+def animated_line(dev, W: int, H: int, spp: int, grid: int, rng_mode: int, frames: int = 5,
+                  dt: float = 1.0 / 60.0) -> dict:
+    """The reference's frame loop (src/ray_trace.cpp:579-582, :741-745): every frame regenerates the
+    scene at its own t (generateRandomScene, src/scene.h:79-157: spheres 1-3 move with t,
+    :94-111), rebuilds the acceleration structure and renders; t advances 1/60 s per frame. The
+    tile hand-out order (LPT) of each frame comes from the previous, different frame. One untimed
+    frame (t = -1/60) first, then `frames` timed frames from t = 0; the last one is checked against
+    the oracle on 4 blocks of pixels."""
+    import numpy as np
+    import torch
+
+    import rtvk
+    r = rtvk.Renderer(dev.index)
+    stream = torch.cuda.Stream(device=dev)
+    opts = rtvk.make_options(accel=rtvk.abi.RT_ACCEL_LBVH, rng_mode=rng_mode)
+    rci = rtvk.canonical_render_call_info(spp, W, H)
+    acc = torch.zeros((H, W, 4), dtype=torch.float32, device=dev)
+    out = torch.zeros((H, W, 4), dtype=torch.uint8, device=dev)
+
+    def frame(t):
+        sc = rtvk.generateRandomScene(t, grid)   # host generation inside the loop, as the reference
+        with torch.cuda.stream(stream):
+            r.set_scene(sc, stream=stream)
+            r.render_device(rci, acc, out, options=opts, stream=stream)
+
+    frame(-dt)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(frames):
+        frame(k * dt)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    ks = r.kernel_times(frames)
+    t_last = (frames - 1) * dt
+    res = {"workload": f"BASELINE config 3 frames ({W}x{H}, {spp} spp) of the reference's animated loop: "
+                       f"scene regenerated at t = k/60 s, structure rebuilt, LPT order from the previous frame",
+           "value": round(W * H * spp * frames / elapsed / 1e6, 2), "unit": "Msamples/s", "frames": frames,
+           "ms_per_step": round(elapsed / frames * 1e3, 3), "kernel_ms": round(sum(ks) / max(1, len(ks)), 3),
+           "t_s": [round(k * dt, 4) for k in range(frames)]}
+    from oracle import oracle
+    oracle.build()
+    sc = oracle.generate_scene(t_last, grid)
+    a_np, o_np = acc.cpu().numpy(), out.cpu().numpy()
+    same_a = same_o = True
+    nb, bh, bw = 4, 2, 8
+    t1 = time.perf_counter()
+    for y, x in zip(np.linspace(0, H - bh, nb).round().astype(int), np.linspace(0, W - bw, nb).round().astype(int)):
+        rows = np.arange(y, y + bh, dtype=np.uint32)
+        oa, oo, _ = oracle.render(sc, oracle.render_call_info(spp, W, H, (int(x), 0)), bw, bh, rows=rows,
+                                  opts=oracle.options(rng_mode=rng_mode), threads=host_cpus()["threads"])
+        same_a &= bool(np.array_equal(a_np[y:y + bh, x:x + bw], oa))
+        same_o &= bool(np.array_equal(o_np[y:y + bh, x:x + bw], oo))
+    res["oracle_check"] = {"t": t_last, "pixels": nb * bh * bw, "accum_bit_exact": same_a, "rgba8_equal": same_o,
+                           "cpu_s": round(time.perf_counter() - t1, 2)}
+    r.close()
+    return res
+
+
+def cold_call_line(W: int, H: int, spp: int, timeout_s: int = 300) -> dict:
+    """One cold call of the drop-in entry point, ray_trace(spp, false, W, H, 1) (src/ray_trace.h:9-15),
+    in a fresh child process with the counter-based stream (RT_RNG=hash, the headline's): HIP
+    runtime start, the RCCL communicator, the context, the canonical scene's build, one frame
+    without LPT history, the resolve and the teardown. `call_s` is the wall time around the call;
+    `frame_ms` is the frame time the library itself prints (duration_per_frame)."""
+    import re
+    import subprocess
+    from rtvk import abi
+    code = ("import ctypes, sys, time\n"
+            "lib = ctypes.CDLL(sys.argv[1])\n"
+            "lib.ray_trace.argtypes = [ctypes.c_uint32, ctypes.c_bool, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]\n"
+            "lib.ray_trace.restype = None\n"
+            "t = time.perf_counter()\n"
+            "lib.ray_trace(int(sys.argv[2]), False, int(sys.argv[3]), int(sys.argv[4]), 1)\n"
+            "dt = time.perf_counter() - t\n"
+            "sys.stdout.flush()\n"
+            "print('CALL_S', dt, flush=True)\n")
+    env = dict(os.environ, RT_RNG="hash")
+    t0 = time.perf_counter()
+    p = subprocess.run([sys.executable, "-c", code, str(abi.LIB_PATH), str(spp), str(W), str(H)], env=env,
+                       capture_output=True, text=True, timeout=timeout_s)
+    proc_s = time.perf_counter() - t0
+    call = re.search(r"CALL_S ([0-9.eE+-]+)", p.stdout)
+    fr = re.search(r"duration_per_frame: ([0-9.]+) ms", p.stdout)
+    if p.returncode != 0 or not call or not fr:
+        return {"error": f"exit {p.returncode}", "stdout": p.stdout[-400:], "stderr": p.stderr[-400:]}
+    call_s, frame_ms = float(call.group(1)), float(fr.group(1))
+    return {"call_s": round(call_s, 4), "frame_ms": round(frame_ms, 3), "setup_s": round(call_s - frame_ms / 1e3, 4),
+            "child_process_s": round(proc_s, 3),
+            "value": round(W * H * spp / call_s / 1e6, 2), "unit": "Msamples/s",
+            "what": f"ray_trace({spp}, false, {W}, {H}, 1) in a fresh process, RT_RNG=hash: HIP start, RCCL "
+                    "communicator, context, scene build, first frame (no LPT history), resolve, teardown"}
+
+
 def env_knobs() -> dict:
     """RT_* variables of this process. The library reads only RT_RNG (ray_trace(), not this bench's
     path) and RT_BVH_BUILD; rtvk reads RT_LIB (another library); bench.py reads RT_BENCH_BACKEND
@@ -422,7 +515,7 @@ def main() -> int:
 
     import rtvk
     from rtvk import abi
-    from rtvk.dist import DistributedRenderer, hip_assembler, hip_band_renderer
+    from rtvk.dist import DistributedRenderer, hip_assembler, hip_band_renderer, hip_resolver, strip_rows
 
     launched = "WORLD_SIZE" in os.environ
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -524,7 +617,8 @@ def main() -> int:
                 self.stream = torch.cuda.Stream(device=dev)
                 with torch.cuda.stream(self.stream):
                     self.dr = DistributedRenderer(W, H, dev, hip_band_renderer(self.renderer, rci, opts),
-                                                  hip_assembler(self.renderer))
+                                                  hip_assembler(self.renderer),
+                                                  resolve=hip_resolver(self.renderer, spp))
                 self.launches = 0
 
             def frame(self):
@@ -564,10 +658,12 @@ def main() -> int:
     elapsed = time.perf_counter() - t0
     # trace-kernel durations inside the timed region (HIP events the library records around the
     # kernel on its launch stream; rt_debug_kernel_times)
+    per_device_ms = None   # N > 1: mean trace-kernel ms of the timed frames per device / rank
     if mode == "multi":
         frames = mr.kernel_times(min(64, args.steps))   # per timed frame, each device
         per_frame = [max(f) for f in frames if f]
         kernel_ms = sum(per_frame) / max(1, len(per_frame))
+        per_device_ms = [sum(f[d] for f in frames) / len(frames) for d in range(len(frames[0]))] if frames else []
         last_k = frames[-1] if frames else []
         k_basis = (f"mean over the {len(per_frame)} timed frames of the slowest device's trace kernel (HIP events "
                    f"on each launch stream); last frame per device: {', '.join(f'{v:.2f}' for v in last_k)} ms")
@@ -590,7 +686,14 @@ def main() -> int:
             k_basis = (f"mean trace-kernel duration of 3 frames rendered one at a time after the timed region "
                        f"(HIP events on the launch stream); the timed region had {len(slots)} frames in flight")
     if mode == "per-process":
-        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+        # every rank's kernel time (the reference records per-GPU durations and the row split of
+        # every benchmark window, src/ray_trace.cpp:750-760), then the max over ranks
+        cdev = dev if backend == "nccl" else torch.device("cpu")
+        mine = torch.tensor([kernel_ms], dtype=torch.float64, device=cdev)
+        allk = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allk, mine)
+        per_device_ms = [float(v.item()) for v in allk]
+        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kernel_ms = float(t[0].item()), float(t[1].item())
         k_basis += f"; max over {world} ranks"
@@ -735,6 +838,14 @@ def main() -> int:
                 "what": "gathered N-GPU frame vs the same frame rendered by one GPU (same seeds, same stream)"}
             result["rccl_ranks"] = multi_info["rccl_ranks"] if mode == "multi" else world
             r1.close()
+            if per_device_ms:
+                mean = sum(per_device_ms) / len(per_device_ms)
+                result["per_device_kernel_ms"] = [round(v, 3) for v in per_device_ms]
+                result["imbalance"] = round(max(per_device_ms) / mean, 4) if mean > 0 else None
+                result["rows_per_device"] = [len(strip_rows(r, n_gpus, H)) for r in range(n_gpus)]
+                result["imbalance_basis"] = ("max / mean over devices of each device's mean trace-kernel ms over "
+                                             "the timed frames (HIP events on its launch stream); rows_per_device: "
+                                             "8-row strips dealt round robin")
         if n_gpus == 1:
             frame_np = (fa.cpu().numpy(), fo.cpu().numpy())
     # Side lines (single GPU): the same frame with the other random stream and with the LBVH walk
@@ -801,6 +912,15 @@ def main() -> int:
                              "frac": round(bflops / (bms * 1e-3) / 1e12 / VALU_FP32_PEAK_TFLOPS, 4)}}
         if args.config == 3 and not args.no_config5 and (W, H, spp, grid) == CONFIGS[3][:4]:
             result["config5"] = config5_line(dev, steps=5, warmup=2, sha=result["roofline"]["lib_sha256"])
+        if args.config == 3 and (W, H, spp, grid) == CONFIGS[3][:4] and accel != abi.RT_ACCEL_BRUTE:
+            # the reference's animated loop and one cold drop-in call, beside the warm static frames
+            result["animated"] = animated_line(dev, W, H, spp, grid, rng_mode)
+            result["animated"]["vs_headline"] = round(result["animated"]["value"] / result["value"], 4)
+            cold = cold_call_line(W, H, spp)
+            if "value" in cold:
+                cold["vs_headline"] = round(cold["value"] / result["value"], 4)
+            result["ray_trace_call"] = cold
+            result["ray_trace_call_s"] = cold.get("call_s")
     if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline and not args.profile:
         result["cpu_baseline"] = cpu_baseline(W, H, spp, grid, rng_mode, frame_np[0], frame_np[1], other=other_frame)
     if rank == 0:

@@ -188,6 +188,14 @@ int rt_scatter_rows(rt_context* ctx, const float* src_accum, const uint8_t* src_
                     float* dst_accum, uint8_t* dst_rgba8, void* stream);
 
 /*
+ * Gather full-image rows into a band on the device: dst_row[i] = src_row[rows[i]] (the inverse
+ * of rt_scatter_rows: the running sums an accumulating multi-GPU frame hands each device). src
+ * has src_rows rows of `width` float4 texels; map entries >= src_rows leave their band row as is.
+ */
+int rt_gather_rows(rt_context* ctx, const float* src_accum, const uint32_t* rows, uint32_t n_rows,
+                   uint32_t width, uint32_t src_rows, float* dst_accum, void* stream);
+
+/*
  * Tonemap a summed accumulator to rgba8 on the device, exactly as the trace kernel's store
  * (shader.rgen:65-66): rgba8 = round(clamp(sqrt(sum / spp), 0, 1) * 255) per channel, alpha 255.
  * accum_rgba32f: n_texels float4 (DEVICE); out_rgba8: n_texels x 4 bytes (DEVICE).
@@ -209,14 +217,18 @@ int rt_multi_set_scene(rt_multi* m, const Sphere* spheres, uint32_t count);
 /*
  * One frame of the whole image rci->image_size (rci->offset ignored). The rows are cut into
  * 8-row strips, strip k rendered by device k % n (rt_render_device with a rows map, global
- * seeds); every device's strips travel to device 0 in one RCCL group (ncclSend / ncclRecv, device
- * 0 included) and are reordered into accum_rgba32f / out_rgba8: DEVICE pointers on device 0,
- * W*H texels. Asynchronous on `stream` (a hipStream_t of device 0; NULL = the legacy stream): the
- * call returns once everything is queued. The image equals the one-device image bit for bit.
- * With opt->accumulate each device adds to its own strips of the previous frame of the same size.
- * One device holding every row renders straight into accum_rgba32f / out_rgba8 (no strip copy,
- * no reorder); its running sum is then read back from the accum buffer the previous frame went
- * to, which the caller leaves unchanged between the two frames.
+ * seeds); every other device's float4 accumulator strips travel to device 0 in one RCCL group
+ * (ncclSend / ncclRecv; device 0's own strips never go through RCCL) and are reordered into
+ * accum_rgba32f, then device 0 tonemaps the whole accumulator into out_rgba8 (rt_resolve_rgba8:
+ * the rgba8 bytes are a function of the float sum, so they are not sent). accum_rgba32f /
+ * out_rgba8: DEVICE pointers on device 0, W*H texels. Asynchronous on `stream` (a hipStream_t of
+ * device 0; NULL = the legacy stream): the call returns once everything is queued. The image
+ * equals the one-device image bit for bit.
+ * opt->accumulate: as rt_render_device, the frame adds to what accum_rgba32f holds when the call's
+ * work starts on `stream`, at every device count (device 0 sends each device the running sums of
+ * its strips first). One device holding every row renders straight into the caller's buffers (no
+ * strip copy, no reorder, no resolve). The frame plan is rt_debug_multi_plan's
+ * (include/rt_mi355x_debug.h).
  */
 int rt_multi_render(rt_multi* m, const RenderCallInfo* rci, const rt_options* opt,
                     float* accum_rgba32f, uint8_t* out_rgba8, void* stream);
@@ -246,74 +258,10 @@ int rt_render(const Sphere* spheres, uint32_t sphere_count, const RenderCallInfo
 /* Writes an rgba8 image as binary PPM (P6, alpha dropped). */
 int rt_store_ppm(const char* path, const uint8_t* rgba8, uint32_t width, uint32_t height);
 
-/* Diagnostic (tests only): evaluates one arithmetic-contract primitive on `device` for n
- * (x, y) pairs: op 0 sqrt(x), 1 x/y, 2 sin(x), 3 fma(x,y,1), 4 normalize(x,y,0.5).x, 5 pow(x,5),
- * 6 sample_seed_hash(bits(x), bits(y)) as bits, 7 / 8 low / high word of the 8.24 fixed-point
- * value of colour x, as bits, 9 checker decision at (x, y, 0.5 (x - y)) as 1 / 0. */
-int rt_debug_math(int device, int op, const float* in_pairs, float* out, uint32_t n);
-/* Diagnostic (tests only): the kernels' cheap correctly rounded operations against hipcc's
- * correctly rounded ones on `device`: rcp_cr(x) vs 1.0f / x and sqrt_cr(x) vs sqrtf(x) over all 2^32
- * binary32 inputs (mismatches3[0], [1]; NaN == NaN), and the camera's float(double(x) * (1 /
- * double(b))) vs x / b for every binary32 x in [0, 65536) and eleven image sizes b (mismatches3[2]). */
-int rt_debug_exact_exhaustive(int device, uint64_t* mismatches3);
-/* Durations (ms) of the trace kernel of ctx's most recent launches (at most 64 are kept), oldest
- * first, from HIP events recorded on the launch stream around the kernel itself (not the resolve):
- * a caller times K launches inside its own timed region and reads them afterwards. *count =
- * min(capacity, launches kept). Synchronises on those events. */
-int rt_debug_kernel_times(rt_context* ctx, float* out_ms, uint32_t capacity, uint32_t* count);
 /* Build provenance of this library: "sources_sha256=<16 hex of the sources it was compiled
  * from>;arch=<offload arch>;flags=<compiler flags>;variant=<A/B variant flags, empty for the
  * shipped build>". Static string. */
 const char* rt_build_info(void);
-/* Diagnostic (tests, A/B timing): sets one launch-plan parameter of ctx (value -1 restores the
- * default). None of them changes an image; the defaults are the measured best. Keys: "grid" (0: no
- * uniform grid), "grid_scale", "grid_coop" (1: wave-cooperative grid walk), "grid_cq" (1: wave-wide
- * candidate queue), "grid_rec" (0: no
- * shading records in LDS), "grid_full_slack", "units_per_lane", "unit_min_samples",
- * "sample_chunks", "head_chunks", "tail_tiles_pm", "schedule" (0 LPT, 1 row-major, 2 LPT by tile
- * sum), "refill_reserve", "isolate_tiles", "sah_knobs". Unknown keys: RT_ERR_INVALID_ARGUMENT.
- * Scene-build keys (grid, grid_scale, sah_knobs) apply from the next rt_set_scene. The library
- * reads no environment variable for any of them. */
-int rt_debug_tune(rt_context* ctx, const char* key, double value);
-/* Diagnostic: of ctx's last launch, {sample chunks per pixel (low 16 bits: of the LPT order's tail
- * tiles; high 16 bits: of its head tiles, 0 when the launch had no head), the kernel form it ran
- * (rt_internal.h ACCEL_*; before any launch: the scene's default form), its dynamic LDS bytes, CU
- * count}. */
-int rt_debug_launch_info(rt_context* ctx, uint32_t* out4);
-/* Diagnostic: per-phase cycle sums of ctx's last launch, filled only by -DRT_STAMPS builds. */
-int rt_debug_stamps(rt_context* ctx, uint64_t* out8);
-/* Diagnostic: lane utilisation of ctx's last launch per kernel code point k (0..15), filled only by
- * -DRT_UTIL builds: out32[2k] wave passes through the point, out32[2k + 1] active lanes summed. */
-int rt_debug_util(rt_context* ctx, uint64_t* out32);
-/* Diagnostic: histogram of LBVH box tests per segment of the last instrumented launch
- * (options.reserved[0] & 1), 2 x 64 bins: [0] segments that miss, [1] segments that hit. */
-int rt_debug_walk_hist(rt_context* ctx, uint64_t* out128);
-/* Diagnostic: walk work (cells + references) of ctx's last instrumented launch per segment pass,
-   max over the wave's tracing lanes [0] and over its bounce (depth > 0) lanes [1], summed over
-   passes; the primary (depth 0) lanes' summed work [2] and their count [3]. */
-int rt_debug_walk_split(rt_context* ctx, uint64_t* out4);
-/* Diagnostic: of ctx's last instrumented launch of a grid walk, {cells visited, visited cells that
- * hold no reference}. */
-int rt_debug_grid_cells(rt_context* ctx, uint64_t* out2);
-/* Diagnostic: segment-loop iterations of the last instrumented launch by the number of lanes
- * (0..64) of the wave tracing in that iteration (the persistent kernel's lane occupancy), then
- * three s_memrealtime stamps (100 MHz): first wave start, pixel queue dry, last wave exit. */
-int rt_debug_lane_hist(rt_context* ctx, uint64_t* out68);
-/* Diagnostic: tail steals of ctx's last instrumented launch (options.reserved[0] & 1;
- * RT_RNG_SAMPLE_HASH: once the work queue is empty, an idle lane takes half of the samples its
- * wave's busiest lane has not started). */
-int rt_debug_steals(rt_context* ctx, uint64_t* out);
-/* Diagnostic: per 8x8 tile of ctx's last LBVH launch, the traced segments of its most expensive
- * pixel (the key its next launch over the same band geometry hands tiles out by, longest
- * first); *count = tiles (ceil(W/8) x ceil(H/8), row-major), 0 before the first launch. */
-int rt_debug_tile_cost(rt_context* ctx, uint32_t* out, uint64_t capacity, uint64_t* count);
-
-/* Diagnostic (tests): copies one scene array of ctx to host memory. what: 0 geometry records,
- * 1 radii, 2 material records, 3 big-sphere ids, 4 LBVH nodes (padded), 5 LBVH nodes (unpadded),
- * 6 leaf geometry, 7 leaf ids, 8 info {u32 n_spheres, n_big, n_nodes, n_leaf_slots,
- * device_built, 0; f32 small_rmax, scene_radius}. *bytes = the array's size; RT_ERR_INVALID_ARGUMENT
- * when it exceeds capacity. */
-int rt_debug_scene(rt_context* ctx, uint32_t what, void* out, uint64_t capacity, uint64_t* bytes);
 
 /* src/ray_trace.h:9-15 — identical symbol and parameter list. Renders the canonical scene once
  * (t = 0) on min(gpu_count, visible) GPUs through rt_multi (8-row strips, RCCL gather, global

@@ -15,10 +15,12 @@
 #include <memory>
 #include <random>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/rt_abi.h"
 #include "../../include/rt_mi355x.h"
+#include "../../include/rt_mi355x_debug.h"
 #include "rt_build.h"
 #include "rt_bvh.h"
 #include "rt_grid.h"
@@ -37,6 +39,8 @@ uint32_t block_size(uint32_t accel);
 hipError_t launch_scatter_rows(const float* src_acc, const uint8_t* src_px, const uint32_t* rows,
                                uint32_t n_rows, uint32_t width, uint32_t dst_rows, float* dst_acc, uint8_t* dst_px,
                                hipStream_t st);
+hipError_t launch_gather_rows(const float* src_acc, const uint32_t* rows, uint32_t n_rows, uint32_t width,
+                              uint32_t src_rows, float* dst_acc, hipStream_t st);
 hipError_t launch_debug_math(int op, const float* in, float* out, uint32_t n, hipStream_t st);
 hipError_t launch_debug_exact(unsigned long long* bad, hipStream_t st);
 }  // namespace rt
@@ -98,10 +102,20 @@ struct rt_context {
     float* big_tab = nullptr;                    // device, in the counters' allocation (TraceParams::big_tab)
     // Every device operation of a context (scene upload / build, render) is ordered after the
     // previous one, whatever streams they are issued on: an op on a stream other than the last
-    // one first waits for `ev_last`, and every op records it when issued.
+    // one first waits for `ev_last`, and every op records it when issued. A device build runs on
+    // the build stream beside the previous op (it waits only for the launches that read its
+    // arena), so it does not cover that op: the op's event moves to `ev_prev`,
+    // which the next op waits for as well (order_on) until an op issued after both clears it.
     hipStream_t last_stream = nullptr;
     hipEvent_t ev_last = nullptr;
     bool ev_valid = false;
+    hipStream_t prev_stream = nullptr;
+    hipEvent_t ev_prev = nullptr;
+    bool prev_valid = false;
+    // the build workspace (ws) holds the topology of a full build that completed: a refit may
+    // reuse it (a full build that failed after overwriting ws leaves it false)
+    bool topo_ok = false;
+    bool pending_refit = false;
     // occupancy cache per kernel form, count flag and rng mode, valid for occ_lds bytes
     int occ[rt::ACCEL_COUNT][2][2] = {};
     size_t occ_lds[rt::ACCEL_COUNT][2][2] = {};
@@ -229,13 +243,37 @@ void size_lds_forms(rt_context* ctx) {
 // Stream chaining of a context's device operations (rt_context::ev_last).
 int order_on(rt_context* ctx, hipStream_t st) {
     if (ctx->ev_valid && ctx->last_stream != st) RT_HIP(hipStreamWaitEvent(st, ctx->ev_last, 0));
+    if (ctx->prev_valid && ctx->prev_stream != st) RT_HIP(hipStreamWaitEvent(st, ctx->ev_prev, 0));
     return RT_OK;
 }
+// After an op issued on `st` behind order_on(ctx, st): it follows everything before it.
 int mark_issued(rt_context* ctx, hipStream_t st) {
     if (!ctx->ev_last) RT_HIP(hipEventCreateWithFlags(&ctx->ev_last, hipEventDisableTiming));
     RT_HIP(hipEventRecord(ctx->ev_last, st));
     ctx->ev_valid = true;
     ctx->last_stream = st;
+    ctx->prev_valid = false;
+    return RT_OK;
+}
+// After a device build on the build stream, which did not wait for the previous op: the build's
+// event becomes ev_last and the previous op's event is kept in ev_prev (unless the previous op
+// was itself a build, whose own ev_prev then still stands).
+int mark_built(rt_context* ctx) {
+    if (ctx->ev_valid && ctx->last_stream != ctx->build_stream) {
+        std::swap(ctx->ev_last, ctx->ev_prev);
+        ctx->prev_valid = true;
+        ctx->prev_stream = ctx->last_stream;
+    }
+    if (!ctx->ev_last) RT_HIP(hipEventCreateWithFlags(&ctx->ev_last, hipEventDisableTiming));
+    RT_HIP(hipEventRecord(ctx->ev_last, ctx->build_stream));
+    ctx->ev_valid = true;
+    ctx->last_stream = ctx->build_stream;
+    return RT_OK;
+}
+// Host wait for every op issued so far (statistics and diagnostic readers).
+int sync_issued(rt_context* ctx) {
+    if (ctx->ev_valid) RT_HIP(hipEventSynchronize(ctx->ev_last));
+    if (ctx->prev_valid) RT_HIP(hipEventSynchronize(ctx->ev_prev));
     return RT_OK;
 }
 
@@ -496,6 +534,7 @@ int rt_context_destroy(rt_context* ctx) {
         if (ctx->stage_ev[k]) (void)hipEventDestroy(ctx->stage_ev[k]);
     }
     if (ctx->ev_last) (void)hipEventDestroy(ctx->ev_last);
+    if (ctx->ev_prev) (void)hipEventDestroy(ctx->ev_prev);
     for (auto& pr : ctx->kev)
         for (hipEvent_t e : pr)
             if (e) (void)hipEventDestroy(e);
@@ -727,6 +766,7 @@ int device_build_begin(rt_context* ctx, const Sphere* spheres, uint32_t count, b
     if (int rc = slot_reserve(ctx, s, count)) return rc;
     if (int rc = stage_spheres(ctx, spheres, count, device_ptr, st)) return rc;
     rt::DeviceScene& d = s.scene;
+    if (!refit) ctx->topo_ok = false;   // the build overwrites the workspace's topology
     if (refit)   // the big set is the topology's (a refit does not re-select it)
         RT_HIP(hipMemcpyAsync(d.big_ids, ctx->slot[ctx->slot_cur].scene.big_ids, 64 * 4, hipMemcpyDeviceToDevice, bs));
     const rt::BuildOutputs o{d.geom, d.radius, d.mat, d.big_ids, d.nodes, d.nodes_raw, d.leaf_geom, d.leaf_ids};
@@ -738,6 +778,7 @@ int device_build_begin(rt_context* ctx, const Sphere* spheres, uint32_t count, b
     ctx->pending = true;
     ctx->pending_slot = k;
     ctx->pending_count = count;
+    ctx->pending_refit = refit;
     return RT_OK;
 }
 
@@ -797,6 +838,7 @@ int device_build_end(rt_context* ctx) {
     }
     ctx->scene = d;
     ctx->slot_cur = k;
+    if (!ctx->pending_refit) ctx->topo_ok = true;   // ws now holds the current arena's topology
     ctx->gpu_tree = true;
     ctx->treelet_stale = true;
     ctx->nodes_host.clear();
@@ -853,7 +895,7 @@ int scene_begin(rt_context* ctx, const Sphere* spheres, uint32_t count, bool dev
         }
     }
     return device_build_begin(ctx, spheres, count, device_ptr, st, refit && ctx->gpu_tree && ctx->slot_cur >= 0 &&
-                                                                       count == ctx->scene.n_spheres &&
+                                                                       ctx->topo_ok && count == ctx->scene.n_spheres &&
                                                                        ctx->ws.topo_n == count);
 }
 
@@ -861,7 +903,7 @@ int scene_end(rt_context* ctx) {
     if (!ctx->pending) return RT_OK;
     DeviceGuard g(ctx->device);
     if (int rc = device_build_end(ctx)) return rc;
-    return mark_issued(ctx, ctx->build_stream);   // the next operation waits for the build
+    return mark_built(ctx);   // the next operation waits for the build and for the op before it
 }
 
 }  // namespace
@@ -1280,7 +1322,7 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
 int rt_get_stats(rt_context* ctx, rt_stats* out) {
     if (!ctx || !out) return fail(RT_ERR_INVALID_ARGUMENT, "ctx or out is NULL");
     DeviceGuard g(ctx->device);
-    if (ctx->ev_valid) RT_HIP(hipEventSynchronize(ctx->ev_last));
+    if (int rc = sync_issued(ctx)) return rc;
     rt::Counters c;
     RT_HIP(hipMemcpy(&c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
     out->segments = c.segments;
@@ -1313,12 +1355,22 @@ int rt_scatter_rows(rt_context* ctx, const float* src_accum, const uint8_t* src_
     return RT_OK;
 }
 
+int rt_gather_rows(rt_context* ctx, const float* src_accum, const uint32_t* rows, uint32_t n_rows, uint32_t width,
+                   uint32_t src_rows, float* dst_accum, void* stream) {
+    if (!ctx || !rows) return fail(RT_ERR_INVALID_ARGUMENT, "ctx or rows is NULL");
+    if (n_rows && width && (!src_accum || !dst_accum)) return fail(RT_ERR_INVALID_ARGUMENT, "accum is NULL");
+    DeviceGuard g(ctx->device);
+    RT_HIP(rt::launch_gather_rows(src_accum, rows, n_rows, width, src_rows, dst_accum,
+                                  static_cast<hipStream_t>(stream)));
+    return RT_OK;
+}
+
 // Diagnostic export: per-code-point lane utilisation of the last launch (RT_UTIL builds; zeros
 // otherwise).
 int rt_debug_util(rt_context* ctx, uint64_t* out32) {
     if (!ctx || !out32) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     DeviceGuard g(ctx->device);
-    if (ctx->ev_valid) RT_HIP(hipEventSynchronize(ctx->ev_last));
+    if (int rc = sync_issued(ctx)) return rc;
     rt::Counters c;
     RT_HIP(hipMemcpy(&c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
     for (int k = 0; k < 32; k++) out32[k] = c.util[k];
@@ -1329,7 +1381,7 @@ int rt_debug_util(rt_context* ctx, uint64_t* out32) {
 int rt_debug_stamps(rt_context* ctx, uint64_t* out8) {
     if (!ctx || !out8) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     DeviceGuard g(ctx->device);
-    if (ctx->ev_valid) RT_HIP(hipEventSynchronize(ctx->ev_last));
+    if (int rc = sync_issued(ctx)) return rc;
     rt::Counters c;
     RT_HIP(hipMemcpy(&c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
     for (int k = 0; k < 8; k++) out8[k] = c.stamp[k];
@@ -1344,7 +1396,7 @@ int rt_debug_tile_cost(rt_context* ctx, uint32_t* out, uint64_t capacity, uint64
     if (!sc.valid || !out) return RT_OK;   // size query
     if (capacity < sc.n) return fail(RT_ERR_INVALID_ARGUMENT, "capacity");
     DeviceGuard g(ctx->device);
-    if (ctx->ev_valid) RT_HIP(hipEventSynchronize(ctx->ev_last));
+    if (int rc = sync_issued(ctx)) return rc;
     RT_HIP(hipMemcpy(out, sc.cost[sc.cur ^ 1], size_t(sc.n) * 4, hipMemcpyDeviceToHost));
     return RT_OK;
 }
@@ -1352,7 +1404,7 @@ int rt_debug_tile_cost(rt_context* ctx, uint32_t* out, uint64_t capacity, uint64
 int rt_debug_lane_hist(rt_context* ctx, uint64_t* out68) {
     if (!ctx || !out68) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     DeviceGuard g(ctx->device);
-    if (ctx->ev_valid) RT_HIP(hipEventSynchronize(ctx->ev_last));
+    if (int rc = sync_issued(ctx)) return rc;
     rt::Counters c;
     RT_HIP(hipMemcpy(&c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
     std::memcpy(out68, c.lane_hist, sizeof(c.lane_hist));
@@ -1365,7 +1417,7 @@ int rt_debug_lane_hist(rt_context* ctx, uint64_t* out68) {
 int rt_debug_steals(rt_context* ctx, uint64_t* out) {
     if (!ctx || !out) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     DeviceGuard g(ctx->device);
-    if (ctx->ev_valid) RT_HIP(hipEventSynchronize(ctx->ev_last));
+    if (int rc = sync_issued(ctx)) return rc;
     rt::Counters c;
     RT_HIP(hipMemcpy(&c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
     *out = c.steals;
@@ -1377,7 +1429,7 @@ int rt_debug_steals(rt_context* ctx, uint64_t* out) {
 int rt_debug_walk_split(rt_context* ctx, uint64_t* out4) {
     if (!ctx || !out4) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     DeviceGuard g(ctx->device);
-    if (ctx->ev_valid) RT_HIP(hipEventSynchronize(ctx->ev_last));
+    if (int rc = sync_issued(ctx)) return rc;
     rt::Counters c;
     RT_HIP(hipMemcpy(&c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
     std::memcpy(out4, c.walk_split, sizeof(c.walk_split));
@@ -1389,7 +1441,7 @@ int rt_debug_walk_split(rt_context* ctx, uint64_t* out4) {
 int rt_debug_grid_cells(rt_context* ctx, uint64_t* out2) {
     if (!ctx || !out2) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     DeviceGuard g(ctx->device);
-    if (ctx->ev_valid) RT_HIP(hipEventSynchronize(ctx->ev_last));
+    if (int rc = sync_issued(ctx)) return rc;
     rt::Counters c;
     RT_HIP(hipMemcpy(&c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
     out2[0] = c.box_tests;
@@ -1401,7 +1453,7 @@ int rt_debug_grid_cells(rt_context* ctx, uint64_t* out2) {
 int rt_debug_walk_hist(rt_context* ctx, uint64_t* out128) {
     if (!ctx || !out128) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     DeviceGuard g(ctx->device);
-    if (ctx->ev_valid) RT_HIP(hipEventSynchronize(ctx->ev_last));
+    if (int rc = sync_issued(ctx)) return rc;
     rt::Counters c;
     RT_HIP(hipMemcpy(&c, ctx->counters, sizeof(c), hipMemcpyDeviceToHost));
     std::memcpy(out128, c.walk_hist, sizeof(c.walk_hist));

@@ -1977,6 +1977,21 @@ __global__ __launch_bounds__(256) void rt_scatter_rows_kernel(const float4* __re
     }
 }
 
+// Full image rows -> band rows (the inverse of rt_scatter_rows_kernel): the running sums an
+// accumulating multi-GPU frame hands each device before it renders (rt_multi.cpp). Rows mapping at
+// or beyond src_rows leave their band row untouched.
+__global__ __launch_bounds__(256) void rt_gather_rows_kernel(const float4* __restrict__ src_acc,
+                                                             const uint32_t* __restrict__ rows, uint32_t n_rows,
+                                                             uint32_t width, uint32_t src_rows,
+                                                             float4* __restrict__ dst_acc) {
+    const uint32_t r = blockIdx.y;
+    if (r >= n_rows) return;
+    const uint32_t sr = rows[r];
+    if (sr >= src_rows) return;
+    for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < width; x += gridDim.x * blockDim.x)
+        dst_acc[size_t(r) * width + x] = src_acc[size_t(sr) * width + x];
+}
+
 // Tonemap of a summed accumulator, exactly the trace kernel's pixel store (shader.rgen:65-66).
 __global__ __launch_bounds__(256) void rt_tonemap_kernel(const float4* __restrict__ acc, uint64_t n, float spp,
                                                          uint32_t* __restrict__ out) {
@@ -2123,6 +2138,15 @@ hipError_t launch_scatter_rows(const float* src_acc, const uint8_t* src_px, cons
                        reinterpret_cast<const float4*>(src_acc), reinterpret_cast<const uint32_t*>(src_px),
                        rows, n_rows, width, dst_rows, reinterpret_cast<float4*>(dst_acc),
                        reinterpret_cast<uint32_t*>(dst_px));
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_rows(const float* src_acc, const uint32_t* rows, uint32_t n_rows, uint32_t width,
+                              uint32_t src_rows, float* dst_acc, hipStream_t st) {
+    if (n_rows == 0 || width == 0) return hipSuccess;
+    dim3 g((width + 255) / 256, n_rows), b(256);
+    hipLaunchKernelGGL(rt_gather_rows_kernel, g, b, 0, st, reinterpret_cast<const float4*>(src_acc), rows, n_rows,
+                       width, src_rows, reinterpret_cast<float4*>(dst_acc));
     return hipGetLastError();
 }
 

@@ -6,10 +6,17 @@
 // GPUs (each device presents its own window). Here the image is tiled into 8-row strips dealt
 // round robin over the devices (interleaving balances sky-heavy and sphere-heavy rows without a
 // tuner), each device renders its strips through a rows map (global pixel seeds, so the image
-// does not depend on the device count), and one RCCL group moves every device's float4 + rgba8
-// strips to device 0 over xGMI (ncclSend / ncclRecv; device 0's own strips are not sent), where
-// one kernel per source puts them in place (rt_scatter_rows); a single device holding every row
-// renders straight into the caller's buffers. SURVEY.md §8(e).
+// does not depend on the device count), one RCCL group moves every other device's float4
+// accumulator strips to device 0 over xGMI (ncclSend / ncclRecv; device 0's own strips are not
+// sent), one kernel per source puts them in place (rt_scatter_rows) and device 0 tonemaps the
+// whole accumulator to rgba8 once (rt_resolve_rgba8: the rgba8 bytes are a function of the float
+// sum, shader.rgen:65-66, so they need not travel). A single device holding every row renders
+// straight into the caller's buffers. SURVEY.md §8(e).
+//
+// A frame is a FramePlan: the partition (device + global rows per part) and the ordered list of
+// steps (row loads / stores on device 0, grouped sends / receives, renders, the resolve) that
+// rt_multi_render executes. The plan is host-only data, so the CPU tests check it for every device
+// count and height without a GPU (rt_debug_multi_plan, tests/test_multi_plan.py).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -21,10 +28,12 @@
 #include <exception>
 #include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/rt_abi.h"
 #include "../../include/rt_mi355x.h"
+#include "../../include/rt_mi355x_debug.h"
 #include "rt_host.h"
 #include "rt_internal.h"
 
@@ -42,22 +51,128 @@ namespace {
 
 constexpr uint32_t kStrip = 8;   // rows per strip: one 8x8 pixel tile high, the kernel's wave tile
 
-// One launch of a multi-device frame: a list of global rows rendered by one device (its own
-// context), gathered into a staging band on device 0.
+// ---- the frame plan ----------------------------------------------------------------------
+// Buffers a step names: the caller's accumulator / rgba8 image on device 0 (W x H), each part's
+// band on its device (rows x W), and each remote part's stage on device 0 (rows x W float4).
+enum PlanOp : uint32_t {
+    OP_LOAD_ROWS = 1,   // device 0: the part's rows of the caller's accumulator -> its band (a part
+                        // of device 0) or its stage (accumulating frames: the running sums)
+    OP_GROUP_START = 2, // ncclGroupStart
+    OP_SEND = 3,        // dev -> peer: `count` floats of the part's band (dev != 0) or stage (dev 0)
+    OP_RECV = 4,        // dev <- peer: `count` floats into the part's band (dev != 0) or stage (dev 0)
+    OP_GROUP_END = 5,   // ncclGroupEnd
+    OP_RENDER = 6,      // dev renders the part; flags bit 0: straight into the caller's buffers
+    OP_STORE_ROWS = 7,  // device 0: the part's band (device 0) or stage -> its rows of the accumulator
+    OP_RESOLVE = 8,     // device 0: rgba8 of the whole accumulator (`count` texels)
+};
+constexpr uint32_t kDirect = 1u;
+
+struct PlanPart {
+    uint32_t dev = 0;
+    std::vector<uint32_t> rows;   // global rows, band order
+    bool whole = false;           // device 0, every row in order: renders into the caller's buffers
+};
+struct PlanStep {
+    uint32_t op, dev, peer, part, flags;
+    uint64_t count;
+};
+struct FramePlan {
+    std::vector<PlanPart> parts;
+    std::vector<PlanStep> steps;
+};
+using Parts = std::vector<std::pair<uint32_t, std::vector<uint32_t>>>;
+
+// Strips k = 0, 1, ... of kStrip rows, strip k on device k % n (rtvk.dist.strip_rows).
+Parts strip_parts(uint32_t n, uint32_t H) {
+    Parts parts(n);
+    for (uint32_t d = 0; d < n; d++) parts[d].first = d;
+    for (uint32_t y = 0; y < H; y++) parts[(y / kStrip) % n].second.push_back(y);
+    return parts;
+}
+
+// The reference's contiguous bands (src/ray_trace.cpp:74-93): band i = rows [start[i], start[i+1])
+// (the last to H), on device i % n. Empty when the starts do not tile [0, H) top to bottom.
+Parts band_parts(uint32_t n, uint32_t H, const uint32_t* start, uint32_t n_bands) {
+    Parts parts(n_bands);
+    for (uint32_t i = 0; i < n_bands; i++) {
+        const uint32_t y0 = start[i], y1 = i + 1 < n_bands ? start[i + 1] : H;
+        if (y1 < y0 || y1 > H || (i == 0 && y0 != 0)) return Parts{};
+        parts[i].first = i % n;
+        for (uint32_t y = y0; y < y1; y++) parts[i].second.push_back(y);
+    }
+    return parts;
+}
+
+// The steps of one frame over `parts` (W x H). accumulate: every part starts from its rows of the
+// caller's accumulator (rt_render_device's accumulate semantics for the whole image, at any
+// device count): device 0 loads them into its own bands and into the stages of the other
+// devices' parts, and sends those in one group. Then every part renders; one group brings the
+// other devices' accumulator bands to device 0's stages; device 0 stores every band in place and
+// tonemaps the whole image. A part of device 0 never goes through RCCL; a `whole` part renders
+// into the caller's buffers and needs nothing else (the one-device frame).
+FramePlan make_plan(uint32_t W, uint32_t H, Parts&& parts, bool accumulate) {
+    FramePlan p;
+    for (auto& pr : parts) {
+        PlanPart q;
+        q.dev = pr.first;
+        q.rows = std::move(pr.second);
+        q.whole = q.dev == 0 && q.rows.size() == H;
+        for (uint32_t y = 0; q.whole && y < H; y++) q.whole = q.rows[y] == y;
+        p.parts.push_back(std::move(q));
+    }
+    const uint32_t np = uint32_t(p.parts.size());
+    auto live = [&](uint32_t i) { return !p.parts[i].rows.empty(); };
+    auto floats = [&](uint32_t i) { return uint64_t(p.parts[i].rows.size()) * W * 4u; };
+    auto add = [&](uint32_t op, uint32_t dev, uint32_t peer, uint32_t part, uint32_t flags, uint64_t count) {
+        p.steps.push_back(PlanStep{op, dev, peer, part, flags, count});
+    };
+    bool whole = false, remote = false;
+    for (uint32_t i = 0; i < np; i++) {
+        whole |= live(i) && p.parts[i].whole;
+        remote |= live(i) && p.parts[i].dev != 0;
+    }
+    if (accumulate && !whole) {
+        for (uint32_t i = 0; i < np; i++)
+            if (live(i)) add(OP_LOAD_ROWS, 0, 0, i, 0, floats(i));
+        if (remote) {
+            add(OP_GROUP_START, 0, 0, 0, 0, 0);
+            for (uint32_t i = 0; i < np; i++) {
+                if (!live(i) || p.parts[i].dev == 0) continue;
+                add(OP_SEND, 0, p.parts[i].dev, i, 0, floats(i));
+                add(OP_RECV, p.parts[i].dev, 0, i, 0, floats(i));
+            }
+            add(OP_GROUP_END, 0, 0, 0, 0, 0);
+        }
+    }
+    for (uint32_t i = 0; i < np; i++)
+        if (live(i)) add(OP_RENDER, p.parts[i].dev, p.parts[i].dev, i, p.parts[i].whole ? kDirect : 0u, 0);
+    if (whole) return p;
+    if (remote) {
+        add(OP_GROUP_START, 0, 0, 0, 0, 0);
+        for (uint32_t i = 0; i < np; i++) {
+            if (!live(i) || p.parts[i].dev == 0) continue;
+            add(OP_SEND, p.parts[i].dev, 0, i, 0, floats(i));
+            add(OP_RECV, 0, p.parts[i].dev, i, 0, floats(i));
+        }
+        add(OP_GROUP_END, 0, 0, 0, 0, 0);
+    }
+    for (uint32_t i = 0; i < np; i++)
+        if (live(i)) add(OP_STORE_ROWS, 0, 0, i, 0, floats(i));
+    add(OP_RESOLVE, 0, 0, 0, 0, uint64_t(W) * H);
+    return p;
+}
+
+// One part of a multi-device frame on its device (its own context), with its buffers.
 struct Launch {
     uint32_t dev = 0;
     std::vector<uint32_t> rows;          // global rows, band order
-    bool whole = false;                  // device 0, every row in order (one device): may render
-                                         // straight into the caller's buffers
-    float* sum_at = nullptr;             // whole: the caller's accum buffer holding the running sum
-                                         // (last frame rendered straight into it), else the band
+    bool whole = false;
     rt_context* ctx = nullptr;           // on dev
     uint32_t* rows_dev = nullptr;        // rows on dev (the kernel's map)
-    uint32_t* rows_root = nullptr;       // rows on device 0 (the scatter's map)
-    float* acc = nullptr;                // band on dev: rows x W float4
-    uint8_t* out = nullptr;              // band on dev: rows x W rgba8
-    float* stage_acc = nullptr;          // band copy on device 0
-    uint8_t* stage_out = nullptr;
+    uint32_t* rows_root = nullptr;       // rows on device 0 (the row loads / stores)
+    float* acc = nullptr;                // band on dev: rows x W float4 (not for a whole part)
+    uint8_t* out = nullptr;              // band on dev: rows x W rgba8 (the kernel's store; not sent)
+    float* stage_acc = nullptr;          // dev != 0: the band's copy on device 0
 };
 
 }  // namespace
@@ -72,7 +187,8 @@ struct rt_multi {
     // cached partition (geometry + kind): strips of W x H, or explicit bands
     uint32_t W = 0, H = 0;
     std::string key;
-    std::vector<Launch> launches;
+    std::vector<Launch> launches;        // one per plan part, same index
+    FramePlan plan[2];                   // steps without / with accumulation
 };
 
 namespace {
@@ -91,9 +207,9 @@ void free_launches(rt_multi* m) {
         (void)hipDeviceSynchronize();
         if (l.rows_root) (void)hipFree(l.rows_root);
         if (l.stage_acc) (void)hipFree(l.stage_acc);
-        if (l.stage_out) (void)hipFree(l.stage_out);
     }
     m->launches.clear();
+    m->plan[0] = m->plan[1] = FramePlan{};
     m->key.clear();
 }
 
@@ -117,109 +233,130 @@ int set_scene_all(rt_multi* m) {
     return rc;
 }
 
-// (Re)builds the launch list for `key` (one entry per launch: device + global rows). Buffers of
-// a launch are zeroed (accumulate adds to the previous frame of the same partition).
-int set_partition(rt_multi* m, const std::string& key, uint32_t W, uint32_t H,
-                  std::vector<std::pair<uint32_t, std::vector<uint32_t>>>&& parts) {
+// (Re)builds the launches for `key` from the partition: one per part (device + global rows), its
+// context and buffers, and the frame's plans with and without accumulation.
+int set_partition(rt_multi* m, const std::string& key, uint32_t W, uint32_t H, Parts&& parts) {
     if (m->key == key && m->W == W && m->H == H) return RT_OK;
     free_launches(m);
     m->W = W;
     m->H = H;
-    for (auto& p : parts) {
+    Parts copy = parts;
+    m->plan[0] = make_plan(W, H, std::move(copy), false);
+    m->plan[1] = make_plan(W, H, std::move(parts), true);
+    for (const PlanPart& q : m->plan[0].parts) {
         Launch l;
-        l.dev = p.first;
-        l.rows = std::move(p.second);
-        l.whole = l.dev == 0 && l.rows.size() == H;
-        for (uint32_t y = 0; l.whole && y < H; y++) l.whole = l.rows[y] == y;
+        l.dev = q.dev;
+        l.rows = q.rows;
+        l.whole = q.whole;
         m->launches.push_back(std::move(l));
     }
     for (Launch& l : m->launches) {
         const size_t nr = l.rows.size(), texels = nr * W;
         if (int rc = rt_context_create(int(l.dev), &l.ctx)) return rc;
-        DeviceGuard g(static_cast<int>(l.dev));
-        if (nr) {
+        if (!nr || l.whole) continue;
+        {
+            DeviceGuard g(static_cast<int>(l.dev));
             RT_HIP(hipMalloc(&l.rows_dev, nr * 4));
             RT_HIP(hipMemcpy(l.rows_dev, l.rows.data(), nr * 4, hipMemcpyHostToDevice));
             RT_HIP(hipMalloc(&l.acc, texels * 16));
             RT_HIP(hipMalloc(&l.out, texels * 4));
-            RT_HIP(hipMemset(l.acc, 0, texels * 16));
-            RT_HIP(hipMemset(l.out, 0, texels * 4));
         }
         DeviceGuard g0(0);
-        if (nr) {
-            RT_HIP(hipMalloc(&l.rows_root, nr * 4));
-            RT_HIP(hipMemcpy(l.rows_root, l.rows.data(), nr * 4, hipMemcpyHostToDevice));
-            if (l.dev != 0) {   // device 0's own bands are scattered in place (gather_to_root)
-                RT_HIP(hipMalloc(&l.stage_acc, texels * 16));
-                RT_HIP(hipMalloc(&l.stage_out, texels * 4));
-            }
-        }
+        RT_HIP(hipMalloc(&l.rows_root, nr * 4));
+        RT_HIP(hipMemcpy(l.rows_root, l.rows.data(), nr * 4, hipMemcpyHostToDevice));
+        if (l.dev != 0) RT_HIP(hipMalloc(&l.stage_acc, texels * 16));
     }
     m->key = key;
     return m->scene_set ? set_scene_all(m) : RT_OK;
 }
 
-// Strips k = 0, 1, ... of kStrip rows, strip k on device k % n.
-std::vector<std::pair<uint32_t, std::vector<uint32_t>>> strip_parts(uint32_t n, uint32_t H) {
-    std::vector<std::pair<uint32_t, std::vector<uint32_t>>> parts(n);
-    for (uint32_t d = 0; d < n; d++) parts[d].first = d;
-    for (uint32_t y = 0; y < H; y++) parts[(y / kStrip) % n].second.push_back(y);
-    return parts;
+// A context on device 0 (the row loads / stores and the resolve run on stream[0]).
+rt_context* root_ctx(rt_multi* m) {
+    for (Launch& l : m->launches)
+        if (l.dev == 0) return l.ctx;
+    return nullptr;
 }
 
-// One RCCL group moves every other device's bands (float4 accumulator, then rgba8 image) to
-// device 0, then one kernel per band puts its rows in place in dst (device 0 pointers, W x H);
-// device 0's own bands go straight from its render buffers (no send to itself: at N = 1 the frame
-// moves no byte through RCCL), and a band rendered into dst itself (`direct`) not at all.
-// Everything on stream[0] after the group.
-int gather_to_root(rt_multi* m, float* dst_acc, uint8_t* dst_out, bool direct) {
-    const uint32_t W = m->W;
-    RT_NCCL(ncclGroupStart());
-    for (Launch& l : m->launches) {
-        const size_t texels = l.rows.size() * size_t(W);
-        if (!texels || l.dev == 0) continue;
-        ncclResult_t e;
-        {
-            DeviceGuard g(static_cast<int>(l.dev));
-            e = ncclSend(l.acc, texels * 4, ncclFloat32, 0, m->comm[l.dev], m->stream[l.dev]);
-            if (e == ncclSuccess) e = ncclSend(l.out, texels * 4, ncclUint8, 0, m->comm[l.dev], m->stream[l.dev]);
+// Executes a frame plan: rcis[i] for part i (n_rci == 1: rcis[0] for every part; offsets replaced
+// by the rows maps), into the caller's acc / out (device 0, W x H). Every step is queued on its
+// device's stream; the stream order of each device and the RCCL groups order them across devices.
+int run_plan(rt_multi* m, const FramePlan& p, const RenderCallInfo* rcis, size_t n_rci, const rt_options* opt,
+             float* acc, uint8_t* out) {
+    const uint32_t W = m->W, H = m->H;
+    rt_context* c0 = root_ctx(m);
+    bool in_group = false;
+    auto body = [&]() -> int {
+        for (const PlanStep& s : p.steps) {
+            Launch& l = m->launches[s.part];
+            float* dev_buf = s.dev == 0 ? l.stage_acc : l.acc;   // a SEND / RECV's buffer on s.dev
+            float* root_buf = l.dev == 0 ? l.acc : l.stage_acc;  // the part's accumulator on device 0
+            const uint32_t nr = uint32_t(l.rows.size());
+            switch (s.op) {
+                case OP_GROUP_START:
+                    RT_NCCL(ncclGroupStart());
+                    in_group = true;
+                    break;
+                case OP_GROUP_END:
+                    in_group = false;
+                    RT_NCCL(ncclGroupEnd());
+                    break;
+                case OP_SEND:
+                case OP_RECV: {
+                    DeviceGuard g(static_cast<int>(s.dev));
+                    const ncclResult_t e =
+                        s.op == OP_SEND
+                            ? ncclSend(dev_buf, s.count, ncclFloat32, int(s.peer), m->comm[s.dev], m->stream[s.dev])
+                            : ncclRecv(dev_buf, s.count, ncclFloat32, int(s.peer), m->comm[s.dev], m->stream[s.dev]);
+                    if (e != ncclSuccess) return fail(RT_ERR_DEVICE, std::string("RCCL: ") + ncclGetErrorString(e));
+                    break;
+                }
+                case OP_LOAD_ROWS:
+                    if (int rc = rt_gather_rows(c0, acc, l.rows_root, nr, W, H, root_buf, m->stream[0])) return rc;
+                    break;
+                case OP_STORE_ROWS:
+                    if (int rc = rt_scatter_rows(c0, root_buf, nullptr, l.rows_root, nr, W, H, acc, nullptr,
+                                                 m->stream[0]))
+                        return rc;
+                    break;
+                case OP_RENDER: {
+                    RenderCallInfo r = rcis[n_rci == 1 ? 0 : s.part];
+                    r.offset = rt_uvec2{0, 0};   // the rows map carries the global rows
+                    const bool d = (s.flags & kDirect) != 0;
+                    if (int rc = rt_render_device(l.ctx, &r, d ? nullptr : l.rows_dev, W, nr, d ? acc : l.acc,
+                                                  d ? out : l.out, opt, m->stream[l.dev]))
+                        return rc;
+                    break;
+                }
+                case OP_RESOLVE:
+                    if (int rc = rt_resolve_rgba8(c0, acc, s.count, rcis[0].samplesPerRenderCall, out, m->stream[0]))
+                        return rc;
+                    break;
+                default:
+                    return fail(RT_ERR_INVALID_ARGUMENT, "bad plan step");
+            }
         }
-        if (e == ncclSuccess) {
-            DeviceGuard g0(0);
-            e = ncclRecv(l.stage_acc, texels * 4, ncclFloat32, int(l.dev), m->comm[0], m->stream[0]);
-            if (e == ncclSuccess) e = ncclRecv(l.stage_out, texels * 4, ncclUint8, int(l.dev), m->comm[0], m->stream[0]);
-        }
-        if (e != ncclSuccess) {
-            (void)ncclGroupEnd();
-            return fail(RT_ERR_DEVICE, std::string("RCCL gather: ") + ncclGetErrorString(e));
-        }
-    }
-    RT_NCCL(ncclGroupEnd());
-    for (Launch& l : m->launches) {
-        if (l.rows.empty() || (direct && l.whole)) continue;
-        const bool own = l.dev == 0;   // rendered on stream[0] itself
-        if (int rc = rt_scatter_rows(m->launches[0].ctx, own ? l.acc : l.stage_acc, own ? l.out : l.stage_out,
-                                     l.rows_root, uint32_t(l.rows.size()), W, m->H, dst_acc, dst_out, m->stream[0]))
-            return rc;
-    }
-    return RT_OK;
+        return RT_OK;
+    };
+    const int rc = body();
+    if (in_group) (void)ncclGroupEnd();   // a failure inside a group still closes it
+    return rc;
 }
 
-// Launch i renders its rows with rcis[i] (offset replaced by the rows map) on its device's stream.
-// direct (dst_acc / dst_out on device 0, W x H): a `whole` launch renders into them, no map.
-int render_bands(rt_multi* m, const RenderCallInfo* rcis, size_t n_rci, const rt_options* opt, bool direct,
-                 float* dst_acc, uint8_t* dst_out) {
-    for (size_t i = 0; i < m->launches.size(); i++) {
-        Launch& l = m->launches[i];
-        if (l.rows.empty()) continue;
-        RenderCallInfo r = rcis[n_rci == 1 ? 0 : i];
-        r.offset = rt_uvec2{0, 0};   // the rows map carries the global rows
-        const bool d = direct && l.whole;
-        if (int rc = rt_render_device(l.ctx, &r, d ? nullptr : l.rows_dev, m->W, uint32_t(l.rows.size()),
-                                      d ? dst_acc : l.acc, d ? dst_out : l.out, opt, m->stream[l.dev]))
-            return rc;
+// Flat form of a plan (rt_debug_multi_plan): {n_parts, n_steps}, then per part {dev, whole,
+// n_rows, rows...}, then per step {op, dev, peer, part, flags, count low, count high}.
+std::vector<uint32_t> serialize(const FramePlan& p) {
+    std::vector<uint32_t> v{uint32_t(p.parts.size()), uint32_t(p.steps.size())};
+    for (const PlanPart& q : p.parts) {
+        v.push_back(q.dev);
+        v.push_back(q.whole ? 1u : 0u);
+        v.push_back(uint32_t(q.rows.size()));
+        v.insert(v.end(), q.rows.begin(), q.rows.end());
     }
-    return RT_OK;
+    for (const PlanStep& s : p.steps) {
+        const uint32_t w[7] = {s.op, s.dev, s.peer, s.part, s.flags, uint32_t(s.count), uint32_t(s.count >> 32)};
+        v.insert(v.end(), w, w + 7);
+    }
+    return v;
 }
 
 }  // namespace
@@ -327,23 +464,32 @@ int rt_multi_render(rt_multi* m, const RenderCallInfo* rci, const rt_options* op
         RT_HIP(hipEventRecord(m->ev_in, st));
         for (uint32_t d = 0; d < m->n; d++) RT_HIP(hipStreamWaitEvent(m->stream[d], m->ev_in, 0));
     }
-    // One device holding every row renders straight into the caller's buffers (no band, no
-    // reorder). Its running sum then lives in that accum buffer: an accumulating frame into the
-    // same buffer adds to it there; into another buffer, the sum is copied into the band first.
-    Launch* w = m->launches.size() == 1 && m->launches[0].whole ? &m->launches[0] : nullptr;
     const bool acc_mode = opt && opt->accumulate;
-    const bool direct = w && (!acc_mode || w->sum_at == accum);
-    if (w && !direct && w->sum_at) {
-        DeviceGuard g0(0);
-        RT_HIP(hipMemcpyAsync(w->acc, w->sum_at, w->rows.size() * size_t(W) * 16, hipMemcpyDeviceToDevice,
-                              m->stream[0]));
-    }
-    if (int rc = render_bands(m, rci, 1, opt, direct, accum, out)) return rc;
-    if (int rc = gather_to_root(m, accum, out, direct)) return rc;
-    if (w) w->sum_at = direct ? accum : nullptr;
+    if (int rc = run_plan(m, m->plan[acc_mode ? 1 : 0], rci, 1, opt, accum, out)) return rc;
     DeviceGuard g0(0);
     RT_HIP(hipEventRecord(m->ev_out, m->stream[0]));   // the caller's later work waits for it
     RT_HIP(hipStreamWaitEvent(st, m->ev_out, 0));
+    return RT_OK;
+}
+
+int rt_debug_multi_plan(uint32_t n_devices, uint32_t width, uint32_t height, const uint32_t* band_starts,
+                        uint32_t n_bands, uint32_t accumulate, uint32_t* out, uint64_t capacity, uint64_t* count) {
+    if (!count) return fail(RT_ERR_INVALID_ARGUMENT, "count is NULL");
+    *count = 0;
+    if (n_devices == 0 || width == 0 || height == 0) return fail(RT_ERR_INVALID_ARGUMENT, "zero size");
+    if (band_starts && n_bands == 0) return fail(RT_ERR_INVALID_ARGUMENT, "no bands");
+    std::vector<uint32_t> v;
+    try {
+        Parts parts = band_starts ? band_parts(n_devices, height, band_starts, n_bands) : strip_parts(n_devices, height);
+        if (parts.empty()) return fail(RT_ERR_INVALID_ARGUMENT, "bands must tile the image top to bottom");
+        v = serialize(make_plan(width, height, std::move(parts), accumulate != 0));
+    } catch (const std::exception& e) {
+        return fail(RT_ERR_OUT_OF_MEMORY, e.what());
+    }
+    *count = v.size();
+    if (!out) return RT_OK;   // size query
+    if (capacity < v.size()) return fail(RT_ERR_INVALID_ARGUMENT, "capacity");
+    std::memcpy(out, v.data(), v.size() * 4);
     return RT_OK;
 }
 
@@ -419,8 +565,12 @@ int rt_render(const Sphere* spheres, uint32_t sphere_count, const RenderCallInfo
     for (uint32_t i = 0; i < rci_count; i++) {
         const uint32_t y0 = rci[i].offset.y;
         const uint32_t y1 = (i + 1 < rci_count) ? rci[i + 1].offset.y : H;
-        if (rci[i].image_size.x != W || rci[i].image_size.y != H || rci[i].offset.x != 0 || y1 < y0 || y1 > H)
+        if (rci[i].image_size.x != W || rci[i].image_size.y != H || rci[i].offset.x != 0 || y1 < y0 || y1 > H ||
+            (i == 0 && y0 != 0))
             return fail(RT_ERR_INVALID_ARGUMENT, "bands must tile the image top to bottom");
+        // device 0 tonemaps the gathered image once (rt_resolve_rgba8), with one spp
+        if (rci[i].samplesPerRenderCall != rci[0].samplesPerRenderCall)
+            return fail(RT_ERR_INVALID_ARGUMENT, "every band must have the same samplesPerRenderCall");
     }
     rt_multi* m = nullptr;
     if (int rc = rt_multi_create(rci_count, &m)) return rc;
@@ -429,26 +579,17 @@ int rt_render(const Sphere* spheres, uint32_t sphere_count, const RenderCallInfo
     uint8_t* dout = nullptr;
     auto run = [&]() -> int {
         if (int rc = rt_multi_set_scene(m, spheres, sphere_count)) return rc;
-        std::vector<std::pair<uint32_t, std::vector<uint32_t>>> parts(rci_count);
-        for (uint32_t i = 0; i < rci_count; i++) {
-            const uint32_t y0 = rci[i].offset.y, y1 = (i + 1 < rci_count) ? rci[i + 1].offset.y : H;
-            parts[i].first = i % m->n;
-            for (uint32_t y = y0; y < y1; y++) parts[i].second.push_back(y);
-        }
-        if (int rc = set_partition(m, "bands", W, H, std::move(parts))) return rc;
-        if (opt && opt->accumulate) {   // the bands start from the host accumulator
-            for (Launch& l : m->launches) {
-                if (l.rows.empty()) continue;
-                DeviceGuard g(static_cast<int>(l.dev));
-                RT_HIP(hipMemcpy(l.acc, accum + size_t(l.rows[0]) * W * 4, l.rows.size() * size_t(W) * 16,
-                                 hipMemcpyHostToDevice));
-            }
-        }
+        std::vector<uint32_t> starts(rci_count);
+        for (uint32_t i = 0; i < rci_count; i++) starts[i] = rci[i].offset.y;
+        if (int rc = set_partition(m, "bands", W, H, band_parts(m->n, H, starts.data(), rci_count))) return rc;
         DeviceGuard g0(0);
         RT_HIP(hipMalloc(&dacc, size_t(W) * H * 16));
         RT_HIP(hipMalloc(&dout, size_t(W) * H * 4));
-        if (int rc = render_bands(m, rci, rci_count, opt, false, nullptr, nullptr)) return rc;   // each band its own RenderCallInfo
-        if (int rc = gather_to_root(m, dacc, dout, false)) return rc;
+        const bool acc_mode = opt && opt->accumulate;
+        if (acc_mode)   // every band starts from its rows of the host accumulator
+            RT_HIP(hipMemcpyAsync(dacc, accum, size_t(W) * H * 16, hipMemcpyHostToDevice, m->stream[0]));
+        // each band its own RenderCallInfo
+        if (int rc = run_plan(m, m->plan[acc_mode ? 1 : 0], rci, rci_count, opt, dacc, dout)) return rc;
         RT_HIP(hipStreamSynchronize(m->stream[0]));
         RT_HIP(hipMemcpy(accum, dacc, size_t(W) * H * 16, hipMemcpyDeviceToHost));
         RT_HIP(hipMemcpy(out, dout, size_t(W) * H * 4, hipMemcpyDeviceToHost));

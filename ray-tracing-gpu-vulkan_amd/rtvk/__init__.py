@@ -26,7 +26,7 @@ __all__ = [
     "DIFFUSE", "METAL", "REFRACTIVE", "SOLID", "CHECKERED", "Sphere", "Scene", "RenderCallInfo",
     "Options", "Stats", "RtError", "generateRandomScene", "canonical_render_call_info",
     "make_options", "Renderer", "MultiRenderer", "render", "ray_trace", "store_ppm", "spheres_to_numpy",
-    "load_library", "HASH", "STREAM",
+    "load_library", "HASH", "STREAM", "multi_plan",
 ]
 
 STREAM = abi.RT_RNG_PIXEL_STREAM   # the reference's per-pixel LCG stream (random.glsl)
@@ -238,22 +238,45 @@ class Renderer:
                 "form": forms.get(int(v[1]), str(v[1])), "lds_bytes": int(v[2]), "cus": int(v[3])}
 
     def scatter_rows(self, src_accum, src_rgba8, rows, dst_accum, dst_rgba8, stream=None) -> None:
-        """dst[rows[i]] = src[i] (device), the reorder after a multi-GPU gather."""
-        n, w = int(src_rgba8.shape[0]), int(src_rgba8.shape[1])
-        _check_dev_tensor(src_rgba8, "torch.uint8", (n, w, 4))
-        dh = int(dst_rgba8.shape[0])
-        _check_dev_tensor(dst_rgba8, "torch.uint8", (dh, w, 4))
-        if src_accum is not None or dst_accum is not None:
+        """dst[rows[i]] = src[i] (device), the reorder after a multi-GPU gather; either image may
+        be None (both its source and destination)."""
+        src = src_rgba8 if src_rgba8 is not None else src_accum
+        dst = dst_rgba8 if dst_rgba8 is not None else dst_accum
+        if src is None or dst is None:
+            raise ValueError("nothing to scatter")
+        n, w, dh = int(src.shape[0]), int(src.shape[1]), int(dst.shape[0])
+        if (src_rgba8 is None) != (dst_rgba8 is None) or (src_accum is None) != (dst_accum is None):
+            raise ValueError("each image needs both a source and a destination, or neither")
+        if src_rgba8 is not None:
+            _check_dev_tensor(src_rgba8, "torch.uint8", (n, w, 4))
+            _check_dev_tensor(dst_rgba8, "torch.uint8", (dh, w, 4))
+        if src_accum is not None:
             _check_dev_tensor(src_accum, "torch.float32", (n, w, 4))
             _check_dev_tensor(dst_accum, "torch.float32", (dh, w, 4))
-        if rows.numel() != n or not rows.is_cuda or rows.element_size() != 4 or not rows.is_contiguous():
-            raise ValueError("rows must be a contiguous 4-byte cuda tensor of one entry per source row")
-        if n and (int(rows.min()) < 0 or int(rows.max()) >= dh):
-            raise ValueError(f"rows must lie in [0, {dh})")
+        self._check_rows(rows, n, dh)
         check(self._lib.rt_scatter_rows(self._ctx, src_accum.data_ptr() if src_accum is not None else None,
-                                        src_rgba8.data_ptr(), rows.data_ptr(), n, w, dh,
+                                        src_rgba8.data_ptr() if src_rgba8 is not None else None,
+                                        rows.data_ptr(), n, w, dh,
                                         dst_accum.data_ptr() if dst_accum is not None else None,
-                                        dst_rgba8.data_ptr(), _stream_ptr(stream, self.device)))
+                                        dst_rgba8.data_ptr() if dst_rgba8 is not None else None,
+                                        _stream_ptr(stream, self.device)))
+
+    @staticmethod
+    def _check_rows(rows, n, limit):
+        if rows.numel() != n or not rows.is_cuda or rows.element_size() != 4 or not rows.is_contiguous():
+            raise ValueError("rows must be a contiguous 4-byte cuda tensor of one entry per band row")
+        if n and (int(rows.min()) < 0 or int(rows.max()) >= limit):
+            raise ValueError(f"rows must lie in [0, {limit})")
+
+    def gather_rows(self, src_accum, rows, dst_accum, stream=None) -> None:
+        """dst[i] = src[rows[i]] (device float4 accumulators), the inverse of scatter_rows."""
+        sh, w = int(src_accum.shape[0]), int(src_accum.shape[1])
+        n = int(dst_accum.shape[0])
+        _check_dev_tensor(src_accum, "torch.float32", (sh, w, 4))
+        _check_dev_tensor(dst_accum, "torch.float32", (n, w, 4))
+        self._check_rows(rows, n, sh)
+        check(self._lib.rt_gather_rows(self._ctx, src_accum.data_ptr(), rows.data_ptr(), n, w, sh,
+                                       dst_accum.data_ptr(), _stream_ptr(stream, self.device)))
 
     def resolve_rgba8(self, accum, spp: int, out, stream=None) -> None:
         """out = rgba8 tonemap of the summed float4 accumulator `accum` (device tensors), exactly
@@ -346,6 +369,38 @@ class MultiRenderer:
         st = Stats()
         check(self._lib.rt_multi_stats(self._m, ctypes.byref(st)))
         return st
+
+
+PLAN_OPS = {1: "load_rows", 2: "group_start", 3: "send", 4: "recv", 5: "group_end", 6: "render",
+            7: "store_rows", 8: "resolve"}
+
+
+def multi_plan(n_devices: int, width: int, height: int, band_starts: Optional[Sequence[int]] = None,
+               accumulate: bool = False) -> dict:
+    """The frame plan rt_multi executes (rt_debug_multi_plan; host only, no GPU needed): the parts
+    [(device, whole, rows)] and the ordered steps [{op, dev, peer, part, flags, count}]. band_starts
+    None: 8-row strips dealt round robin (rt_multi_render); else the bands of rt_render."""
+    lib = load_library()
+    bs = None if band_starts is None else (ctypes.c_uint32 * len(band_starts))(*band_starts)
+    nb = 0 if band_starts is None else len(band_starts)
+    n = ctypes.c_uint64(0)
+    check(lib.rt_debug_multi_plan(n_devices, width, height, bs, nb, int(accumulate), None, 0, ctypes.byref(n)))
+    buf = np.zeros(n.value, np.uint32)
+    check(lib.rt_debug_multi_plan(n_devices, width, height, bs, nb, int(accumulate), buf.ctypes.data, n.value,
+                                  ctypes.byref(n)))
+    n_parts, n_steps = int(buf[0]), int(buf[1])
+    at, parts, steps = 2, [], []
+    for _ in range(n_parts):
+        dev, whole, nr = (int(v) for v in buf[at:at + 3])
+        parts.append((dev, bool(whole), buf[at + 3:at + 3 + nr].copy()))
+        at += 3 + nr
+    for _ in range(n_steps):
+        op, dev, peer, part, flags, lo, hi = (int(v) for v in buf[at:at + 7])
+        steps.append({"op": PLAN_OPS.get(op, op), "dev": dev, "peer": peer, "part": part, "flags": flags,
+                      "count": lo | (hi << 32)})
+        at += 7
+    assert at == len(buf)
+    return {"parts": parts, "steps": steps}
 
 
 @dataclass

@@ -1,4 +1,5 @@
-"""ctypes mirror of include/rt_abi.h and include/rt_mi355x.h (the C-ABI of librt_mi355x.so).
+"""ctypes mirror of include/rt_abi.h, include/rt_mi355x.h (the C-ABI of librt_mi355x.so) and
+include/rt_mi355x_debug.h (its diagnostic entry points).
 
 Struct layouts are the reference's byte-exact host<->device ABI:
   Sphere          src/scene.h:16-22            (80 B)
@@ -92,7 +93,7 @@ assert ctypes.sizeof(Scene) == 41024 and Scene.sphereAmount.offset == 40960
 assert ctypes.sizeof(RenderCallInfo) == 64 and RenderCallInfo.camera_dir.offset == 48
 assert ctypes.sizeof(Options) == 32
 
-# Every symbol include/rt_mi355x.h declares: (name, restype, argtypes).
+# Every symbol include/rt_mi355x.h and include/rt_mi355x_debug.h declare: (name, restype, argtypes).
 _P, _U32, _I = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
 EXPORTS = {
     "rt_abi_version": (_U32, []),
@@ -111,6 +112,7 @@ EXPORTS = {
     "rt_get_stats": (_I, [_P, ctypes.POINTER(Stats)]),
     "rt_scatter_rows": (_I, [_P, _P, _P, _P, _U32, _U32, _U32, _P, _P, _P]),
     "rt_resolve_rgba8": (_I, [_P, _P, ctypes.c_uint64, _U32, _P, _P]),
+    "rt_gather_rows": (_I, [_P, _P, _P, _U32, _U32, _U32, _P, _P]),
     "rt_multi_create": (_I, [_U32, ctypes.POINTER(_P)]),
     "rt_multi_destroy": (_I, [_P]),
     "rt_multi_device_count": (_I, [_P, ctypes.POINTER(_U32)]),
@@ -138,6 +140,9 @@ EXPORTS = {
     "rt_debug_tile_cost": (_I, [_P, _P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     "rt_debug_scene": (_I, [_P, _U32, _P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     "ray_trace": (None, [_U32, ctypes.c_bool, _U32, _U32, _U32]),
+    # include/rt_mi355x_debug.h (diagnostics, A/B, the multi-GPU frame plan)
+    "rt_debug_multi_plan": (_I, [_U32, _U32, _U32, _P, _U32, _U32, _P, ctypes.c_uint64,
+                                 ctypes.POINTER(ctypes.c_uint64)]),
 }
 
 _lib = None

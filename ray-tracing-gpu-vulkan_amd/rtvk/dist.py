@@ -5,8 +5,10 @@ The reference splits the image into contiguous row bands, one per Vulkan device,
 band taking the remainder (src/ray_trace.cpp:74-93), and never moves pixels between GPUs (each
 device presents its own window, :96-105). Here rank r renders the 8-row strips k with
 k % world == r — interleaving balances sky-heavy and sphere-heavy rows without the reference's
-tuner (src/workload_tuner.hpp) — and one gather per buffer brings every rank's strips to rank 0,
-where rt_scatter_rows puts them in place.
+tuner (src/workload_tuner.hpp) — and one gather brings every rank's float4 accumulator strips to
+rank 0, where rt_scatter_rows puts them in place and rt_resolve_rgba8 tonemaps the whole image
+once (the rgba8 bytes are a function of the float sum, shader.rgen:65-66, so they need not
+travel: 20 % fewer bytes and half the collectives of gathering both images).
 
 Pixels are independent and seeds are global (RT_SEED_GLOBAL), so the assembled image is
 bit-identical to a one-GPU render whatever the world size, in both random stream modes. With the
@@ -46,13 +48,15 @@ class DistributedRenderer:
     render_band(rows_dev, accum_dev, out_dev): renders this rank's rows into [rows, W, 4] buffers
     (rows_dev None at one rank: the whole frame, no row map).
     assemble(band_accum, band_out, rows_dev, full_accum, full_out): rank-0 reorder of one rank's
-    gathered band into the full image.
+    gathered band into the full image (band_out / full_out None when only accumulators travel).
+    resolve(full_accum, full_out): rank-0 tonemap of the assembled accumulator; when given (with
+    gather_accum), only the accumulators are gathered. Without it both images are gathered.
     force_gather: run the gather + reassembly even on one rank (tests of the collective path).
     """
 
     def __init__(self, width: int, height: int, device, render_band: Callable,
                  assemble: Optional[Callable] = None, strip: int = STRIP, gather_accum: bool = True,
-                 force_gather: bool = False):
+                 force_gather: bool = False, resolve: Optional[Callable] = None):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
@@ -62,6 +66,7 @@ class DistributedRenderer:
         self.render_band = render_band
         self.assemble = assemble
         self.gather_accum = gather_accum
+        self.resolve = resolve if gather_accum else None
         self.rows_np = strip_rows(self.rank, self.world, height, strip)
         self.nmax = max_rows(self.world, height, strip)
         n = len(self.rows_np)
@@ -80,7 +85,7 @@ class DistributedRenderer:
             self.all_rows = [torch.from_numpy(strip_rows(r, self.world, height, strip)).to(device)
                              for r in range(self.world)]
             self.g_accum = [torch.empty_like(self.accum) for _ in range(self.world)]
-            self.g_out = [torch.empty_like(self.out) for _ in range(self.world)]
+            self.g_out = [torch.empty_like(self.out) for _ in range(self.world)] if resolve is None else None
             self.full_accum = torch.zeros((height, width, 4), dtype=torch.float32, device=device)
             self.full_out = torch.zeros((height, width, 4), dtype=torch.uint8, device=device)
 
@@ -92,14 +97,19 @@ class DistributedRenderer:
             return self.accum[: self.n], self.out[: self.n]
         if self.gather_accum:
             self._gather(self.accum, self.g_accum if self.rank == 0 else None)
-        self._gather(self.out, self.g_out if self.rank == 0 else None)
+        if self.resolve is None:
+            self._gather(self.out, self.g_out if self.rank == 0 else None)
         if self.rank != 0:
             return None
         for r in range(self.world):
             rows = self.all_rows[r]
             k = rows.numel()
-            self.assemble(self.g_accum[r][:k] if self.gather_accum else None, self.g_out[r][:k], rows,
-                          self.full_accum if self.gather_accum else None, self.full_out)
+            self.assemble(self.g_accum[r][:k] if self.gather_accum else None,
+                          None if self.resolve is not None else self.g_out[r][:k], rows,
+                          self.full_accum if self.gather_accum else None,
+                          None if self.resolve is not None else self.full_out)
+        if self.resolve is not None:
+            self.resolve(self.full_accum, self.full_out)
         return self.full_accum, self.full_out
 
     def _gather(self, band, glist):
@@ -129,3 +139,10 @@ def hip_assembler(renderer, stream=None):
         if rows.numel():
             renderer.scatter_rows(band_accum, band_out, rows, full_accum, full_out, stream=stream)
     return assemble
+
+
+def hip_resolver(renderer, spp: int, stream=None):
+    """resolve backed by rt_resolve_rgba8 (device kernel, the trace kernel's own pixel store)."""
+    def resolve(full_accum, full_out):
+        renderer.resolve_rgba8(full_accum, spp, full_out, stream=stream)
+    return resolve

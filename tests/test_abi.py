@@ -18,20 +18,34 @@ def rtvk():
     return m
 
 
-def declared_functions():
-    text = (ROOT / "include" / "rt_mi355x.h").read_text()
+def declared_functions(header="rt_mi355x.h"):
+    text = (ROOT / "include" / header).read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"^\s*(?:[A-Za-z_][\w\s\*]*?)\b(rt_\w+|ray_trace)\s*\(", text, flags=re.M)))
 
 
-def test_exports_every_declared_symbol(rtvk):
+@pytest.mark.parametrize("header", ["rt_mi355x.h", "rt_mi355x_debug.h"])
+def test_exports_every_declared_symbol(rtvk, header):
+    """Both headers' functions are exported by the one library and bound in rtvk.abi; the
+    drop-in header (what replaces src/ray_trace.h) declares no diagnostic entry point, the debug
+    header declares only those."""
     from rtvk import abi
     lib = ctypes.CDLL(str(abi.LIB_PATH))
-    names = declared_functions()
-    assert "ray_trace" in names and "rt_render_device" in names and len(names) >= 15
+    names = declared_functions(header)
+    if header == "rt_mi355x.h":
+        assert "ray_trace" in names and "rt_render_device" in names and len(names) >= 15
+        assert not [n for n in names if n.startswith("rt_debug_")]
+    else:
+        assert len(names) >= 15 and all(n.startswith("rt_debug_") for n in names)
     for n in names:
         assert hasattr(lib, n), n
         assert n in abi.EXPORTS, f"{n} missing from the Python binding table"
+
+
+def test_binding_table_has_no_undeclared_symbol():
+    from rtvk import abi
+    declared = set(declared_functions("rt_mi355x.h")) | set(declared_functions("rt_mi355x_debug.h"))
+    assert set(abi.EXPORTS) == declared
 
 
 def test_ray_trace_signature_matches_reference(rtvk):

@@ -33,7 +33,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_path, rng_mode=0):
+def _worker(rank, world, port, out_path, rng_mode=0, resolve_on_root=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle import oracle
@@ -51,9 +51,15 @@ def _worker(rank, world, port, out_path, rng_mode=0):
 
     def assemble(band_accum, band_out, rows, full_accum, full_out):
         full_accum[rows.long()] = band_accum
-        full_out[rows.long()] = band_out
+        if full_out is not None:
+            full_out[rows.long()] = band_out
 
-    dr = DistributedRenderer(W, H, torch.device("cpu"), render_band, assemble)
+    def resolve(full_accum, full_out):   # rank 0 tonemaps the gathered accumulator once
+        full_out.copy_(torch.from_numpy(oracle.resolve(full_accum.numpy(), SPP)))
+
+    dr = DistributedRenderer(W, H, torch.device("cpu"), render_band, assemble,
+                             resolve=resolve if resolve_on_root else None)
+    assert (dr.g_out is None) == resolve_on_root if rank == 0 else True
     res = dr.step()
     if rank == 0:
         np.savez(out_path, accum=res[0].numpy(), rgba8=res[1].numpy())
@@ -63,13 +69,16 @@ def _worker(rank, world, port, out_path, rng_mode=0):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,rng_mode", [(2, 0), (2, 2), (3, 2)])
-def test_gather_reassembly(tmp_path, oracle, world, rng_mode):
+@pytest.mark.parametrize("world,rng_mode,resolve_on_root", [(2, 0, True), (2, 2, True), (3, 2, True), (2, 2, False)])
+def test_gather_reassembly(tmp_path, oracle, world, rng_mode, resolve_on_root):
     """Strips on `world` gloo ranks, gathered and reassembled on rank 0, equal the one-device
-    frame bit for bit, for the reference stream (rng_mode 0) and the counter-based stream (2)."""
+    frame bit for bit, for the reference stream (rng_mode 0) and the counter-based stream (2):
+    accumulators gathered and tonemapped once on rank 0 (the default of the bench path), or both
+    images gathered."""
     port = _free_port()
     out = str(tmp_path / "img.npz")
-    mp.start_processes(_worker, args=(world, port, out, rng_mode), nprocs=world, join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(world, port, out, rng_mode, resolve_on_root), nprocs=world, join=True,
+                       start_method="spawn")
     got = np.load(out)
     ref_a, ref_o, _ = oracle.render(oracle.generate_scene(), oracle.render_call_info(SPP, W, H), W, H,
                                     opts=oracle.options(rng_mode=rng_mode))

@@ -479,28 +479,47 @@ def test_multi_renderer_rccl(rtvk, torch, oracle, rng_mode):
 
 @pytest.mark.parametrize("rng_mode", [COUNTER, HASH])
 def test_multi_renderer_accumulate(rtvk, torch, oracle, rng_mode):
-    """rt_multi accumulation: each frame adds its samples (sample_base) to the previous frame's sum,
-    whether the previous frame went straight into the caller's buffer (one device holding every
-    row), the next one accumulates into that buffer or into another one (the sum then continues
-    from the launch's band), and again into the other one: every frame equals the oracle's."""
+    """rt_multi accumulation adds the frame's samples (sample_base) to what the caller's accum
+    buffer holds, at every device count (rt_render_device's semantics for the whole image): into
+    the same buffer, into another buffer the caller copied the sum to, and, after the first
+    buffers are freed, into a new buffer holding a sum the caller changed. The library keeps no
+    pointer to an earlier frame's buffer (the direct frame used to keep reading it)."""
     W, H = 40, 27
     sc = oracle.generate_scene()
     rci_np = oracle.render_call_info(2, W, H)
     rci = rtvk.RenderCallInfo.from_buffer_copy(rci_np.tobytes())
-    bufs = [(torch.zeros((H, W, 4), dtype=torch.float32, device="cuda:0"),
-             torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda:0")) for _ in range(2)]
-    prev = None
+
+    def pair():
+        return (torch.zeros((H, W, 4), dtype=torch.float32, device="cuda:0"),
+                torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda:0"))
+
+    def check(acc, out, prev, k):
+        torch.cuda.synchronize()
+        ra, ro, _ = oracle.render(sc, rci_np, W, H, accum=prev, opts=oracle.options(
+            rng_mode=rng_mode, accumulate=int(k > 0), sample_base=2 * k))
+        assert_same(acc.cpu().numpy(), out.cpu().numpy(), ra, ro)
+        return ra
+
     with rtvk.MultiRenderer(8) as m:
         m.set_scene(sc)
-        for k, b in enumerate([0, 0, 1, 1]):   # frame k into buffer pair b
-            acc, out = bufs[b]
-            m.render(rci, acc, out, options=rtvk.make_options(rng_mode=rng_mode, accumulate=k > 0,
-                                                               sample_base=2 * k))
-            torch.cuda.synchronize()
-            ra, ro, _ = oracle.render(sc, rci_np, W, H, accum=prev, opts=oracle.options(
-                rng_mode=rng_mode, accumulate=int(k > 0), sample_base=2 * k))
-            assert_same(acc.cpu().numpy(), out.cpu().numpy(), ra, ro)
-            prev = ra
+        opt = lambda k: rtvk.make_options(rng_mode=rng_mode, accumulate=k > 0, sample_base=2 * k)   # noqa: E731
+        a0, o0 = pair()
+        m.render(rci, a0, o0, options=opt(0))
+        prev = check(a0, o0, None, 0)
+        m.render(rci, a0, o0, options=opt(1))                      # same buffer
+        prev = check(a0, o0, prev, 1)
+        a1, o1 = pair()
+        a1.copy_(a0)                                               # the caller moves the sum
+        m.render(rci, a1, o1, options=opt(2))
+        prev = check(a1, o1, prev, 2)
+        del a0, o0, a1, o1
+        torch.cuda.empty_cache()
+        a2, o2 = pair()
+        changed = (prev * np.float32(0.5)).astype(np.float32)     # a running sum the caller edited
+        changed[..., 3] = 1.0
+        a2.copy_(torch.from_numpy(changed))
+        m.render(rci, a2, o2, options=opt(3))
+        check(a2, o2, changed, 3)
 
 
 # ---- full size --------------------------------------------------------------------------------
@@ -681,14 +700,15 @@ def test_scene_swap_between_queued_frames(rtvk, renderer, torch, oracle):
         assert_same(a.cpu().numpy(), o.cpu().numpy(), ra, ro)
 
 
-@pytest.mark.parametrize("rng_mode", [STREAM, HASH])
-def test_strips_rccl_world1(rtvk, renderer, torch, oracle, rng_mode):
+@pytest.mark.parametrize("rng_mode,resolve", [(STREAM, True), (HASH, True), (HASH, False)])
+def test_strips_rccl_world1(rtvk, renderer, torch, oracle, rng_mode, resolve):
     """bench.py's N > 1 path (rtvk.dist.DistributedRenderer: row strips per rank, torch.distributed
-    gathers over RCCL, rt_scatter_rows on rank 0) on a one-rank NCCL group: the frame equals the
+    gathers over RCCL, rt_scatter_rows on rank 0, rgba8 resolved from the gathered accumulator by
+    rt_resolve_rgba8 — or both images gathered) on a one-rank NCCL group: the frame equals the
     one-GPU oracle frame bit for bit."""
     import socket
     import torch.distributed as dist
-    from rtvk.dist import DistributedRenderer, hip_assembler, hip_band_renderer
+    from rtvk.dist import DistributedRenderer, hip_assembler, hip_band_renderer, hip_resolver
     W, H, spp = 80, 48, 3
     sc = oracle.generate_scene()
     renderer.set_scene(sc)
@@ -701,7 +721,8 @@ def test_strips_rccl_world1(rtvk, renderer, torch, oracle, rng_mode):
     try:
         dr = DistributedRenderer(W, H, torch.device("cuda", 0),
                                  hip_band_renderer(renderer, rci, rtvk.make_options(rng_mode=rng_mode)),
-                                 hip_assembler(renderer), force_gather=True)
+                                 hip_assembler(renderer), force_gather=True,
+                                 resolve=hip_resolver(renderer, spp) if resolve else None)
         acc, out = dr.step()
         torch.cuda.synchronize()
     finally:
@@ -863,6 +884,37 @@ def test_render_streams_alternate_on_one_context(rtvk, torch, oracle):
             r.render_device(rci_c, a, o, options=rtvk.make_options(), stream=streams[k % 2])
         torch.cuda.synchronize()
         for a, o in bufs:
+            assert_same(a.cpu().numpy(), o.cpu().numpy(), ra, ro)
+
+
+@pytest.mark.parametrize("refit", [False, True])
+def test_device_build_between_streams(rtvk, torch, oracle, refit):
+    """A render on stream A, then a device-built scene (its build runs on the context's build
+    stream beside the render), then a render on stream B: the second render must
+    wait for the first one too (it reuses the context's counters, tile costs and big-sphere table),
+    not only for the build. Both frames equal the oracle's; then the same with the
+    streams swapped."""
+    W, H, spp = 128, 64, 1024   # frame 0 runs ~1 ms on the GPU: longer than the build beside it
+    scs = [oracle.generate_scene(t) for t in (0.0, 0.7, 1.9)]
+    rci = oracle.render_call_info(spp, W, H)
+    rci_c = rtvk.RenderCallInfo.from_buffer_copy(rci.tobytes())
+    refs = [oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=HASH), threads=16)[:2] for sc in scs]
+    with rtvk.Renderer(0) as r:
+        sa, sb = torch.cuda.Stream(), torch.cuda.Stream()
+        bufs = [(torch.zeros((H, W, 4), dtype=torch.float32, device="cuda"),
+                 torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")) for _ in range(3)]
+        dev_scs = [torch.from_numpy(sc).cuda() for sc in scs]
+        torch.cuda.synchronize()
+        opt = rtvk.make_options(rng_mode=HASH, accel=LBVH)
+        r.set_scene_device(dev_scs[0], stream=sa)
+        r.render_device(rci_c, *bufs[0], options=opt, stream=sa)
+        r.set_scene_device(dev_scs[1], refit=refit, stream=sa)       # build beside frame 0
+        r.render_device(rci_c, *bufs[1], options=opt, stream=sb)    # frame 1 on the other stream
+        r.set_scene_device(dev_scs[2], refit=refit, stream=sb)
+        r.render_device(rci_c, *bufs[2], options=opt, stream=sa)
+        torch.cuda.synchronize()
+        assert r.scene_array(8)["device_built"]
+        for (a, o), (ra, ro) in zip(bufs, refs):
             assert_same(a.cpu().numpy(), o.cpu().numpy(), ra, ro)
 
 
