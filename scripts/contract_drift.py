@@ -55,6 +55,40 @@ def render3(sc, rci, w, h, rows, rng, threads):
     return out
 
 
+def sweep(args, sc) -> int:
+    """PSNR of the reference stream (identical seed) against the GLSL read literally, per spp: where
+    the north star's 50-dB bar starts to hold."""
+    W, H = 1920, 1080
+    rows_per_block = args.rows
+    ys = np.linspace(0, H - rows_per_block, args.blocks).round().astype(int)
+    out = {"what": "config 3 blocks (1920x1080 frame, canonical scene), reference per-pixel LCG stream at the "
+                   "reference's seed: the contract (= the kernel, bit for bit) against shader.rint:46-55 as written "
+                   "(rint) and every dot / normalize as written too (all)", "rows": {}}
+    for spp in [int(v) for v in args.sweep.split(",")]:
+        px = int(min(W * rows_per_block * args.blocks, max(1536, args.budget / spp)))
+        bw = max(1, min(W, px // (args.blocks * rows_per_block)))
+        xs = np.linspace(0, W - bw, args.blocks).round().astype(int)[::-1]
+        parts = {k: [] for k in ("contract", "rint", "all")}
+        t0 = time.perf_counter()
+        for y, x in zip(ys, xs):
+            rows = np.arange(y, y + rows_per_block, dtype=np.uint32)
+            r = render3(sc, oracle.render_call_info(spp, W, H, (int(x), 0)), bw, rows_per_block, rows, 0, args.threads)
+            for k in parts:
+                parts[k].append(r[k][:2])
+        cat = {k: (np.concatenate([p[0] for p in v]), np.concatenate([p[1] for p in v])) for k, v in parts.items()}
+        out["rows"][spp] = {"pixels": int(args.blocks * rows_per_block * bw),
+                            "blocks": f"{args.blocks} blocks of {rows_per_block} rows x {bw} px",
+                            "rint_literal": compare(*cat["rint"], *cat["contract"]),
+                            "all_literal": compare(*cat["all"], *cat["contract"]),
+                            "cpu_s": round(time.perf_counter() - t0, 1)}
+        print(f"{spp} spp: {out['rows'][spp]['pixels']} px, rint {out['rows'][spp]['rint_literal']['psnr_db']} dB, "
+              f"all {out['rows'][spp]['all_literal']['psnr_db']} dB", flush=True)
+    print(json.dumps(out, indent=1))
+    if args.out:
+        Path(args.out).write_text(json.dumps(out, indent=1) + "\n")
+    return 0
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--blocks", type=int, default=8)
@@ -63,9 +97,16 @@ def main() -> int:
     ap.add_argument("--spp", type=int, default=10000)
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 1)
     ap.add_argument("--out", default=None, help="also write the JSON here")
+    ap.add_argument("--sweep", default=None,
+                    help="spp list (e.g. 64,256,1000,10000): the reference stream at the identical seed against "
+                         "both literal forms on config 3's blocks at each spp, the block width scaled so every spp "
+                         "renders about --budget samples per form")
+    ap.add_argument("--budget", type=float, default=2.4e7)
     args = ap.parse_args()
     oracle.build()
     sc = oracle.generate_scene(0.0)
+    if args.sweep:
+        return sweep(args, sc)
     res = {}
     # (1) config 3 blocks, counter-based stream (the bench's stream), spread like bench.py's cpu_baseline
     W, H = 1920, 1080

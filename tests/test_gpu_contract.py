@@ -26,26 +26,64 @@ def test_config3_full_frame_grid_equals_lbvh(rtvk, renderer, torch, oracle, rng_
     assert (st.segments, st.samples) == (st2.segments, st2.samples) and st.samples == W * H * spp
 
 
-@pytest.mark.parametrize("rng_mode,min_psnr", [(HASH, 50.0), (STREAM, 40.0)])
-def test_kernel_vs_literal_glsl(rtvk, renderer, torch, oracle, rng_mode, min_psnr):
+# rgba8 PSNR floors against (LIT_RINT, LIT_ALL) at 320x180 / 64 spp: the measured value minus 1 dB
+# (deterministic: kernel = contract oracle bit for bit; profiles/r03_contract_drift.json: hash 58.7 /
+# 54.5 dB, reference stream 45.6 / 42.8 dB)
+LIT_FLOORS_64SPP = {HASH: (57.7, 53.5), STREAM: (44.6, 41.8)}
+
+
+@pytest.mark.parametrize("rng_mode", [HASH, STREAM])
+def test_kernel_vs_literal_glsl(rtvk, renderer, torch, oracle, rng_mode):
     """Contract drift: the kernel is bit-exact to the shipped contract; against
     the oracle's literal readings of the GLSL (shader.rint:46-55 with unfused D and a true / a;
     then every dot / normalize as written) it differs only where rounding flips a branch. At
-    320x180, 64 spp the rgba8 PSNR stays above the floor (hash stream: a flipped branch changes
-    one sample; reference stream: it changes the rest of the pixel's chain)."""
+    320x180, 64 spp the rgba8 PSNR stays above the measured value minus 1 dB (hash stream: a
+    flipped branch changes one sample; reference stream: it changes the rest of the pixel's chain,
+    which is why this low-spp regime sits below 50 dB there)."""
     W, H, spp = 320, 180, 64
     sc = oracle.generate_scene()
     rci = oracle.render_call_info(spp, W, H)
     a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH, rng_mode=rng_mode)
     ca, co, _ = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=rng_mode), threads=16)
     assert_same(a, o, ca, co)
-    for lit in (oracle.LIT_RINT, oracle.LIT_ALL):
+    for lit, min_psnr in zip((oracle.LIT_RINT, oracle.LIT_ALL), LIT_FLOORS_64SPP[rng_mode]):
         la, lo, _ = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=rng_mode, lit=lit), threads=16)
         same = np.all(a[..., :3] == la[..., :3], axis=-1).mean()
         mse = np.mean((o[..., :3].astype(np.float64) - lo[..., :3]) ** 2)
         psnr = 10 * np.log10(255 ** 2 / mse)
         print(f"rng {rng_mode} lit {lit}: {same:.4f} of accumulator texels bit-identical, rgba8 PSNR {psnr:.2f} dB")
         assert psnr >= min_psnr and same > 0.7
+
+
+# Where the 50-dB identical-seed bar starts to hold in the reference stream (DESIGN.md §3.2,
+# scripts/contract_drift.py --sweep, profiles/r05_contract_drift_sweep.json): config 3's blocks at
+# 256 spp measure 51.70 / 49.13 dB against (LIT_RINT, LIT_ALL), at 512 spp 53.92 / 51.59 dB.
+# Floors: measured minus 1 dB.
+@pytest.mark.parametrize("spp,bw,floors", [(256, 1464, (50.7, 48.1)), (512, 732, (52.9, 50.6))])
+def test_reference_stream_drift_threshold(rtvk, renderer, torch, oracle, spp, bw, floors):
+    """The kernel's reference-stream pixels (identical seed) of config 3's frame, 8 blocks of 8 rows
+    x bw px (the drift sweep's blocks), are the contract oracle's bit for bit, and their PSNR
+    against the literal readings of the GLSL is the sweep's: >= 50 dB against LIT_RINT from 256
+    spp, against LIT_ALL from 512 spp."""
+    W, H = 1920, 1080
+    sc = oracle.generate_scene()
+    ys = np.linspace(0, H - 8, 8).round().astype(int)
+    xs = np.linspace(0, W - bw, 8).round().astype(int)[::-1]
+    got, ref = [], {k: [] for k in ("contract", "rint", "all")}
+    for y, x in zip(ys, xs):
+        rows = np.arange(y, y + 8, dtype=np.uint32)
+        rci = oracle.render_call_info(spp, W, H, (int(x), 0))
+        got.append(gpu_render(rtvk, renderer, torch, sc, rci, bw, 8, rows=rows, accel=LBVH, rng_mode=STREAM)[:2])
+        for name, lit in (("contract", oracle.LIT_CONTRACT), ("rint", oracle.LIT_RINT), ("all", oracle.LIT_ALL)):
+            ref[name].append(oracle.render(sc, rci, bw, 8, rows=rows, opts=oracle.options(rng_mode=STREAM, lit=lit),
+                                           threads=16)[:2])
+    ga, go = np.concatenate([g[0] for g in got]), np.concatenate([g[1] for g in got])
+    assert_same(ga, go, np.concatenate([r[0] for r in ref["contract"]]), np.concatenate([r[1] for r in ref["contract"]]))
+    for name, floor in zip(("rint", "all"), floors):
+        lo = np.concatenate([r[1] for r in ref[name]])
+        psnr = 10 * np.log10(255 ** 2 / np.mean((go[..., :3].astype(np.float64) - lo[..., :3]) ** 2))
+        print(f"{spp} spp, literal {name}: rgba8 PSNR {psnr:.2f} dB")
+        assert psnr >= floor
 
 
 def _blocks(W, H, n_blocks, rows, width):
