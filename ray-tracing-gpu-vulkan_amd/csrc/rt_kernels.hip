@@ -795,53 +795,6 @@ __device__ __forceinline__ bool shade_rec(const rt::TraceParams& P, const Camera
             UTIL(4, true);
             sd = add(n, ru);
             if (fabsf(sd.x) < 1e-8f && fabsf(sd.y) < 1e-8f && fabsf(sd.z) < 1e-8f) sd = n;
-#ifdef RT_SPEC_MERGED
-        } else if (mtype <= 2u) {
-            // A/B variant: metal and dielectric in ONE specular region, so a
-            // wave holding both pays one divergent region instead of two. Shared: dn = dot(n, d)
-            // (the dielectric's cos_t is -dn exactly: negation commutes with every rounding),
-            // reflect(d, n), and the first correctly rounded sqrt — of |v|^2 for metal (its
-            // normalize), of 1 - cos_t^2 for dielectric (canRefract). Same values bit for bit.
-            UTIL(5, true);
-            const bool metal = mtype == 1u;
-            const float dn = dot(n, d);
-            const V3 refl = reflect(d, n);
-            const V3 v = add(refl, scale(m0.w, ru));           // metal: reflect + fuzz * unit
-            const float t1 = 1.0f - dn * dn;                    // dielectric: 1 - cos_t^2
-            const float q = sqrt_cr(metal ? dot(v, v) : t1);
-            if (metal) {
-                const float inv = rcp_cr(q);
-                const V3 sc = v3(v.x * inv, v.y * inv, v.z * inv);
-                if (dot(sc, n) > 0.0f) sd = sc;
-            } else {
-                UTIL(6, true);
-                float eta, r;
-                if (tt & rt::kMatDielConst) {
-                    eta = front ? m1.x : m0.w;
-                    r = front ? m1.y : m1.z;
-                } else {
-                    eta = front ? (1.0f / m0.w) : m0.w;
-                    const float qq = (1.0f - eta) / (1.0f + eta);
-                    r = qq * qq;
-                }
-                bool refracts = false;
-                if (eta * q <= 1.0f) {
-                    const float rf = r + (1.0f - r) * pow5(1.0f + dn);   // 1 - cos_t
-                    refracts = rf < rnd(ps.seed);
-                }
-                sd = refl;
-                if (refracts) {   // GLSL refract(d, n, eta) with d' = dot(n, d) = dn
-                    const float k = 1.0f - eta * eta * t1;
-                    if (k < 0.0f) {
-                        sd = v3(0.0f, 0.0f, 0.0f);
-                    } else {
-                        const float s = eta * dn + sqrt_cr(k);
-                        sd = sub(scale(eta, d), scale(s, n));
-                    }
-                }
-            }
-        }
-#else
         } else if (mtype == 1u) {                // metal, shader.rchit:78-89
             UTIL(5, true);
             const V3 refl = reflect(d, n);
@@ -869,7 +822,6 @@ __device__ __forceinline__ bool shade_rec(const rt::TraceParams& P, const Camera
             }
             sd = refracts ? refract(d, n, eta) : reflect(d, n);
         }
-#endif
         scatter = !(sd.x == 0.0f && sd.y == 0.0f && sd.z == 0.0f);  // shader.rchit:48
     }
     // shader.rgen:77-88
@@ -1002,13 +954,6 @@ struct Ray {
     float best;
     uint32_t bi;           // closest so far
     bool walk;             // the segment has a tree to walk
-#ifdef RT_C5_ENTRY_EARLY
-    // A/B variant (L2 grid): the entry cell's offsets, loaded before the big-sphere tests so their
-    // L2 round trip runs under that VALU work; tn / tf0: the grid box's entry and exit before the
-    // cull limit (tf = min(tf0, limit)).
-    float etn, etf0;
-    uint32_t eb, ee;
-#endif
 };
 constexpr uint32_t END = 0xffffffffu;
 
@@ -1069,37 +1014,11 @@ __device__ __forceinline__ uint32_t octant(const V3 d) {
     return (__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 31) << 1) | ((__float_as_uint(d.z) >> 31) << 2);
 }
 
-#ifdef RT_C5_ENTRY_EARLY
-// Entry cell of the grid walk (the L2 grid): as grid_walk computes it, with tf before the limit.
-__device__ __forceinline__ int grid_cell_of(const rt::GridInfo& G, float p, int k) {
-    const int c = int(floorf((p - G.gmin[k]) * G.inv_cs[k]));
-    return min(max(c, 0), int(G.n[k]) - 1);
-}
-__device__ __forceinline__ void grid_entry_early(const rt::TraceParams& P, Ray& r) {
-    const rt::GridInfo& G = P.grid;
-    const float x0 = (G.lo_m[0] - r.o.x) * r.inv.x, x1 = (G.hi_m[0] - r.o.x) * r.inv.x;
-    const float y0 = (G.lo_m[1] - r.o.y) * r.inv.y, y1 = (G.hi_m[1] - r.o.y) * r.inv.y;
-    const float z0 = (G.lo_m[2] - r.o.z) * r.inv.z, z1 = (G.hi_m[2] - r.o.z) * r.inv.z;
-    r.etn = fmaxf(fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1)), T_MIN);
-    r.etf0 = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1));
-    const int cx = grid_cell_of(G, __builtin_fmaf(r.etn, r.d.x, r.o.x), 0);
-    const int cy = grid_cell_of(G, __builtin_fmaf(r.etn, r.d.y, r.o.y), 1);
-    const int cz = grid_cell_of(G, __builtin_fmaf(r.etn, r.d.z, r.o.z), 2);
-    const uint32_t cell = (uint32_t(cz) * G.n[1] + uint32_t(cy)) * G.n[0] + uint32_t(cx);
-    r.eb = P.cell_start[cell];   // a clamped cell: always inside the offsets array
-    r.ee = P.cell_start[cell + 1];
-}
-#endif
-
 // New segment: hoisted per-ray terms and the exhaustive big spheres.
-template <bool ENTRY = false>
 __device__ __forceinline__ void setup_ray(const rt::TraceParams& P, Ray& r, uint32_t& n_sph) {
     r.a = dot(r.d, r.d);
     r.ia = rcp_cr(r.a);
     r.inv = v3(rcp_cr(r.d.x), rcp_cr(r.d.y), rcp_cr(r.d.z));
-#ifdef RT_C5_ENTRY_EARLY
-    if (ENTRY) grid_entry_early(P, r);
-#endif
     // closest so far: none, with t <= tMax (shader.rint:32-39 reports t <= tMax). The walks accept
     // (t <= best, lowest id on ties), so best = 10000 exactly accepts a report at tMax and nothing
     // beyond it, and the (t bits, id) keys of the cooperative walk order the same way.
@@ -1206,22 +1125,11 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
                                           const float4* __restrict__ rec, const uint32_t* __restrict__ ids,
                                           Ray& r, uint32_t& n_cell, uint32_t& n_sph, uint32_t& n_empty) {
     const rt::GridInfo& G = P.grid;
-#ifdef RT_C5_ENTRY_EARLY
-    float tn = PAIRS ? r.etn : 0.0f;
-    float tf = PAIRS ? fminf(r.etf0, r.limit) : 0.0f;
-    if (!PAIRS) {
-#endif
     const float x0 = (G.lo_m[0] - r.o.x) * r.inv.x, x1 = (G.hi_m[0] - r.o.x) * r.inv.x;
     const float y0 = (G.lo_m[1] - r.o.y) * r.inv.y, y1 = (G.hi_m[1] - r.o.y) * r.inv.y;
     const float z0 = (G.lo_m[2] - r.o.z) * r.inv.z, z1 = (G.hi_m[2] - r.o.z) * r.inv.z;
-#ifdef RT_C5_ENTRY_EARLY
-    tn = fmaxf(fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1)), T_MIN);
-    tf = fminf(fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1)), r.limit);
-    }
-#else
     const float tn = fmaxf(fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1)), T_MIN);
     const float tf = fminf(fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1)), r.limit);
-#endif
     if (!(tn <= tf)) return;
     // entry cell (clamped: a point rounded just outside belongs to the border cell)
     auto cell_of = [&](float p, int k) {
@@ -1244,16 +1152,8 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
     float tz = bound_t(cz, sz, 2, r.o.z, r.inv.z);
     // linear cell index (a step adds the stepped axis's stride, dda_step)
     uint32_t cell = (uint32_t(cz) * G.n[1] + uint32_t(cy)) * G.n[0] + uint32_t(cx);
-#ifdef RT_C5_ENTRY_EARLY
-    bool first = PAIRS;
-#endif
     for (;;) {
-#ifdef RT_C5_ENTRY_EARLY
-        const uint32_t b = first ? r.eb : cstart[cell], e = first ? r.ee : cstart[cell + 1];
-        first = false;
-#else
         const uint32_t b = cstart[cell], e = cstart[cell + 1];
-#endif
         if (COUNT) {
             n_cell++;
             n_empty += b == e ? 1u : 0u;
@@ -1794,7 +1694,7 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
         STAMP(1);
         UTIL(8, st == ST_TRACING);
         const uint32_t box0 = n_box;
-        if (st == ST_TRACING) setup_ray<LAYOUT == LAYOUT_GRID_L2>(P, r, n_sph);
+        if (st == ST_TRACING) setup_ray(P, r, n_sph);
         STAMP(2);
         if constexpr (LAYOUT == LAYOUT_GRID_COOP) {   // every lane of the wave takes part (tracing or not)
             grid_walk_coop<COUNT>(P, reinterpret_cast<const uint32_t*>(nodes4), leaf4, leaf_ids, r, st == ST_TRACING,
