@@ -420,9 +420,10 @@ def animated_line(dev, W: int, H: int, spp: int, grid: int, rng_mode: int, frame
 def cold_call_line(W: int, H: int, spp: int, timeout_s: int = 300) -> dict:
     """One cold call of the drop-in entry point, ray_trace(spp, false, W, H, 1) (src/ray_trace.h:9-15),
     in a fresh child process with the counter-based stream (RT_RNG=hash, the headline's): HIP
-    runtime start, the RCCL communicator, the context, the canonical scene's build, one frame
-    without LPT history, the resolve and the teardown. `call_s` is the wall time around the call;
-    `frame_ms` is the frame time the library itself prints (duration_per_frame)."""
+    runtime start, the devices and streams (no RCCL communicator for one device), the context, the
+    canonical scene's build, one frame without LPT history, the resolve and the teardown. `call_s`
+    is the wall time around the call; `frame_ms` is the frame time the library itself prints
+    (duration_per_frame), `create_ms` / `scene_ms` the setup it prints."""
     import re
     import subprocess
     from rtvk import abi
@@ -442,14 +443,18 @@ def cold_call_line(W: int, H: int, spp: int, timeout_s: int = 300) -> dict:
     proc_s = time.perf_counter() - t0
     call = re.search(r"CALL_S ([0-9.eE+-]+)", p.stdout)
     fr = re.search(r"duration_per_frame: ([0-9.]+) ms", p.stdout)
+    su = re.search(r"setup: [^0-9]*([0-9.]+) ms, scene build \+ upload ([0-9.]+) ms", p.stdout)
     if p.returncode != 0 or not call or not fr:
         return {"error": f"exit {p.returncode}", "stdout": p.stdout[-400:], "stderr": p.stderr[-400:]}
     call_s, frame_ms = float(call.group(1)), float(fr.group(1))
+    parts = {"create_ms": float(su.group(1)), "scene_ms": float(su.group(2))} if su else {}
     return {"call_s": round(call_s, 4), "frame_ms": round(frame_ms, 3), "setup_s": round(call_s - frame_ms / 1e3, 4),
+            **parts,
             "child_process_s": round(proc_s, 3),
             "value": round(W * H * spp / call_s / 1e6, 2), "unit": "Msamples/s",
-            "what": f"ray_trace({spp}, false, {W}, {H}, 1) in a fresh process, RT_RNG=hash: HIP start, RCCL "
-                    "communicator, context, scene build, first frame (no LPT history), resolve, teardown"}
+            "what": f"ray_trace({spp}, false, {W}, {H}, 1) in a fresh process, RT_RNG=hash: HIP start, "
+                    "devices and streams (create_ms), the canonical scene's build and upload (scene_ms), the first "
+                    "frame without LPT history (frame_ms), teardown"}
 
 
 def env_knobs() -> dict:
@@ -778,8 +783,11 @@ def main() -> int:
         walk = "brute-force sphere list (scalar cache)" if form == "brute" else WALK_NAMES.get(form, (form, form))[1]
         if mode == "multi":
             par = (f"rt_multi (C-ABI, one process): {multi_info['devices']} GPUs, {multi_info['strip_rows']}-row "
-                   f"strips dealt round robin, RCCL grouped ncclSend/ncclRecv gather of every strip to GPU 0 "
-                   f"(ncclCommInitAll communicator of {multi_info['rccl_ranks']} ranks) + device reorder")
+                   f"strips dealt round robin, "
+                   + (f"RCCL grouped ncclSend/ncclRecv gather of every other GPU's accumulator strips to GPU 0 "
+                      f"(ncclCommInitAll communicator of {multi_info['rccl_ranks']} ranks) + device reorder + "
+                      f"resolve on GPU 0" if multi_info["devices"] > 1 else
+                      "one GPU renders straight into the caller's buffers (no communicator, no collective)"))
         elif mode == "per-process":
             par = (f"torch.distributed ({backend}): {world} processes, one per GPU, 8-row strips round robin + "
                    f"gather to rank 0 + device reorder")

@@ -388,9 +388,14 @@ int rt_multi_create(uint32_t gpu_count, rt_multi** out) {
             RT_HIP(hipEventCreateWithFlags(&m->ev_in, hipEventDisableTiming));
             RT_HIP(hipEventCreateWithFlags(&m->ev_out, hipEventDisableTiming));
         }
-        std::vector<int> devs(m->n);
-        for (uint32_t d = 0; d < m->n; d++) devs[d] = int(d);
-        RT_NCCL(ncclCommInitAll(m->comm.data(), int(m->n), devs.data()));
+        // A single device's frame plan holds no send or receive (tests/test_multi_plan.py), so
+        // one device needs no communicator: the drop-in ray_trace(..., 1) does not pay RCCL's
+        // initialisation on its cold call.
+        if (m->n > 1) {
+            std::vector<int> devs(m->n);
+            for (uint32_t d = 0; d < m->n; d++) devs[d] = int(d);
+            RT_NCCL(ncclCommInitAll(m->comm.data(), int(m->n), devs.data()));
+        }
         return RT_OK;
     };
     int rc;
@@ -495,8 +500,8 @@ int rt_debug_multi_plan(uint32_t n_devices, uint32_t width, uint32_t height, con
 
 int rt_multi_info(const rt_multi* m, uint32_t* out4) {
     if (!m || !out4) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
-    int ranks = 0;
-    RT_NCCL(ncclCommCount(m->comm[0], &ranks));
+    int ranks = 0;   // 0: one device, no communicator
+    if (m->comm[0]) RT_NCCL(ncclCommCount(m->comm[0], &ranks));
     uint32_t launches = 0;
     for (const Launch& l : m->launches) launches += l.rows.empty() ? 0u : 1u;
     out4[0] = m->n;
@@ -626,14 +631,20 @@ int rt_render(const Sphere* spheres, uint32_t sphere_count, const RenderCallInfo
 // parameter for it, so the selection travels out of band).
 void ray_trace(uint32_t samples, bool storeRenderResult, uint32_t width, uint32_t height, uint32_t gpu_count) {
     auto report = [](const char* what) { std::fprintf(stderr, "ray_trace: %s: %s\n", what, rt::g_last_error.c_str()); };
+    using clk = std::chrono::steady_clock;
+    auto ms_since = [](clk::time_point t) { return std::chrono::duration<double, std::milli>(clk::now() - t).count(); };
     try {
+        const auto t_c = clk::now();
         rt_multi* m = nullptr;
         if (rt_multi_create(gpu_count, &m)) return report("rt_multi_create");
         std::unique_ptr<rt_multi, int (*)(rt_multi*)> guard(m, rt_multi_destroy);
+        const double create_ms = ms_since(t_c);
+        const auto t_s = clk::now();
         std::vector<Sphere> scene(488);
         uint32_t cnt = 0;
         rt_generate_scene(0.0f, 11, scene.data(), uint32_t(scene.size()), &cnt);
         if (rt_multi_set_scene(m, scene.data(), cnt)) return report("rt_multi_set_scene");
+        const double scene_ms = ms_since(t_s);
         RenderCallInfo rci;
         rt_canonical_render_call_info(samples, width, height, &rci);
         rt_options opt;
@@ -673,6 +684,8 @@ void ray_trace(uint32_t samples, bool storeRenderResult, uint32_t width, uint32_
         std::printf("duration_per_frame: %.3f ms (%u GPU, %s stream, %llu samples, %.1f Msamples/s incl. first-launch setup)\n",
                     sec * 1e3, m->n, opt.rng_mode == RT_RNG_SAMPLE_HASH ? "hash" : "reference",
                     (unsigned long long)st.samples, double(st.samples) / sec / 1e6);
+        std::printf("setup: devices + streams%s %.1f ms, scene build + upload %.1f ms\n",
+                    m->n > 1 ? " + RCCL communicator" : "", create_ms, scene_ms);
         if (storeRenderResult && rt_store_ppm("render.ppm", img.data(), width, height)) report("store");
     } catch (const std::exception& e) {
         std::fprintf(stderr, "ray_trace: %s\n", e.what());

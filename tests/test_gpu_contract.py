@@ -213,7 +213,8 @@ def test_build_provenance(rtvk):
 
 def test_multi_renderer_reports_communicator(rtvk, torch, oracle):
     """rt_multi_info: the RCCL communicator's own rank count (ncclCommCount) equals the devices
-    rt_multi opened, and the last frame's launches / per-device kernel times are reported."""
+    rt_multi opened (0 for one device, which needs no communicator), and the last frame's launches /
+    per-device kernel times are reported."""
     n = torch.cuda.device_count()
     with rtvk.MultiRenderer(n) as m:
         m.set_scene(oracle.generate_scene())
@@ -223,7 +224,8 @@ def test_multi_renderer_reports_communicator(rtvk, torch, oracle):
         m.render(rtvk.canonical_render_call_info(2, W, H), acc, out, options=rtvk.make_options(rng_mode=HASH))
         torch.cuda.synchronize()
         info = m.info()
-        assert info["devices"] == n and info["rccl_ranks"] == n and info["strip_rows"] == 8
+        # one device holds no communicator (its frame plan has no send or receive)
+        assert info["devices"] == n and info["rccl_ranks"] == (n if n > 1 else 0) and info["strip_rows"] == 8
         assert info["launches"] == min(n, (H + 7) // 8)
         kt = m.kernel_times()
         assert len(kt) == info["launches"] and all(k > 0 for k in kt)
