@@ -182,11 +182,21 @@ __device__ __forceinline__ float4 lds_reload(const float4* p) {
 // (config 3 -3.1 %, reference stream -2.9 %, config 5 -1.3 %).
 __shared__ float4 s_walk_axis[3];   // (cs[k], gmin[k], stride[k], n[k]): stride and n as uint bits
 __shared__ float2 s_walk_slack;     // (cull_near_abs, cull_abs)
+#ifdef RT_ENTRY_LDS
+// A/B variant: the grid walk's entry parameters (the widened grid box, 1 / cell size, the last
+// cell index per axis) from LDS as well, instead of kernel-argument reloads (s_load + an lgkmcnt(0)
+// wait at every walk's entry) and spilled SGPRs.
+__shared__ float4 s_walk_entry[3];   // per axis: (lo_m, hi_m, inv_cs, n - 1 as uint bits)
+#endif
 __device__ __forceinline__ void stage_walk_params(const rt::TraceParams& P, uint32_t tid) {
     if (tid < 3u) {
         const uint32_t stride = tid == 0u ? 1u : tid == 1u ? P.grid.n[0] : P.grid.n[0] * P.grid.n[1];
         s_walk_axis[tid] = make_float4(P.grid.cs[tid], P.grid.gmin[tid], __uint_as_float(stride),
                                        __uint_as_float(P.grid.n[tid]));
+#ifdef RT_ENTRY_LDS
+        s_walk_entry[tid] = make_float4(P.grid.lo_m[tid], P.grid.hi_m[tid], P.grid.inv_cs[tid],
+                                        __uint_as_float(P.grid.n[tid] - 1u));
+#endif
     }
     if (tid == 3u) s_walk_slack = make_float2(P.cull_near_abs, P.cull_abs);
 }
@@ -1014,16 +1024,37 @@ __device__ __forceinline__ uint32_t octant(const V3 d) {
     return (__float_as_uint(d.x) >> 31) | ((__float_as_uint(d.y) >> 31) << 1) | ((__float_as_uint(d.z) >> 31) << 2);
 }
 
+// Four big spheres (records sb, ids ib; SGPR operands): the discriminants, then a candidate tail
+// per sphere that any lane needs (wave-uniform record: no reload, no per-lane select).
+__device__ __forceinline__ void big_group(Ray& r, const float (&sb)[16], const uint32_t (&ib)[4]) {
+    float bk[4], Dk[4];
+    uint32_t cand = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float rr = sb[4 * k + 3] * sb[4 * k + 3];
+        const float ocx = r.o.x - sb[4 * k], ocy = r.o.y - sb[4 * k + 1], ocz = r.o.z - sb[4 * k + 2];
+        bk[k] = __builtin_fmaf(ocz, r.d.z, __builtin_fmaf(ocy, r.d.y, ocx * r.d.x));
+        const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - rr;
+        Dk[k] = __builtin_fmaf(bk[k], bk[k], -(r.a * c));
+        cand |= (Dk[k] >= 0.0f && !behind(bk[k], c) ? 1u : 0u) << k;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if ((cand >> k) & 1u) {
+            const float sq = sqrt_cr(Dk[k]);
+            float t = (-bk[k] - sq) * r.ia;
+            if (!(t >= T_MIN)) t = (-bk[k] + sq) * r.ia;   // report t1 if t1 >= tmin, else t2
+            const uint32_t id = ib[k];
+            if ((t >= T_MIN) & (t <= r.best) & ((t < r.best) | (id < r.bi))) {
+                r.best = t;
+                r.bi = id;
+            }
+        }
+    }
+}
+
 // New segment: hoisted per-ray terms and the exhaustive big spheres.
 __device__ __forceinline__ void setup_ray(const rt::TraceParams& P, Ray& r, uint32_t& n_sph) {
-    r.a = dot(r.d, r.d);
-    r.ia = rcp_cr(r.a);
-    r.inv = v3(rcp_cr(r.d.x), rcp_cr(r.d.y), rcp_cr(r.d.z));
-    // closest so far: none, with t <= tMax (shader.rint:32-39 reports t <= tMax). The walks accept
-    // (t <= best, lowest id on ties), so best = 10000 exactly accepts a report at tMax and nothing
-    // beyond it, and the (t bits, id) keys of the cooperative walk order the same way.
-    r.best = 10000.0f;
-    r.bi = 0xffffffffu;
     // records and ids through the scalar cache (TraceParams::big_tab, SGPR operands, no LDS round
     // trip: config 3 -1.6 %, reference stream -1.7 %, config 5 -2.2 % against an LDS table); the
     // four discriminants stay in registers for the candidate passes, which run per sphere with a
@@ -1032,34 +1063,38 @@ __device__ __forceinline__ void setup_ray(const rt::TraceParams& P, Ray& r, uint
     typedef const __attribute__((address_space(4))) uint32_t* ConstU;
     const ConstF g = (ConstF)(P.big_tab);
     const ConstU gid = (ConstU)(P.big_tab + 4u * rt::kBigMax);
+#ifdef RT_BIG_EARLY
+    // A/B variant: the first four records and ids are requested before the reciprocals, so the
+    // scalar loads' latency runs under them (the table always holds kBigMax entries: reading the
+    // first four is safe whatever n_big)
+    float sb0[16];
+    uint32_t ib0[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) sb0[k] = g[k];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) ib0[k] = gid[k];
+#endif
+    r.a = dot(r.d, r.d);
+    r.ia = rcp_cr(r.a);
+    r.inv = v3(rcp_cr(r.d.x), rcp_cr(r.d.y), rcp_cr(r.d.z));
+    // closest so far: none, with t <= tMax (shader.rint:32-39 reports t <= tMax). The walks accept
+    // (t <= best, lowest id on ties), so best = 10000 exactly accepts a report at tMax and nothing
+    // beyond it, and the (t bits, id) keys of the cooperative walk order the same way.
+    r.best = 10000.0f;
+    r.bi = 0xffffffffu;
+#ifdef RT_BIG_EARLY
+    if (P.n_big) big_group(r, sb0, ib0);
+    for (uint32_t k0 = 4; k0 < P.n_big; k0 += 4) {
+#else
     for (uint32_t k0 = 0; k0 < P.n_big; k0 += 4) {
+#endif
         float sb[16];
+        uint32_t ib[4];
 #pragma unroll
         for (uint32_t k = 0; k < 16; ++k) sb[k] = g[k0 * 4u + k];
-        float bk[4], Dk[4];
-        uint32_t cand = 0u;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float rr = sb[4 * k + 3] * sb[4 * k + 3];
-            const float ocx = r.o.x - sb[4 * k], ocy = r.o.y - sb[4 * k + 1], ocz = r.o.z - sb[4 * k + 2];
-            bk[k] = __builtin_fmaf(ocz, r.d.z, __builtin_fmaf(ocy, r.d.y, ocx * r.d.x));
-            const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - rr;
-            Dk[k] = __builtin_fmaf(bk[k], bk[k], -(r.a * c));
-            cand |= (Dk[k] >= 0.0f && !behind(bk[k], c) ? 1u : 0u) << k;
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if ((cand >> k) & 1u) {
-                const float sq = sqrt_cr(Dk[k]);
-                float t = (-bk[k] - sq) * r.ia;
-                if (!(t >= T_MIN)) t = (-bk[k] + sq) * r.ia;   // report t1 if t1 >= tmin, else t2
-                const uint32_t id = gid[k0 + k];
-                if ((t >= T_MIN) & (t <= r.best) & ((t < r.best) | (id < r.bi))) {
-                    r.best = t;
-                    r.bi = id;
-                }
-            }
-        }
+        for (uint32_t k = 0; k < 4; ++k) ib[k] = gid[k0 + k];
+        big_group(r, sb, ib);
     }
     n_sph += P.n_big;
     r.limit = cull_limit(P, r.best);
@@ -1125,16 +1160,31 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
                                           const float4* __restrict__ rec, const uint32_t* __restrict__ ids,
                                           Ray& r, uint32_t& n_cell, uint32_t& n_sph, uint32_t& n_empty) {
     const rt::GridInfo& G = P.grid;
-    const float x0 = (G.lo_m[0] - r.o.x) * r.inv.x, x1 = (G.hi_m[0] - r.o.x) * r.inv.x;
-    const float y0 = (G.lo_m[1] - r.o.y) * r.inv.y, y1 = (G.hi_m[1] - r.o.y) * r.inv.y;
-    const float z0 = (G.lo_m[2] - r.o.z) * r.inv.z, z1 = (G.hi_m[2] - r.o.z) * r.inv.z;
+#ifdef RT_ENTRY_LDS
+    const float4 ex = s_walk_entry[0], ey = s_walk_entry[1], ez = s_walk_entry[2];
+    const float4 axx = s_walk_axis[0], axy = s_walk_axis[1], axz = s_walk_axis[2];
+    const float lo0 = ex.x, lo1 = ey.x, lo2 = ez.x, hi0 = ex.y, hi1 = ey.y, hi2 = ez.y;
+    const float ics[3] = {ex.z, ey.z, ez.z}, gmn[3] = {axx.y, axy.y, axz.y}, csz[3] = {axx.x, axy.x, axz.x};
+    const int nm1[3] = {int(__float_as_uint(ex.w)), int(__float_as_uint(ey.w)), int(__float_as_uint(ez.w))};
+    const uint32_t n0 = __float_as_uint(axx.w), n1 = __float_as_uint(axy.w);
+#else
+    const float lo0 = G.lo_m[0], lo1 = G.lo_m[1], lo2 = G.lo_m[2], hi0 = G.hi_m[0], hi1 = G.hi_m[1], hi2 = G.hi_m[2];
+    const float* ics = G.inv_cs;
+    const float* gmn = G.gmin;
+    const float* csz = G.cs;
+    const int nm1[3] = {int(G.n[0]) - 1, int(G.n[1]) - 1, int(G.n[2]) - 1};
+    const uint32_t n0 = G.n[0], n1 = G.n[1];
+#endif
+    const float x0 = (lo0 - r.o.x) * r.inv.x, x1 = (hi0 - r.o.x) * r.inv.x;
+    const float y0 = (lo1 - r.o.y) * r.inv.y, y1 = (hi1 - r.o.y) * r.inv.y;
+    const float z0 = (lo2 - r.o.z) * r.inv.z, z1 = (hi2 - r.o.z) * r.inv.z;
     const float tn = fmaxf(fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fminf(z0, z1)), T_MIN);
     const float tf = fminf(fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fmaxf(z0, z1)), r.limit);
     if (!(tn <= tf)) return;
     // entry cell (clamped: a point rounded just outside belongs to the border cell)
     auto cell_of = [&](float p, int k) {
-        const int c = int(floorf((p - G.gmin[k]) * G.inv_cs[k]));
-        return min(max(c, 0), int(G.n[k]) - 1);
+        const int c = int(floorf((p - gmn[k]) * ics[k]));
+        return min(max(c, 0), nm1[k]);
     };
     int cx = cell_of(__builtin_fmaf(tn, r.d.x, r.o.x), 0);
     int cy = cell_of(__builtin_fmaf(tn, r.d.y, r.o.y), 1);
@@ -1144,14 +1194,14 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
     const int sz = r.d.z > 0.0f ? 1 : (r.d.z < 0.0f ? -1 : 0);
     // t of the boundary ahead on each axis (+inf on an axis the ray does not move along)
     auto bound_t = [&](int c, int s, int k, float o, float inv) {
-        const float plane = __builtin_fmaf(float(c + (s > 0 ? 1 : 0)), G.cs[k], G.gmin[k]);
+        const float plane = __builtin_fmaf(float(c + (s > 0 ? 1 : 0)), csz[k], gmn[k]);
         return s == 0 ? __builtin_inff() : (plane - o) * inv;
     };
     float tx = bound_t(cx, sx, 0, r.o.x, r.inv.x);
     float ty = bound_t(cy, sy, 1, r.o.y, r.inv.y);
     float tz = bound_t(cz, sz, 2, r.o.z, r.inv.z);
     // linear cell index (a step adds the stepped axis's stride, dda_step)
-    uint32_t cell = (uint32_t(cz) * G.n[1] + uint32_t(cy)) * G.n[0] + uint32_t(cx);
+    uint32_t cell = (uint32_t(cz) * n1 + uint32_t(cy)) * n0 + uint32_t(cx);
     for (;;) {
         const uint32_t b = cstart[cell], e = cstart[cell + 1];
         if (COUNT) {
