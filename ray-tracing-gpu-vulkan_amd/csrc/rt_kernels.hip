@@ -1202,12 +1202,44 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
     float tz = bound_t(cz, sz, 2, r.o.z, r.inv.z);
     // linear cell index (a step adds the stepped axis's stride, dda_step)
     uint32_t cell = (uint32_t(cz) * n1 + uint32_t(cy)) * n0 + uint32_t(cx);
+#ifdef RT_GRID_INLINE
+    const float4* __restrict__ pcells = reinterpret_cast<const float4*>(P.grid_cells);
+#endif
     for (;;) {
+#ifdef RT_GRID_INLINE
+        uint32_t b, e;
+        if (PAIRS && pcells) {
+            // A/B variant: the cell's header and first two references in one L2 round trip
+            // (DeviceScene::grid_cells), the rest from the reference arrays as before
+            const float4 h = pcells[3 * size_t(cell)], q0 = pcells[3 * size_t(cell) + 1],
+                         q1 = pcells[3 * size_t(cell) + 2];
+            const uint32_t n = __float_as_uint(h.x);
+            if (COUNT) {
+                n_cell++;
+                n_empty += n == 0u ? 1u : 0u;
+                n_sph += min(n, 2u);
+            }
+            if (n > 0u) test1<true>(q0, [&] { return __float_as_uint(h.z); }, r.o, r.d, r.inv, r.a, r.ia, r.best,
+                                    r.bi, r.limit, P);
+            if (n > 1u) test1<true>(q1, [&] { return __float_as_uint(h.w); }, r.o, r.d, r.inv, r.a, r.ia, r.best,
+                                    r.bi, r.limit, P);
+            b = __float_as_uint(h.y);
+            e = n > 2u ? b + (n - 2u) : b;
+        } else {
+            b = cstart[cell];
+            e = cstart[cell + 1];
+            if (COUNT) {
+                n_cell++;
+                n_empty += b == e ? 1u : 0u;
+            }
+        }
+#else
         const uint32_t b = cstart[cell], e = cstart[cell + 1];
         if (COUNT) {
             n_cell++;
             n_empty += b == e ? 1u : 0u;
         }
+#endif
         uint32_t j = b;
         if (PAIRS) {   // references from L2: two at a time (two record loads in flight; config 5 -3.5 %)
           // the ids are loaded with the records (one L2 round trip instead of a second, dependent

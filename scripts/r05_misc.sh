@@ -6,6 +6,10 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 TAG=${TAG:-r05g}
+if [ -n "${TESTS:-}" ]; then
+timeout -k 10 600 python -u -m pytest $TESTS -m gpu -q -x --timeout 300 --timeout-method thread > gpurun_out/${TAG}_pytest.log 2>&1
+rc=$?; tail -3 gpurun_out/${TAG}_pytest.log; [ $rc -lt 124 ] || exit $rc
+fi
 SKIP_BAND=1 TAG=$TAG bash scripts/r05_ab.sh; rc=$?; [ $rc -lt 124 ] || exit $rc
 if [ "${SKIP_REHEARSAL:-0}" != 1 ]; then
 RT_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
