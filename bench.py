@@ -790,7 +790,7 @@ def main() -> int:
                       "one GPU renders straight into the caller's buffers (no communicator, no collective)"))
         elif mode == "per-process":
             par = (f"torch.distributed ({backend}): {world} processes, one per GPU, 8-row strips round robin + "
-                   f"gather to rank 0 + device reorder")
+                   f"gather of the float4 accumulator strips to rank 0 + device reorder + rgba8 resolve on rank 0")
         else:
             par = "1 GPU"
         result = {

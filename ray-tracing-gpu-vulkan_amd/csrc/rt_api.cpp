@@ -802,7 +802,6 @@ int device_build_end(rt_context* ctx) {
     d.small_rmin = rt::summary_float(sm.rmin_o);
     d.grid = rt::GridInfo{};
     d.cell_start = d.grid_ids = nullptr;
-    d.grid_cells = nullptr;
     d.grid_rec = nullptr;
     ctx->colours_unit = sm.colour_out_of_range == 0u;
     ctx->scene_radius = rt::summary_float(sm.R_o);
@@ -818,12 +817,7 @@ int device_build_end(rt_context* ctx) {
             const size_t nc1 = size_t(gi.n_cells) + 1, tb = rt::grid_scan_bytes(gi.n_cells);
             const size_t off_cur = round256(nc1 * 4), off_rec = off_cur + round256(nc1 * 4),
                          off_ids = off_rec + round256(size_t(bound) * sizeof(rt::GeomRec)),
-                         off_tmp = off_ids + round256(size_t(bound) * 4), off_cells = off_tmp + round256(tb),
-#ifdef RT_GRID_INLINE
-                         total = off_cells + round256(size_t(gi.n_cells) * 3 * sizeof(rt::GeomRec));
-#else
-                         total = off_cells;
-#endif
+                         off_tmp = off_ids + round256(size_t(bound) * 4), total = off_tmp + round256(tb);
             if (s.grid_cap < total) {
                 if (int rc = retire_slot_memory(ctx, s, s.grid_mem)) return rc;
                 s.grid_cap = 0;
@@ -836,10 +830,6 @@ int device_build_end(rt_context* ctx) {
             d.grid_ids = reinterpret_cast<uint32_t*>(g + off_ids);
             RT_HIP(rt::build_grid_gpu(ctx->ws, ctx->d_spheres, d.n_spheres, gi, reinterpret_cast<uint32_t*>(g + off_cur),
                                       d.cell_start, d.grid_rec, d.grid_ids, g + off_tmp, tb, bs));
-#ifdef RT_GRID_INLINE
-            d.grid_cells = reinterpret_cast<rt::GeomRec*>(g + off_cells);
-            RT_HIP(rt::pack_grid_cells(d.cell_start, d.grid_rec, d.grid_ids, gi.n_cells, d.grid_cells, bs));
-#endif
             gi.n_refs = 0;   // exact count left on the device: the grid is walked from L2
             d.grid = gi;
             ctx->has_grid = true;
@@ -1102,7 +1092,6 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
         P.cell_start = d.cell_start;
         P.grid_rec = d.grid_rec;
         P.grid_ids = d.grid_ids;
-        P.grid_cells = d.grid_cells;
     }
     P.n_leaf = d.n_leaf;
     P.leaf_geom = d.leaf_geom;

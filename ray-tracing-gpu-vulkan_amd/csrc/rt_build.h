@@ -107,8 +107,5 @@ hipError_t build_grid_gpu(const BuildWorkspace& ws, const Sphere* d_spheres, uin
                           uint32_t* cursor, uint32_t* cell_start, GeomRec* rec, uint32_t* ids, void* tmp,
                           size_t tmp_bytes, hipStream_t st);
 size_t grid_scan_bytes(uint32_t n_cells);
-// Packed cells of a built grid (DeviceScene::grid_cells): 3 records per cell.
-hipError_t pack_grid_cells(const uint32_t* cell_start, const GeomRec* rec, const uint32_t* ids, uint32_t n_cells,
-                           GeomRec* cells, hipStream_t st);
 
 }  // namespace rt

@@ -750,29 +750,6 @@ hipError_t build_grid_gpu(const BuildWorkspace& ws, const Sphere* sph, uint32_t 
     return hipGetLastError();
 }
 
-// Cell c -> {count, first overflow reference, id0, id1} (bits) + its first two references (a
-// missing one: a copy of the header, never read: the walk tests `count` of them).
-__global__ void __launch_bounds__(kBlock) k_grid_pack(const uint32_t* __restrict__ cell_start,
-                                                      const GeomRec* __restrict__ rec,
-                                                      const uint32_t* __restrict__ ids, uint32_t n_cells,
-                                                      GeomRec* __restrict__ cells) {
-    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
-    if (c >= n_cells) return;
-    const uint32_t b = cell_start[c], e = cell_start[c + 1], n = e - b;
-    const GeomRec h{__uint_as_float(n), __uint_as_float(b + 2u), __uint_as_float(n > 0 ? ids[b] : 0u),
-                    __uint_as_float(n > 1 ? ids[b + 1] : 0u)};
-    cells[3 * size_t(c)] = h;
-    cells[3 * size_t(c) + 1] = n > 0 ? rec[b] : h;
-    cells[3 * size_t(c) + 2] = n > 1 ? rec[b + 1] : h;
-}
-
-hipError_t pack_grid_cells(const uint32_t* cell_start, const GeomRec* rec, const uint32_t* ids, uint32_t n_cells,
-                           GeomRec* cells, hipStream_t st) {
-    if (!n_cells) return hipSuccess;
-    k_grid_pack<<<blocks(n_cells), kBlock, 0, st>>>(cell_start, rec, ids, n_cells, cells);
-    return hipGetLastError();
-}
-
 size_t grid_scan_bytes(uint32_t n_cells) {
     size_t tb = 0;
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tb, static_cast<uint32_t*>(nullptr),

@@ -124,10 +124,6 @@ struct DeviceScene {
     uint32_t* cell_start = nullptr;
     GeomRec* grid_rec = nullptr;
     uint32_t* grid_ids = nullptr;
-    // device grids walked from L2: per cell {count, first overflow reference, id0, id1} + the first
-    // two references inline (3 records, 48 B): the cell's offsets and its first references in one
-    // round trip (null: not packed)
-    GeomRec* grid_cells = nullptr;
 };
 
 // Trace kernel forms (rt_kernels.hip pick()). Production: BRUTE (BASELINE config 2), OCT (trees
@@ -242,7 +238,6 @@ struct TraceParams {
     const uint32_t* cell_start;
     const GeomRec* grid_rec;
     const uint32_t* grid_ids;
-    const GeomRec* grid_cells;     // packed cells (DeviceScene::grid_cells), or null
     // outputs
     float* accum;                  // STREAM: band_w * band_h * 4 floats
     uint32_t* out;                 // STREAM: band_w * band_h packed rgba8

@@ -182,21 +182,19 @@ __device__ __forceinline__ float4 lds_reload(const float4* p) {
 // (config 3 -3.1 %, reference stream -2.9 %, config 5 -1.3 %).
 __shared__ float4 s_walk_axis[3];   // (cs[k], gmin[k], stride[k], n[k]): stride and n as uint bits
 __shared__ float2 s_walk_slack;     // (cull_near_abs, cull_abs)
-#ifdef RT_ENTRY_LDS
-// A/B variant: the grid walk's entry parameters (the widened grid box, 1 / cell size, the last
-// cell index per axis) from LDS as well, instead of kernel-argument reloads (s_load + an lgkmcnt(0)
-// wait at every walk's entry) and spilled SGPRs.
+// ... and the grid walk's entry parameters (the widened grid box, 1 / cell size, the last cell
+// index per axis) from LDS as well, instead of kernel-argument reloads (an s_load and an
+// lgkmcnt(0) wait, which also drains the wave's LDS reads, at every walk's entry) and spilled
+// SGPRs (together with the early big-sphere loads of setup_ray: config 3 -2.2 %, reference
+// stream -4.6 %, config 5 -1.5 %).
 __shared__ float4 s_walk_entry[3];   // per axis: (lo_m, hi_m, inv_cs, n - 1 as uint bits)
-#endif
 __device__ __forceinline__ void stage_walk_params(const rt::TraceParams& P, uint32_t tid) {
     if (tid < 3u) {
         const uint32_t stride = tid == 0u ? 1u : tid == 1u ? P.grid.n[0] : P.grid.n[0] * P.grid.n[1];
         s_walk_axis[tid] = make_float4(P.grid.cs[tid], P.grid.gmin[tid], __uint_as_float(stride),
                                        __uint_as_float(P.grid.n[tid]));
-#ifdef RT_ENTRY_LDS
         s_walk_entry[tid] = make_float4(P.grid.lo_m[tid], P.grid.hi_m[tid], P.grid.inv_cs[tid],
                                         __uint_as_float(P.grid.n[tid] - 1u));
-#endif
     }
     if (tid == 3u) s_walk_slack = make_float2(P.cull_near_abs, P.cull_abs);
 }
@@ -1063,17 +1061,15 @@ __device__ __forceinline__ void setup_ray(const rt::TraceParams& P, Ray& r, uint
     typedef const __attribute__((address_space(4))) uint32_t* ConstU;
     const ConstF g = (ConstF)(P.big_tab);
     const ConstU gid = (ConstU)(P.big_tab + 4u * rt::kBigMax);
-#ifdef RT_BIG_EARLY
-    // A/B variant: the first four records and ids are requested before the reciprocals, so the
-    // scalar loads' latency runs under them (the table always holds kBigMax entries: reading the
-    // first four is safe whatever n_big)
+    // the first four records and ids are requested before the reciprocals, so the scalar loads'
+    // latency runs under them (the table always holds kBigMax entries: reading the first four is
+    // safe whatever n_big); the ids come with the records, not one dependent load per candidate
     float sb0[16];
     uint32_t ib0[4];
 #pragma unroll
     for (uint32_t k = 0; k < 16; ++k) sb0[k] = g[k];
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k) ib0[k] = gid[k];
-#endif
     r.a = dot(r.d, r.d);
     r.ia = rcp_cr(r.a);
     r.inv = v3(rcp_cr(r.d.x), rcp_cr(r.d.y), rcp_cr(r.d.z));
@@ -1082,12 +1078,8 @@ __device__ __forceinline__ void setup_ray(const rt::TraceParams& P, Ray& r, uint
     // beyond it, and the (t bits, id) keys of the cooperative walk order the same way.
     r.best = 10000.0f;
     r.bi = 0xffffffffu;
-#ifdef RT_BIG_EARLY
     if (P.n_big) big_group(r, sb0, ib0);
     for (uint32_t k0 = 4; k0 < P.n_big; k0 += 4) {
-#else
-    for (uint32_t k0 = 0; k0 < P.n_big; k0 += 4) {
-#endif
         float sb[16];
         uint32_t ib[4];
 #pragma unroll
@@ -1159,22 +1151,13 @@ template <bool COUNT, bool PAIRS>
 __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32_t* __restrict__ cstart,
                                           const float4* __restrict__ rec, const uint32_t* __restrict__ ids,
                                           Ray& r, uint32_t& n_cell, uint32_t& n_sph, uint32_t& n_empty) {
-    const rt::GridInfo& G = P.grid;
-#ifdef RT_ENTRY_LDS
+    // grid parameters from the block's LDS tables (stage_walk_params), not from the kernel arguments
     const float4 ex = s_walk_entry[0], ey = s_walk_entry[1], ez = s_walk_entry[2];
     const float4 axx = s_walk_axis[0], axy = s_walk_axis[1], axz = s_walk_axis[2];
     const float lo0 = ex.x, lo1 = ey.x, lo2 = ez.x, hi0 = ex.y, hi1 = ey.y, hi2 = ez.y;
     const float ics[3] = {ex.z, ey.z, ez.z}, gmn[3] = {axx.y, axy.y, axz.y}, csz[3] = {axx.x, axy.x, axz.x};
     const int nm1[3] = {int(__float_as_uint(ex.w)), int(__float_as_uint(ey.w)), int(__float_as_uint(ez.w))};
     const uint32_t n0 = __float_as_uint(axx.w), n1 = __float_as_uint(axy.w);
-#else
-    const float lo0 = G.lo_m[0], lo1 = G.lo_m[1], lo2 = G.lo_m[2], hi0 = G.hi_m[0], hi1 = G.hi_m[1], hi2 = G.hi_m[2];
-    const float* ics = G.inv_cs;
-    const float* gmn = G.gmin;
-    const float* csz = G.cs;
-    const int nm1[3] = {int(G.n[0]) - 1, int(G.n[1]) - 1, int(G.n[2]) - 1};
-    const uint32_t n0 = G.n[0], n1 = G.n[1];
-#endif
     const float x0 = (lo0 - r.o.x) * r.inv.x, x1 = (hi0 - r.o.x) * r.inv.x;
     const float y0 = (lo1 - r.o.y) * r.inv.y, y1 = (hi1 - r.o.y) * r.inv.y;
     const float z0 = (lo2 - r.o.z) * r.inv.z, z1 = (hi2 - r.o.z) * r.inv.z;
@@ -1202,44 +1185,12 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
     float tz = bound_t(cz, sz, 2, r.o.z, r.inv.z);
     // linear cell index (a step adds the stepped axis's stride, dda_step)
     uint32_t cell = (uint32_t(cz) * n1 + uint32_t(cy)) * n0 + uint32_t(cx);
-#ifdef RT_GRID_INLINE
-    const float4* __restrict__ pcells = reinterpret_cast<const float4*>(P.grid_cells);
-#endif
     for (;;) {
-#ifdef RT_GRID_INLINE
-        uint32_t b, e;
-        if (PAIRS && pcells) {
-            // A/B variant: the cell's header and first two references in one L2 round trip
-            // (DeviceScene::grid_cells), the rest from the reference arrays as before
-            const float4 h = pcells[3 * size_t(cell)], q0 = pcells[3 * size_t(cell) + 1],
-                         q1 = pcells[3 * size_t(cell) + 2];
-            const uint32_t n = __float_as_uint(h.x);
-            if (COUNT) {
-                n_cell++;
-                n_empty += n == 0u ? 1u : 0u;
-                n_sph += min(n, 2u);
-            }
-            if (n > 0u) test1<true>(q0, [&] { return __float_as_uint(h.z); }, r.o, r.d, r.inv, r.a, r.ia, r.best,
-                                    r.bi, r.limit, P);
-            if (n > 1u) test1<true>(q1, [&] { return __float_as_uint(h.w); }, r.o, r.d, r.inv, r.a, r.ia, r.best,
-                                    r.bi, r.limit, P);
-            b = __float_as_uint(h.y);
-            e = n > 2u ? b + (n - 2u) : b;
-        } else {
-            b = cstart[cell];
-            e = cstart[cell + 1];
-            if (COUNT) {
-                n_cell++;
-                n_empty += b == e ? 1u : 0u;
-            }
-        }
-#else
         const uint32_t b = cstart[cell], e = cstart[cell + 1];
         if (COUNT) {
             n_cell++;
             n_empty += b == e ? 1u : 0u;
         }
-#endif
         uint32_t j = b;
         if (PAIRS) {   // references from L2: two at a time (two record loads in flight; config 5 -3.5 %)
           // the ids are loaded with the records (one L2 round trip instead of a second, dependent
