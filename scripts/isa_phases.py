@@ -8,7 +8,7 @@ marker above them, so code the compiler sinks or hoists across a marker counts w
 Counts are static (each instruction once), not dynamic: a loop body counts once.
 
 usage: python scripts/isa_phases.py LISTING.s [KERNEL_SUBSTRING] [--json out]
-       (listing: make -C ray-tracing-gpu-vulkan_amd asm-marks)
+       (listing: make -C ray-tracing-gpu-vulkan_amd asm DEVFLAGS="--offload-arch=gfx950 -fno-gpu-rdc -fno-slp-vectorize -DRT_ASM_MARKS")
 default kernel: the headline form rt_trace_grid_kernel<false, MODE_HASH, IN_LDS, !COOP, REC, !CQ>."""
 import json
 import re
