@@ -30,7 +30,8 @@
 namespace rt {
 hipError_t launch_trace(const TraceParams& P, uint32_t accel, bool count, int mode, int grid, size_t lds_bytes,
                         hipStream_t st);
-hipError_t trace_occupancy(uint32_t accel, bool count, int mode, size_t lds_bytes, int* blocks_per_cu);
+hipError_t trace_occupancy(uint32_t accel, bool count, int mode, bool flat, size_t lds_bytes, int* blocks_per_cu);
+bool flat_grid_form(const TraceParams& P, uint32_t accel, bool count);
 hipError_t launch_resolve_fixed(unsigned long long* fixed, uint64_t n_texels, uint32_t accumulate, uint32_t spp,
                                 float* accum, uint8_t* out, hipStream_t st);
 hipError_t launch_tonemap(const float* accum, uint64_t n_texels, uint32_t spp, uint8_t* out, hipStream_t st);
@@ -117,8 +118,8 @@ struct rt_context {
     bool topo_ok = false;
     bool pending_refit = false;
     // occupancy cache per kernel form, count flag and rng mode, valid for occ_lds bytes
-    int occ[rt::ACCEL_COUNT][2][2] = {};
-    size_t occ_lds[rt::ACCEL_COUNT][2][2] = {};
+    int occ[rt::ACCEL_COUNT][3][2] = {};   // [form][plain, count_tests, one-layer grid walk][mode]
+    size_t occ_lds[rt::ACCEL_COUNT][3][2] = {};
     size_t lds1_bytes = 0;                       // one node copy + leaves + big table (0: no fit)
     size_t oct_bytes = 0;                        // 8 octant node copies + leaves + big table (0: no fit)
     size_t grid_bytes = 0;                       // grid references + offsets + big table (0: no grid / no fit)
@@ -153,6 +154,7 @@ struct rt_context {
     uint32_t last_chunks = 1;
     uint32_t last_accel = 0;                     // kernel form (rt::ACCEL_*) of the last launch, 0 = none yet
     size_t last_lds = 0;                         // its dynamic LDS bytes
+    bool last_flat = false;                      // its grid walk was the one-layer form
     // every colour the shaders can return lies in [0, 1] (RT_RNG_SAMPLE_HASH's fixed point needs it)
     bool colours_unit = true;
     // HIP events bracketing the trace kernel of the last kKernelEvents launches (ring; timing
@@ -1156,20 +1158,21 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     // after their own data (band_row, rt_kernels.hip) when that keeps the blocks per CU; else it
     // is read from global memory.
     P.rows_lds = rt::kNoRowsLds;
+    const bool flat = rt::flat_grid_form(P, accel, count);   // the kernel launch_trace picks
     if (rows && accel != rt::ACCEL_BRUTE) {
         const size_t off = (lds + 15) & ~size_t(15), with = off + size_t(band_height) * 4u;
         int b0 = 0, b1 = 0;
-        if (with <= kMaxLdsBytes && rt::trace_occupancy(accel, count, mode, lds, &b0) == hipSuccess &&
-            rt::trace_occupancy(accel, count, mode, with, &b1) == hipSuccess && b1 >= b0 && b1 > 0) {
+        if (with <= kMaxLdsBytes && rt::trace_occupancy(accel, count, mode, flat, lds, &b0) == hipSuccess &&
+            rt::trace_occupancy(accel, count, mode, flat, with, &b1) == hipSuccess && b1 >= b0 && b1 > 0) {
             P.rows_lds = uint32_t(off);
             lds = with;
         }
     }
     // Grid: one persistent block per CU slot the occupancy allows.
-    const int ci = count ? 1 : 0;
+    const int ci = count ? 1 : flat ? 2 : 0;
     if (ctx->occ_lds[accel][ci][mode] != lds) {
         int b = 0;
-        RT_HIP(rt::trace_occupancy(accel, count, mode, lds, &b));
+        RT_HIP(rt::trace_occupancy(accel, count, mode, flat, lds, &b));
         ctx->occ[accel][ci][mode] = std::max(1, b);
         ctx->occ_lds[accel][ci][mode] = lds;
     }
@@ -1207,6 +1210,7 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     P.chunks = uint32_t(chunks);
     ctx->last_accel = accel;
     ctx->last_lds = lds;
+    ctx->last_flat = flat;
     const uint64_t texels = uint64_t(band_width) * band_height;
     if (mode == rt::MODE_HASH) {
         if (ctx->fixed_cap < texels) {
@@ -1521,7 +1525,7 @@ int rt_debug_launch_info(rt_context* ctx, uint32_t* out4) {
     if (!ctx || !out4) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     out4[0] = ctx->last_chunks;
     if (ctx->last_accel) {   // the kernel form the last launch actually ran
-        out4[1] = ctx->last_accel;
+        out4[1] = ctx->last_accel | (ctx->last_flat ? 0x10000u : 0u);
         out4[2] = uint32_t(ctx->last_lds);
     } else {   // no launch yet: the default form of the current scene (camera within its pad radius)
         size_t lds = 0;

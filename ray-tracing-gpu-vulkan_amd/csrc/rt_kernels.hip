@@ -221,6 +221,27 @@ __device__ __forceinline__ bool dda_step(float tm, float& tx, float& ty, float& 
     return true;
 }
 
+// dda_step for a grid one cell thick in y (every ray is in cell row 0): the same cells in the same
+// order. With one y cell a y step always leaves the grid, so the walk ends where dda_step would
+// return false; only x and z step (x before z on ties, as there).
+__device__ __forceinline__ bool dda_step_xz(float tm, float& tx, float ty, float& tz, int& cx, int& cz, int sx,
+                                            int sz, uint32_t& cell, V3 o, V3 inv) {
+    const bool mx = tx == tm;
+    if (!mx && ty == tm) return false;
+    const float4 ax = s_walk_axis[mx ? 0 : 2];
+    const int s = mx ? sx : sz;
+    const int c = (mx ? cx : cz) + s;
+    if (uint32_t(c) >= __float_as_uint(ax.w)) return false;
+    cx = mx ? c : cx;
+    cz = mx ? cz : c;
+    cell = s > 0 ? cell + __float_as_uint(ax.z) : cell - __float_as_uint(ax.z);
+    const float ok = mx ? o.x : o.z, ik = mx ? inv.x : inv.z;
+    const float tnew = (__builtin_fmaf(float(c + (s > 0 ? 1 : 0)), ax.x, ax.y) - ok) * ik;
+    tx = mx ? tnew : tx;
+    tz = mx ? tz : tnew;
+    return true;
+}
+
 // Cull limit of a closest-so-far t: best + cull_abs + cull_rel best, with
 // the smaller absolute slack of grid walks for t <= cull_near_t (rt_api.cpp; -1 elsewhere).
 __device__ __forceinline__ float cull_limit(const rt::TraceParams& P, float t) {
@@ -295,6 +316,16 @@ __device__ __forceinline__ void test1(const float4 sp, IdAt id_at, V3 o, V3 d, V
         const float sq = sqrt_cr(D);
         float t = (-b - sq) * ia;
         if (!(t >= T_MIN)) t = (-b + sq) * ia;     // report t1 if t1 >= tmin, else t2
+#ifdef RT_UTIL
+        {   // grid walks: what the candidate tails find (12 beyond the closest so far, 13 the current
+            // winner again from a later cell, 14 both roots below tmin, 15 passes no lane needed)
+            const uint32_t idd = id_at();
+            UTIL(12, t > best);
+            UTIL(13, t == best && idd == bi);
+            UTIL(14, !(t >= T_MIN));
+            if (!__ballot((t >= T_MIN) & ((t < best) | ((t == best) & (idd < bi))))) UTIL(15, true);
+        }
+#endif
         if (ID_READY) {
             const uint32_t id = id_at();
             if ((t >= T_MIN) & (t <= best) & ((t < best) | (id < bi))) {   // one predicate, one branch
@@ -1147,7 +1178,7 @@ __device__ __forceinline__ void walk_global_range(const rt::TraceParams& P, cons
 // coordinate (no accumulated rounding), so the cells visited cover the ray up to rounding distance
 // of the boundaries, which the margin covers. Ties step one axis at a time (an
 // extra cell, never a skipped one).
-template <bool COUNT, bool PAIRS>
+template <bool COUNT, bool PAIRS, bool FLAT = false>
 __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32_t* __restrict__ cstart,
                                           const float4* __restrict__ rec, const uint32_t* __restrict__ ids,
                                           Ray& r, uint32_t& n_cell, uint32_t& n_sph, uint32_t& n_empty) {
@@ -1170,7 +1201,7 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
         return min(max(c, 0), nm1[k]);
     };
     int cx = cell_of(__builtin_fmaf(tn, r.d.x, r.o.x), 0);
-    int cy = cell_of(__builtin_fmaf(tn, r.d.y, r.o.y), 1);
+    int cy = FLAT ? 0 : cell_of(__builtin_fmaf(tn, r.d.y, r.o.y), 1);
     int cz = cell_of(__builtin_fmaf(tn, r.d.z, r.o.z), 2);
     const int sx = r.d.x > 0.0f ? 1 : (r.d.x < 0.0f ? -1 : 0);
     const int sy = r.d.y > 0.0f ? 1 : (r.d.y < 0.0f ? -1 : 0);
@@ -1184,7 +1215,7 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
     float ty = bound_t(cy, sy, 1, r.o.y, r.inv.y);
     float tz = bound_t(cz, sz, 2, r.o.z, r.inv.z);
     // linear cell index (a step adds the stepped axis's stride, dda_step)
-    uint32_t cell = (uint32_t(cz) * n1 + uint32_t(cy)) * n0 + uint32_t(cx);
+    uint32_t cell = FLAT ? uint32_t(cz) * n0 + uint32_t(cx) : (uint32_t(cz) * n1 + uint32_t(cy)) * n0 + uint32_t(cx);
     for (;;) {
         const uint32_t b = cstart[cell], e = cstart[cell + 1];
         if (COUNT) {
@@ -1230,7 +1261,11 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
         UTIL(0, true);
         const float tm = fminf(fminf(tx, ty), tz);
         if (!(tm <= r.limit)) break;   // the next cell starts beyond every closer candidate
-        if (!dda_step(tm, tx, ty, tz, cx, cy, cz, sx, sy, sz, cell, r.o, r.inv)) break;
+        if (FLAT) {
+            if (!dda_step_xz(tm, tx, ty, tz, cx, cz, sx, sz, cell, r.o, r.inv)) break;
+        } else if (!dda_step(tm, tx, ty, tz, cx, cy, cz, sx, sy, sz, cell, r.o, r.inv)) {
+            break;
+        }
     }
 }
 
@@ -1572,8 +1607,8 @@ __device__ __forceinline__ void regate_brute(const rt::TraceParams& P, const flo
     }
 }
 
-// The whole walk of one segment.
-template <bool COUNT, int LAYOUT>
+// The whole walk of one segment. FLAT: the grid is one cell thick in y (grid_walk).
+template <bool COUNT, int LAYOUT, bool FLAT = false>
 __device__ __forceinline__ void walk(const rt::TraceParams& P, const float4* __restrict__ nodes4,
                                      const float4* __restrict__ leaf4, const uint32_t* __restrict__ leaf_ids,
                                      Ray& r, uint32_t& n_box, uint32_t& n_sph, uint32_t& n_empty) {
@@ -1584,8 +1619,8 @@ __device__ __forceinline__ void walk(const rt::TraceParams& P, const float4* __r
     }
     if (LAYOUT == LAYOUT_GRID || LAYOUT == LAYOUT_GRID_L2) {   // nodes4 = cell offsets, leaf4 / leaf_ids = references
         if (r.walk)
-            grid_walk<COUNT, LAYOUT == LAYOUT_GRID_L2>(P, reinterpret_cast<const uint32_t*>(nodes4), leaf4, leaf_ids, r,
-                                                       n_box, n_sph, n_empty);
+            grid_walk<COUNT, LAYOUT == LAYOUT_GRID_L2, FLAT>(P, reinterpret_cast<const uint32_t*>(nodes4), leaf4, leaf_ids,
+                                                             r, n_box, n_sph, n_empty);
         return;
     }
     const RayBox q = ray_box(r.o, r.inv);
@@ -1673,7 +1708,7 @@ __device__ __forceinline__ void walk(const rt::TraceParams& P, const float4* __r
 // longest walk ends. Stamp slots: 0 loop head, 4 sample start, 5 refill, 6 block fetch, 1 ray
 // setup (big spheres), 2 LBVH walk, 3 shading, 7 other.
 // ---------------------------------------------------------------------------------------------
-template <bool COUNT, int LAYOUT, int MODE, bool REC = false>
+template <bool COUNT, int LAYOUT, int MODE, bool REC = false, bool FLAT = false>
 __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4* __restrict__ nodes4,
                                           const float4* __restrict__ leaf4,
                                           const uint32_t* __restrict__ leaf_ids,
@@ -1733,7 +1768,7 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
             grid_walk_coop<COUNT>(P, reinterpret_cast<const uint32_t*>(nodes4), leaf4, leaf_ids, r, st == ST_TRACING,
                                   n_box, n_sph);
         } else {
-            if (st == ST_TRACING) walk<COUNT, LAYOUT>(P, nodes4, leaf4, leaf_ids, r, n_box, n_sph, n_empty);
+            if (st == ST_TRACING) walk<COUNT, LAYOUT, FLAT>(P, nodes4, leaf4, leaf_ids, r, n_box, n_sph, n_empty);
         }
         // the AABB gate of the winner only (winner_gated); the rare lanes whose winner fails it
         // get the contract's answer by a wave-cooperative gated brute force. The winner's shading
@@ -1862,7 +1897,9 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
 
 // Grid kernel (ACCEL_GRID): the grid's cell offsets and references staged in LDS once per
 // persistent block: [references (float4) | reference ids | cell offsets | shading records (REC)].
-template <bool COUNT, int MODE, bool IN_LDS, bool COOP = false, bool REC = false, bool CQ = false>
+// FLAT: the grid is one cell thick in y, as every grid of a scene whose small spheres lie in one
+// layer is (configs 3 and 5): the DDA steps x and z only (grid_walk; launch_trace picks it).
+template <bool COUNT, int MODE, bool IN_LDS, bool COOP = false, bool REC = false, bool CQ = false, bool FLAT = false>
 __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace_grid_kernel(const rt::TraceParams P) {
     UTIL_INIT;
     PLACEMENT_RECORD(P);
@@ -1871,7 +1908,7 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
         stage_walk_params(P, threadIdx.x);
         stage_rows(P, threadIdx.x, kTraceBlock);
         __syncthreads();
-        lbvh_loop<COUNT, COOP ? LAYOUT_GRID_COOP : LAYOUT_GRID_L2, MODE>(P, reinterpret_cast<const float4*>(P.cell_start),
+        lbvh_loop<COUNT, COOP ? LAYOUT_GRID_COOP : LAYOUT_GRID_L2, MODE, false, FLAT>(P, reinterpret_cast<const float4*>(P.cell_start),
                                             reinterpret_cast<const float4*>(P.grid_rec), P.grid_ids,
                                             reinterpret_cast<const float4*>(P.geom),
                                             reinterpret_cast<const float4*>(P.mat));
@@ -1898,12 +1935,12 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
             smat[2 * i + 1] = mat4[2 * i + 1];
         }
         __syncthreads();
-        lbvh_loop<COUNT, CQ ? LAYOUT_GRID_CQ : LAYOUT_GRID, MODE, true>(P, reinterpret_cast<const float4*>(cst), lds, ids,
-                                                                        srec, smat);
+        lbvh_loop<COUNT, CQ ? LAYOUT_GRID_CQ : LAYOUT_GRID, MODE, true, FLAT>(P, reinterpret_cast<const float4*>(cst), lds,
+                                                                              ids, srec, smat);
         return;
     }
     __syncthreads();
-    lbvh_loop<COUNT, COOP ? LAYOUT_GRID_COOP : CQ ? LAYOUT_GRID_CQ : LAYOUT_GRID, MODE>(P, reinterpret_cast<const float4*>(cst), lds, ids,
+    lbvh_loop<COUNT, COOP ? LAYOUT_GRID_COOP : CQ ? LAYOUT_GRID_CQ : LAYOUT_GRID, MODE, false, FLAT>(P, reinterpret_cast<const float4*>(cst), lds, ids,
                                         reinterpret_cast<const float4*>(P.geom),
                                         reinterpret_cast<const float4*>(P.mat));
 }
@@ -2088,8 +2125,16 @@ __global__ __launch_bounds__(256) void rt_debug_exact_kernel(uint64_t base, floa
 namespace rt {
 
 template <int MODE>
-static const void* pick_mode(uint32_t accel, bool count) {
+static const void* pick_mode(uint32_t accel, bool count, bool flat) {
 #define RT_FN(...) reinterpret_cast<const void*>(__VA_ARGS__)
+    if (flat && !count) {   // the grid walks of one-layer grids (instrumented builds count the same cells)
+        switch (accel) {
+            case ACCEL_GRID: return RT_FN(rt_trace_grid_kernel<false, MODE, true, false, false, false, true>);
+            case ACCEL_GRID_REC: return RT_FN(rt_trace_grid_kernel<false, MODE, true, false, true, false, true>);
+            case ACCEL_GRID_GLOBAL: return RT_FN(rt_trace_grid_kernel<false, MODE, false, false, false, false, true>);
+            default: break;
+        }
+    }
     switch (accel) {
         case ACCEL_BRUTE:
             return count ? RT_FN(rt_trace_brute_kernel<true, MODE>) : RT_FN(rt_trace_brute_kernel<false, MODE>);
@@ -2125,8 +2170,13 @@ static const void* pick_mode(uint32_t accel, bool count) {
 #undef RT_FN
 }
 
-static const void* pick(uint32_t accel, bool count, int mode) {
-    return mode == MODE_HASH ? pick_mode<MODE_HASH>(accel, count) : pick_mode<MODE_STREAM>(accel, count);
+static const void* pick(uint32_t accel, bool count, int mode, bool flat) {
+    return mode == MODE_HASH ? pick_mode<MODE_HASH>(accel, count, flat) : pick_mode<MODE_STREAM>(accel, count, flat);
+}
+
+bool flat_grid_form(const TraceParams& P, uint32_t accel, bool count) {
+    return !count && P.cell_start != nullptr && P.grid.n[1] == 1u &&
+           (accel == ACCEL_GRID || accel == ACCEL_GRID_REC || accel == ACCEL_GRID_GLOBAL);
 }
 
 uint32_t block_size(uint32_t accel) { return accel == ACCEL_BRUTE ? kBruteBlock : kTraceBlock; }
@@ -2134,11 +2184,12 @@ uint32_t block_size(uint32_t accel) { return accel == ACCEL_BRUTE ? kBruteBlock 
 hipError_t launch_trace(const TraceParams& P, uint32_t accel, bool count, int mode, int grid, size_t lds_bytes,
                         hipStream_t st) {
     void* args[] = {const_cast<TraceParams*>(&P)};
-    return hipLaunchKernel(pick(accel, count, mode), dim3(grid), dim3(block_size(accel)), args, lds_bytes, st);
+    return hipLaunchKernel(pick(accel, count, mode, flat_grid_form(P, accel, count)), dim3(grid), dim3(block_size(accel)),
+                           args, lds_bytes, st);
 }
 
-hipError_t trace_occupancy(uint32_t accel, bool count, int mode, size_t lds_bytes, int* blocks_per_cu) {
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, pick(accel, count, mode),
+hipError_t trace_occupancy(uint32_t accel, bool count, int mode, bool flat, size_t lds_bytes, int* blocks_per_cu) {
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, pick(accel, count, mode, flat),
                                                         block_size(accel), lds_bytes);
 }
 

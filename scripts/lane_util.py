@@ -41,7 +41,9 @@ for rng in (rtvk.HASH,):
     abi.check(lib.rt_debug_util(r._ctx, u))
     st = r.stats()
     print(f"{W}x{H} spp {spp} grid {K} rng {'hash' if rng == rtvk.HASH else 'stream'}: segments {st.segments}")
-    for k in (8, 7, 0, 12, 13, 14, 11, 1, 2, 3, 10, 9, 4, 5, 6):
+    if os.environ.get("RT_WALK", "0") in ("0", "12"):   # grid walks: slots 12-15 describe test1's candidates
+        NAMES.update({12: "cand beyond best", 13: "cand = winner", 14: "cand < tmin", 15: "cand pass, none useful"})
+    for k in (8, 7, 0, 12, 13, 14, 15, 11, 1, 2, 3, 10, 9, 4, 5, 6):
         n, a = u[2 * k], u[2 * k + 1]
         if n == 0:
             continue

@@ -322,6 +322,42 @@ def test_grid_lattice_axis_rays(rtvk, renderer, torch, oracle, builder):
             assert_same(a, o, ra, ro)
 
 
+@pytest.mark.parametrize("builder", [None, "gpu"])
+def test_grid_one_layer_and_layered_forms(rtvk, renderer, torch, oracle, builder):
+    """The grid walks have a one-layer form (the grid one cell thick in y: the DDA steps x and z
+    only), picked when the scene's grid has one cell row in y, as the canonical scenes' grids have,
+    and the general 3D form otherwise. Canonical scene: the one-layer form runs (launch_info
+    flat_grid) and equals the oracle and the instrumented build (which always runs the general
+    form) bit for bit; a stack of small spheres from y = 0.2 to 4.6: the general form runs and
+    equals the oracle. Both streams, host grid (LDS) and device grid (L2)."""
+    W, H = 48, 32
+    base = oracle.generate_scene()[4:5]
+    stack = [oracle.generate_scene()[:1].copy()]   # the ground sphere
+    rng = np.random.default_rng(11)
+    for k in range(240):
+        r = base.copy()
+        r[0, :16].view(np.float32)[:] = [rng.uniform(-4, 4), 0.2 + 4.4 * k / 239, rng.uniform(-4, 4), 0.2]
+        stack.append(r)
+    cases = [(oracle.generate_scene(), True, ((13.0, 2.0, 3.0), (0.0, 0.0, 0.0))),
+             (np.concatenate(stack), False, ((9.0, 3.0, -9.0), (0.0, 2.0, 0.0)))]
+    for sc, flat, (cam, look) in cases:
+        rci = oracle.render_call_info(3, W, H)
+        f = rci.view(np.float32)
+        f[8:11] = cam
+        f[12:15] = [look[k] - cam[k] for k in range(3)]
+        for rng_mode in (STREAM, HASH):
+            ra, ro, rst = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=rng_mode))
+            a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=GRID, rng_mode=rng_mode, builder=builder)
+            info = renderer.launch_info()
+            assert info["form"].startswith("grid") and info["flat_grid"] == flat, info
+            assert_same(a, o, ra, ro)
+            assert (st.segments, st.samples) == rst[:2]
+            a2, o2, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=GRID, rng_mode=rng_mode, builder=builder,
+                                   count=True)
+            assert not renderer.launch_info()["flat_grid"]
+            assert_same(a2, o2, ra, ro)
+
+
 @pytest.mark.parametrize("K,builder", [(11, None), (40, "gpu")])
 @pytest.mark.parametrize("accel", [LBVH, LBVH_OCT, LBVH_GLOBAL])
 def test_forced_regate_equals_oracle(rtvk, renderer, torch, oracle, accel, K, builder):
@@ -998,7 +1034,7 @@ def test_config5_full_frame(rtvk, renderer, torch, oracle):
     sc = oracle.generate_scene(0.0, K)
     rci = oracle.render_call_info(spp, W, H)
     a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=LBVH, rng_mode=HASH)
-    assert renderer.launch_info()["form"] == "grid-global"
+    assert renderer.launch_info()["form"] == "grid-global" and renderer.launch_info()["flat_grid"]
     for form in (LBVH_OCT, LBVH_GLOBAL):   # the treelet walk and the all-L2 tree walk
         a2, o2, st2 = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=form, rng_mode=HASH)
         assert_same(a, o, a2, o2)
