@@ -609,8 +609,8 @@ rt::HostPackagePtr build_host_package(const rt_context* ctx, const Sphere* spher
     pad_nodes(pk->nodes_host, pk->bvh.nodes, pad_for(pk->pad_radius));
     make_octant_orders(pk->bvh.nodes, pk->oct);
     // Uniform grid (rt_grid.h) when the scene suits one: the default walk.
-    // Tuning grid = 0 disables it, grid_scale scales the cell size (A/B).
-    const float gscale = float(Tuning::get(ctx->tune.grid_scale, rt::kGridCellScale));
+    // Tuning grid = 0 disables it, grid_scale sets the cell size scale (A/B; rt_grid.h).
+    const float gscale = float(Tuning::get(ctx->tune.grid_scale, rt::kGridCellScaleHost));
     pk->has_grid = Tuning::get(ctx->tune.grid, 1) != 0 &&
                    rt::build_grid_host(spheres, count, pk->bvh.big_ids, 64.0f * 0x1p-24f * pk->pad_radius, gscale,
                                        1u << 22, pk->grid);

@@ -33,6 +33,12 @@ bool build_grid_host(const Sphere* spheres, uint32_t n, const std::vector<uint32
 // (scripts/scale_ab.py, images bit-identical): 1.5 / 1.7 / 1.9 / 2.2 / 2.6 / 3.0 ->
 // 138.4 / 137.8 / 138.4 / 139.3 / 141.9 / 147.0 ms and 15.31 / 15.17 / 15.28 / 15.39 / 15.49 / 15.88 ms.
 constexpr float kGridCellScale = 1.7f;
+// Host-built grids (<= 1 024 spheres: staged in LDS, where a cell step costs an LDS read instead of
+// an L2 round trip) take slightly smaller cells. Round 5, the one-layer walk, config 3 at 10 000 spp
+// (scripts/grid_scale_ab.py): 1.55 / 1.6 / 1.65 / 1.7 -> 1 127.8 / 1 114.6 / 1 114.3 / 1 124.7 ms
+// (19 cells a side at 1.6-1.65 against 18 at 1.7); config 5's device-built L2 grid keeps 1.7
+// (1.65: +0.6 %).
+constexpr float kGridCellScaleHost = 1.65f;
 
 // Spare part of the registration margin, in cells (rt_api.cpp: it bounds the near cull slack).
 #ifndef RT_GRID_SPARE

@@ -243,7 +243,7 @@ struct TraceParams {
     uint32_t* out;                 // STREAM: band_w * band_h packed rgba8
     unsigned long long* fixed;     // HASH: 3 planes of band_w * band_h u64 (r, g, b), zero on entry
     Counters* counters;
-    const float* big_tab;          // the big spheres as kBigMax records {cx, cy, cz, r^2} (padded to a
+    const float* big_tab;          // the big spheres as kBigMax records {cx, cy, cz, r} (padded to a
                                    // multiple of 4 by repeating the last) + kBigMax ids, filled per
                                    // launch (rt_big_table_kernel), read through the scalar cache
 };
@@ -257,7 +257,7 @@ constexpr uint32_t kFixedFlush = 128;
 
 // "Big" spheres (radius above a scene-relative threshold, e.g. the ground sphere) are tested by
 // every segment before the tree walk; at most kBigMax of them. A one-wave kernel writes their
-// records (center, radius^2) and ids into TraceParams::big_tab before each launch; the walk kernels
+// records (center, radius) and ids into TraceParams::big_tab before each launch; the walk kernels
 // read them through the scalar cache (rt_kernels.hip setup_ray).
 constexpr uint32_t kBigMax = 64;
 constexpr uint32_t kNoRowsLds = 0xffffffffu;

@@ -1060,7 +1060,7 @@ __device__ __forceinline__ void big_group(Ray& r, const float (&sb)[16], const u
     uint32_t cand = 0u;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const float rr = sb[4 * k + 3];   // r * r rounded once (GeomRec), as test4 computes it
+        const float rr = sb[4 * k + 3] * sb[4 * k + 3];
         const float ocx = r.o.x - sb[4 * k], ocy = r.o.y - sb[4 * k + 1], ocz = r.o.z - sb[4 * k + 2];
         bk[k] = __builtin_fmaf(ocz, r.d.z, __builtin_fmaf(ocy, r.d.y, ocx * r.d.x));
         const float c = __builtin_fmaf(ocz, ocz, __builtin_fmaf(ocy, ocy, ocx * ocx)) - rr;
@@ -1976,7 +1976,7 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
 // this launch's samples plus the incoming float accumulator (accumulate = 1), rounded once to
 // float, stored with alpha 1, tonemapped to rgba8; the fixed-point planes are zeroed for the next
 // launch. HBM-bound: 24 B read + 24 B zeroed + 20 B stored per texel (+16 B read when accumulating).
-// The big-sphere table of a launch (TraceParams::big_tab): records {cx, cy, cz, r^2} of the n_big
+// The big-sphere table of a launch (TraceParams::big_tab): records {cx, cy, cz, r} of the n_big
 // spheres, padded to a multiple of 4 by repeating the last (a duplicate never changes (best, bi)),
 // then their ids. One wave, before the trace kernel on the same stream.
 // Per-launch preparation in one kernel instead of five stream operations: block 0
@@ -1985,6 +1985,7 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
 // zeroes its share of the tile-cost table this launch records into.
 __global__ __launch_bounds__(256) void rt_launch_prep_kernel(rt::Counters* __restrict__ counters, uint32_t work_head,
                                                              const rt::GeomRec* __restrict__ geom,
+                                                             const float* __restrict__ radius,
                                                              const uint32_t* __restrict__ big_ids, uint32_t n_big,
                                                              float4* __restrict__ tab, uint32_t* __restrict__ cost,
                                                              uint32_t n_cost) {
@@ -1997,7 +1998,7 @@ __global__ __launch_bounds__(256) void rt_launch_prep_kernel(rt::Counters* __res
     if (threadIdx.x < nb4 && n_big != 0u) {
         const uint32_t id = big_ids[min(threadIdx.x, n_big - 1u)];
         const rt::GeomRec g = geom[id];
-        tab[threadIdx.x] = make_float4(g.cx, g.cy, g.cz, g.rr);
+        tab[threadIdx.x] = make_float4(g.cx, g.cy, g.cz, radius[id]);
         reinterpret_cast<uint32_t*>(tab + rt::kBigMax)[threadIdx.x] = id;
     }
     __syncthreads();   // the words below were zeroed by other threads of the block
@@ -2199,7 +2200,7 @@ static uint32_t stream_blocks(uint64_t n) {
 
 hipError_t launch_prep(const TraceParams& P, uint32_t work_head, float* tab, uint32_t n_cost, hipStream_t st) {
     const uint32_t blocks = n_cost > 4096u ? min(64u, (n_cost + 4095u) / 4096u) : 1u;
-    hipLaunchKernelGGL(rt_launch_prep_kernel, dim3(blocks), dim3(256), 0, st, P.counters, work_head, P.geom,
+    hipLaunchKernelGGL(rt_launch_prep_kernel, dim3(blocks), dim3(256), 0, st, P.counters, work_head, P.geom, P.radius,
                        P.big_ids, P.n_big, reinterpret_cast<float4*>(tab), P.tile_cost, n_cost);
     return hipGetLastError();
 }

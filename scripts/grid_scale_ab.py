@@ -2,7 +2,8 @@
 """A/B of the uniform grid's cell scale (tuning grid_scale, rt_grid.h kGridCellScale) on the
 config 3 frame, interleaved rounds in one process. The scale is applied when the scene is built, so
 every timed render follows its own set_scene (outside the timed region); every scale must render
-the same image. Usage: python scripts/grid_scale_ab.py SPP ROUNDS scale [scale ...]"""
+the same image. Usage: python scripts/grid_scale_ab.py SPP ROUNDS scale [scale ...] [--config5]
+(--config5: config 5's frame, 3840x2160 and the 99 860-sphere scene, grid built on the device)."""
 import sys
 
 import numpy as np
@@ -11,11 +12,13 @@ sys.path.insert(0, "ray-tracing-gpu-vulkan_amd")
 import torch  # noqa: E402
 import rtvk  # noqa: E402
 
-spp, rounds = int(sys.argv[1]), int(sys.argv[2])
-scales = [float(x) for x in sys.argv[3:]]
-W, H = 1920, 1080
+c5 = "--config5" in sys.argv
+argv = [a for a in sys.argv if a != "--config5"]
+spp, rounds = int(argv[1]), int(argv[2])
+scales = [float(x) for x in argv[3:]]
+W, H = (3840, 2160) if c5 else (1920, 1080)
 r = rtvk.Renderer(0)
-scene = rtvk.generateRandomScene(0.0, 11)
+scene = rtvk.generateRandomScene(0.0, 158 if c5 else 11)
 acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
 out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
 rci = rtvk.canonical_render_call_info(spp, W, H)
@@ -44,6 +47,6 @@ for rnd in range(rounds + 1):
             times[s].append(e0.elapsed_time(e1))
 r.tune(grid_scale=None)
 base = np.median(times[scales[0]])
-print(f"spp {spp}, {rounds} rounds: " + ", ".join(
+print(f"{'config 5 ' if c5 else ''}spp {spp}, {rounds} rounds: " + ", ".join(
     f"scale {s} [{forms[s]}] {np.median(v):.2f} ms ({(np.median(v) / base - 1) * 100:+.2f} %, min {min(v):.2f})"
     for s, v in times.items()), flush=True)
