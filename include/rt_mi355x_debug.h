@@ -77,8 +77,9 @@ int rt_debug_tile_cost(rt_context* ctx, uint32_t* out, uint64_t capacity, uint64
 /* Diagnostic (tests): copies one scene array of ctx to host memory. what: 0 geometry records,
  * 1 radii, 2 material records, 3 big-sphere ids, 4 LBVH nodes (padded), 5 LBVH nodes (unpadded),
  * 6 leaf geometry, 7 leaf ids, 8 info {u32 n_spheres, n_big, n_nodes, n_leaf_slots,
- * device_built, 0; f32 small_rmax, scene_radius}. *bytes = the array's size; RT_ERR_INVALID_ARGUMENT
- * when it exceeds capacity. */
+ * device_built, 0; f32 small_rmax, scene_radius}, 9 grid {u32 cells in x, y, z, cells, references}
+ * (zeros without a grid). *bytes = the array's size; RT_ERR_INVALID_ARGUMENT when it exceeds
+ * capacity. */
 int rt_debug_scene(rt_context* ctx, uint32_t what, void* out, uint64_t capacity, uint64_t* bytes);
 
 /*

@@ -1549,6 +1549,14 @@ int rt_debug_scene(rt_context* ctx, uint32_t what, void* out, uint64_t capacity,
         std::memcpy(out, &info, sizeof(info));
         return RT_OK;
     }
+    if (what == 9) {   // the uniform grid's layout (all 0 without a grid)
+        const rt::GridInfo gi = ctx->has_grid ? d.grid : rt::GridInfo{};
+        const uint32_t info[5] = {gi.n[0], gi.n[1], gi.n[2], gi.n_cells, gi.n_refs};
+        *bytes = sizeof(info);
+        if (!out || capacity < sizeof(info)) return fail(RT_ERR_INVALID_ARGUMENT, "capacity too small");
+        std::memcpy(out, info, sizeof(info));
+        return RT_OK;
+    }
     const void* src = nullptr;
     size_t n = 0;
     switch (what) {

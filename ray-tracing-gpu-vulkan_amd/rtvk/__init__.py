@@ -170,8 +170,13 @@ class Renderer:
                      4: (np.uint8, 32), 5: (np.uint8, 32), 6: (np.float32, 4), 7: (np.uint32, 1)}
 
     def scene_array(self, what: int) -> np.ndarray:
-        """Diagnostic copy of one device scene array (rt_debug_scene); what 8 returns a dict."""
+        """Diagnostic copy of one device scene array (rt_debug_scene); what 8 (scene) and 9 (grid
+        layout) return a dict."""
         nbytes = ctypes.c_uint64(0)
+        if what == 9:
+            g = (ctypes.c_uint32 * 5)()
+            check(self._lib.rt_debug_scene(self._ctx, 9, g, 20, ctypes.byref(nbytes)))
+            return {"n": (int(g[0]), int(g[1]), int(g[2])), "cells": int(g[3]), "refs": int(g[4])}
         if what == 8:
             raw = (ctypes.c_uint8 * 32)()
             check(self._lib.rt_debug_scene(self._ctx, 8, raw, 32, ctypes.byref(nbytes)))

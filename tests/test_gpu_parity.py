@@ -350,6 +350,7 @@ def test_grid_one_layer_and_layered_forms(rtvk, renderer, torch, oracle, builder
             a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=GRID, rng_mode=rng_mode, builder=builder)
             info = renderer.launch_info()
             assert info["form"].startswith("grid") and info["flat_grid"] == flat, info
+            assert (renderer.scene_array(9)["n"][1] == 1) == flat
             assert_same(a, o, ra, ro)
             assert (st.segments, st.samples) == rst[:2]
             a2, o2, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=GRID, rng_mode=rng_mode, builder=builder,
