@@ -9,7 +9,7 @@ Counts are static (each instruction once), not dynamic: a loop body counts once.
 
 usage: python scripts/isa_phases.py LISTING.s [KERNEL_SUBSTRING] [--json out]
        (listing: make -C ray-tracing-gpu-vulkan_amd asm DEVFLAGS="--offload-arch=gfx950 -fno-gpu-rdc -fno-slp-vectorize -DRT_ASM_MARKS")
-default kernel: the headline form rt_trace_grid_kernel<false, MODE_HASH, IN_LDS, !COOP, REC, !CQ>."""
+default kernel: the headline form rt_trace_grid_kernel<false, MODE_HASH, IN_LDS, !COOP, REC, !CQ, FLAT>."""
 import json
 import re
 import sys
@@ -17,7 +17,7 @@ from collections import Counter, OrderedDict
 
 PHASES = {0: "loop head", 4: "sample start", 5: "refill: hand-out", 6: "refill: block fetch", 1: "ray setup (big spheres)",
           2: "walk", 3: "shading", 7: "exit", -1: "prologue"}
-HEADLINE = "_ZN12_GLOBAL__N_120rt_trace_grid_kernelILb0ELi1ELb1ELb0ELb1ELb0EEEvN2rt11TraceParamsE"
+HEADLINE = "_ZN12_GLOBAL__N_120rt_trace_grid_kernelILb0ELi1ELb1ELb0ELb1ELb0ELb1EEEvN2rt11TraceParamsE"
 
 
 def classify(op: str) -> list:
