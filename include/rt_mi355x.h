@@ -27,7 +27,8 @@
  *                            Device pointers, caller's stream, asynchronous.
  *   rt_multi_*()             one process driving N devices (src/ray_trace.cpp:42-105 creates one
  *                            Vulkan device per GPU, :74-93 splits the image into bands): one RCCL
- *                            communicator over the devices (ncclCommInitAll), the image tiled into
+ *                            communicator over the devices (ncclCommInitAll; none for one device,
+ *                            whose frame has no collective), the image tiled into
  *                            8-row strips dealt round robin, every device's strips gathered to
  *                            device 0 over xGMI (grouped ncclSend/ncclRecv) and reordered there.
  *   rt_render()              host-pointer convenience wrapper (one call = one frame); rci_count > 1
@@ -206,7 +207,8 @@ int rt_resolve_rgba8(rt_context* ctx, const float* accum_rgba32f, uint64_t n_tex
 /* ---- multi-device (one process, N GPUs, RCCL over xGMI) ----------------------------- */
 typedef struct rt_multi rt_multi;
 /* Devices 0 .. n-1, n = min(gpu_count, visible devices) (>= 1): one context and one stream per
- * device and one RCCL communicator over them (ncclCommInitAll). */
+ * device and, for n > 1, one RCCL communicator over them (ncclCommInitAll); one device renders
+ * straight into the caller's buffers and builds no communicator. */
 int rt_multi_create(uint32_t gpu_count, rt_multi** out);
 int rt_multi_destroy(rt_multi* m);
 int rt_multi_device_count(const rt_multi* m, uint32_t* n);
@@ -234,8 +236,8 @@ int rt_multi_render(rt_multi* m, const RenderCallInfo* rci, const rt_options* op
                     float* accum_rgba32f, uint8_t* out_rgba8, void* stream);
 /* Sum over the devices of the last frame's statistics (synchronises). */
 int rt_multi_stats(rt_multi* m, rt_stats* out);
-/* {devices, ranks of the RCCL communicator (ncclCommCount), rows per strip, devices that rendered
- * rows in the last frame}. */
+/* {devices, ranks of the RCCL communicator (ncclCommCount; 0 for one device: no communicator),
+ * rows per strip, devices that rendered rows in the last frame}. */
 int rt_multi_info(const rt_multi* m, uint32_t* out4);
 /* Trace-kernel duration (ms, HIP events on the launch stream) of the last frame on each device
  * that rendered rows, in device order; *count = devices written (synchronises). */
