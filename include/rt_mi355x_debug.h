@@ -43,8 +43,8 @@ int rt_debug_tune(rt_context* ctx, const char* key, double value);
 /* Diagnostic: of ctx's last launch, {sample chunks per pixel (low 16 bits: of the LPT order's tail
  * tiles; high 16 bits: of its head tiles, 0 when the launch had no head), the kernel form it ran
  * (low 16 bits: rt_internal.h ACCEL_*, before any launch the scene's default form; bit 16: its
- * grid walk was the one-layer form, the grid one cell thick in y), its dynamic LDS bytes, CU
- * count}. */
+ * grid walk was the one-layer form, the grid one cell thick in y; bit 17: its camera rays started
+ * at the camera position itself, the pinhole shortcut), its dynamic LDS bytes, CU count}. */
 int rt_debug_launch_info(rt_context* ctx, uint32_t* out4);
 /* Diagnostic: per-phase cycle sums of ctx's last launch, filled only by -DRT_STAMPS builds. */
 int rt_debug_stamps(rt_context* ctx, uint64_t* out8);

@@ -155,6 +155,7 @@ struct rt_context {
     uint32_t last_accel = 0;                     // kernel form (rt::ACCEL_*) of the last launch, 0 = none yet
     size_t last_lds = 0;                         // its dynamic LDS bytes
     bool last_flat = false;                      // its grid walk was the one-layer form
+    bool last_pinhole = false;                   // its camera rays started at lf (TraceParams::pinhole_lf)
     // every colour the shaders can return lies in [0, 1] (RT_RNG_SAMPLE_HASH's fixed point needs it)
     bool colours_unit = true;
     // HIP events bracketing the trace kernel of the last kKernelEvents launches (ring; timing
@@ -365,6 +366,9 @@ void fill_camera(const RenderCallInfo& rci, rt::TraceParams& P) {
     auto put = [](float* d, F3 v) { d[0] = v.x; d[1] = v.y; d[2] = v.z; };
     put(P.lf, from); put(P.hor, hor); put(P.ver, ver); put(P.ulc, ulc); put(P.cup, cup); put(P.crt, right);
     P.half_aperture = aperture / 2.0f;
+    auto finite3 = [](F3 v) { return std::isfinite(v.x) && std::isfinite(v.y) && std::isfinite(v.z); };
+    P.pinhole_lf = (P.half_aperture == 0.0f && from.x != 0.0f && from.y != 0.0f && from.z != 0.0f &&
+                    finite3(right) && finite3(cup)) ? 1u : 0u;
     P.size_x = sx;
     P.size_y = sy;
     P.inv_size_x = 1.0 / double(sx);
@@ -1211,6 +1215,7 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     ctx->last_accel = accel;
     ctx->last_lds = lds;
     ctx->last_flat = flat;
+    ctx->last_pinhole = P.pinhole_lf != 0;
     const uint64_t texels = uint64_t(band_width) * band_height;
     if (mode == rt::MODE_HASH) {
         if (ctx->fixed_cap < texels) {
@@ -1525,7 +1530,7 @@ int rt_debug_launch_info(rt_context* ctx, uint32_t* out4) {
     if (!ctx || !out4) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     out4[0] = ctx->last_chunks;
     if (ctx->last_accel) {   // the kernel form the last launch actually ran
-        out4[1] = ctx->last_accel | (ctx->last_flat ? 0x10000u : 0u);
+        out4[1] = ctx->last_accel | (ctx->last_flat ? 0x10000u : 0u) | (ctx->last_pinhole ? 0x20000u : 0u);
         out4[2] = uint32_t(ctx->last_lds);
     } else {   // no launch yet: the default form of the current scene (camera within its pad radius)
         size_t lds = 0;

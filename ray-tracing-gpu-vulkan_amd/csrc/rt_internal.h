@@ -189,6 +189,9 @@ struct TraceParams {
     // Camera / viewport (shader.rgen:92-115), computed once per launch on the host.
     float lf[3], hor[3], ver[3], ulc[3], cup[3], crt[3];
     float half_aperture;
+    uint32_t pinhole_lf;           // 1: half_aperture = 0, lf has no zero component and crt / cup are
+                                   // finite, so the ray origin lf + rx crt + ry cup (rx, ry = +-0, or
+                                   // NaN when the disk sample is (0, 0)) is lf itself or NaN
     float size_x, size_y;          // full image size as float (shader.rgen:42)
     double inv_size_x, inv_size_y; // 1 / size, rounded to double (camera division, rt_kernels.hip)
     uint32_t number, spp, max_depth;

@@ -728,6 +728,16 @@ __device__ __forceinline__ void camera_ray(const rt::TraceParams& P, const Camer
     uy = float(double(uy) * P.inv_size_y);
     const float lxr = rnd_pm1(ps.seed);
     const float lyr = rnd_pm1(ps.seed);
+    V3 from;
+    if (P.pinhole_lf) {   // wave-uniform (launch parameter): the reference camera (aperture 0), every
+        // component of lf nonzero, crt and cup finite: rx and ry below are +-0 (or both NaN when the
+        // disk sample is (0, 0)), so lf + (rx crt + ry cup) is lf itself (or NaN), without the six
+        // products and sums and the 6 SGPRs of crt / cup (config 3 -0.65 %, reference stream -1.5 %,
+        // config 5 -0.75 %)
+        const bool nan = lxr == 0.0f && lyr == 0.0f;
+        const float q = __builtin_nanf("");
+        from = nan ? v3(q, q, q) : cam.lf;
+    } else {
     float rx, ry;
     if (P.half_aperture != 0.0f) {   // wave-uniform (launch parameter)
         const float l2 = __builtin_sqrtf(__builtin_fmaf(lyr, lyr, lxr * lxr));
@@ -743,7 +753,8 @@ __device__ __forceinline__ void camera_ray(const rt::TraceParams& P, const Camer
         rx = nan ? __builtin_nanf("") : __uint_as_float(sa ^ (__float_as_uint(lxr) & 0x80000000u));
         ry = nan ? __builtin_nanf("") : __uint_as_float(sa ^ (__float_as_uint(lyr) & 0x80000000u));
     }
-    const V3 from = add(cam.lf, add(scale(rx, cam.crt), scale(ry, cam.cup)));
+    from = add(cam.lf, add(scale(rx, cam.crt), scale(ry, cam.cup)));
+    }
     const V3 to = sub(add(cam.ulc, scale(ux, cam.hor)), scale(uy, cam.ver));
     o = from;
     v = sub(to, from);

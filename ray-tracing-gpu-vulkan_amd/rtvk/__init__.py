@@ -234,15 +234,16 @@ class Renderer:
     def launch_info(self) -> dict:
         """Of the last launch: sample chunks per pixel (of the LPT order's tail ranks; head_chunks:
         of its head ranks, None when there is no head), the kernel form it ran, its dynamic LDS
-        bytes, the CU count, and whether its grid walk was the one-layer form (flat_grid: the grid
-        is one cell thick in y) (rt_debug_launch_info)."""
+        bytes, the CU count, whether its grid walk was the one-layer form (flat_grid: the grid is
+        one cell thick in y) and whether its camera rays started at the camera position itself
+        (pinhole_origin) (rt_debug_launch_info)."""
         v = (ctypes.c_uint32 * 4)()
         check(self._lib.rt_debug_launch_info(self._ctx, v))
         forms = {1: "brute", 2: "lbvh-global", 3: "lbvh-lds", 4: "lbvh-octant-lds", 5: "lbvh-treelet", 6: "grid-lds", 7: "grid-global",
                  8: "grid-lds-coop", 9: "grid-global-coop", 10: "grid-lds-rec", 11: "grid-lds-cq", 12: "grid-lds-rec-cq"}
         return {"chunks": int(v[0]) & 0xffff, "head_chunks": (int(v[0]) >> 16) or None,
                 "form": forms.get(int(v[1]) & 0xffff, str(v[1])), "lds_bytes": int(v[2]), "cus": int(v[3]),
-                "flat_grid": bool(int(v[1]) >> 16)}
+                "flat_grid": bool((int(v[1]) >> 16) & 1), "pinhole_origin": bool((int(v[1]) >> 17) & 1)}
 
     def scatter_rows(self, src_accum, src_rgba8, rows, dst_accum, dst_rgba8, stream=None) -> None:
         """dst[rows[i]] = src[i] (device), the reorder after a multi-GPU gather; either image may

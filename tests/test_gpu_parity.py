@@ -644,6 +644,26 @@ def test_far_and_grazing_cameras(rtvk, renderer, torch, oracle, cam):
     assert_same(a, o, ra, ro)
 
 
+def test_pinhole_origin_shortcut_and_fallback(rtvk, renderer, torch, oracle):
+    """Camera rays start at the camera position itself (lf) when the host proves lf + rx crt + ry cup
+    is lf (aperture 0, every lf component nonzero); a camera position with a zero component takes
+    the general form. Both equal the oracle bit for bit, both streams, grid and brute force."""
+    W, H = 40, 24
+    sc = oracle.generate_scene()
+    for cam, shortcut in [((13.0, 2.0, 3.0), True), ((0.0, 2.0, 12.0), False), ((9.0, 0.0, -9.0), False),
+                          ((-0.0, 3.0, 10.0), False)]:
+        rci = oracle.render_call_info(2, W, H)
+        f = rci.view(np.float32)
+        f[8:11] = cam
+        f[12:15] = [-cam[0], 0.5 - cam[1], -cam[2]]
+        for rng_mode in (STREAM, HASH):
+            ra, ro, _ = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=rng_mode))
+            for accel in (LBVH, BRUTE):
+                a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=accel, rng_mode=rng_mode)
+                assert renderer.launch_info()["pinhole_origin"] == shortcut, cam
+                assert_same(a, o, ra, ro)
+
+
 def test_scatter_rows_reassembles_strips(rtvk, renderer, torch, oracle):
     """The multi-GPU reassembly on device: strips rendered through row maps, scattered back with
     rt_scatter_rows, equal the full-frame render (rtvk.dist's rank-0 step)."""
