@@ -1120,7 +1120,7 @@ __device__ __forceinline__ void setup_ray(const rt::TraceParams& P, Ray& r, uint
     // beyond it, and the (t bits, id) keys of the cooperative walk order the same way.
     r.best = 10000.0f;
     r.bi = 0xffffffffu;
-    if (P.n_big) big_group(r, sb0, ib0);
+    big_group(r, sb0, ib0);   // (without big spheres the table holds four inert records: no test)
     for (uint32_t k0 = 4; k0 < P.n_big; k0 += 4) {
         float sb[16];
         uint32_t ib[4];
@@ -1777,6 +1777,13 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
         UTIL(8, st == ST_TRACING);
         const uint32_t box0 = n_box;
         if (st == ST_TRACING) setup_ray(P, r, n_sph);
+        // Grid kernels always have a grid to walk: a compile-time fact instead of the launch test
+        // (a loop-invariant lane mask the compiler spilled and reloaded every segment). With the
+        // two changes beside it (the inert big-sphere records, the regate flag as a scalar select):
+        // config 3 -1.2 %, DESIGN.md §5.
+        if constexpr (LAYOUT == LAYOUT_GRID || LAYOUT == LAYOUT_GRID_L2 || LAYOUT == LAYOUT_GRID_COOP ||
+                      LAYOUT == LAYOUT_GRID_CQ)
+            r.walk = true;
         STAMP(2);
         if constexpr (LAYOUT == LAYOUT_GRID_COOP) {   // every lane of the wave takes part (tracing or not)
             grid_walk_coop<COUNT>(P, reinterpret_cast<const uint32_t*>(nodes4), leaf4, leaf_ids, r, st == ST_TRACING,
@@ -1793,9 +1800,11 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
             hr = load_hit(geom4, mat4, r.bi);
             rad = REC ? hr.g.w : P.radius[r.bi];
         }
-        const unsigned long long regate = __ballot(
-            st == ST_TRACING && (P.force_regate || (r.bi != 0xffffffffu && !aabb_hit(hr.g.x, hr.g.y, hr.g.z, rad, r.o,
-                                                                                       r.inv))));
+        // (the test-only flag replaces the ballot by a scalar select: folded into the per-lane
+        // predicate it became a loop-invariant 64-bit lane mask the compiler spilled and reloaded)
+        unsigned long long regate = __ballot(
+            st == ST_TRACING && r.bi != 0xffffffffu && !aabb_hit(hr.g.x, hr.g.y, hr.g.z, rad, r.o, r.inv));
+        if (P.force_regate) regate = __ballot(st == ST_TRACING);
         if (__builtin_expect(regate != 0ull, 0)) {
             regate_brute<COUNT>(P, reinterpret_cast<const float4*>(P.geom), lane, regate, r);
             if (((regate >> lane) & 1ull) && r.bi != 0xffffffffu) hr = load_hit(geom4, mat4, r.bi);
@@ -2014,6 +2023,12 @@ __global__ __launch_bounds__(256) void rt_launch_prep_kernel(rt::Counters* __res
         const rt::GeomRec g = geom[id];
         tab[threadIdx.x] = make_float4(g.cx, g.cy, g.cz, radius[id]);
         reinterpret_cast<uint32_t*>(tab + rt::kBigMax)[threadIdx.x] = id;
+    }
+    if (n_big == 0u && threadIdx.x < 4u) {   // four inert records (setup_ray tests the first four
+        // unconditionally): centre (1e19, 1e19, 1e19), radius 0: c = |oc|^2 >= 0 and D <= 0 by
+        // Cauchy-Schwarz, and any rounding-made candidate reports t ~ 1e19 > tMax
+        tab[threadIdx.x] = make_float4(1e19f, 1e19f, 1e19f, 0.0f);
+        reinterpret_cast<uint32_t*>(tab + rt::kBigMax)[threadIdx.x] = 0xffffffffu;
     }
     __syncthreads();   // the words below were zeroed by other threads of the block
     if (threadIdx.x == 0) {

@@ -323,6 +323,34 @@ def test_grid_lattice_axis_rays(rtvk, renderer, torch, oracle, builder):
 
 
 @pytest.mark.parametrize("builder", [None, "gpu"])
+def test_scene_without_big_spheres(rtvk, renderer, torch, oracle, builder):
+    """A scene of small spheres only (no ground): no big sphere, so the segment's exhaustive tests
+    run on four inert table records (setup_ray tests the first four unconditionally) that must never
+    report a hit. Grid, tree and brute-force walks equal the oracle bit for bit, both streams, host
+    and device builds."""
+    base = oracle.generate_scene()[4:5]
+    recs = []
+    for i in range(-5, 6):
+        for j in range(-5, 6):
+            r = base.copy()
+            r[0, :16].view(np.float32)[:] = [float(i) * 0.9, 0.2, float(j) * 0.9, 0.2]
+            recs.append(r)
+    sc = np.concatenate(recs)
+    W, H = 40, 24
+    rci = oracle.render_call_info(2, W, H)
+    f = rci.view(np.float32)
+    f[8:11] = [7.0, 3.0, -6.0]
+    f[12:15] = [-7.0, -2.8, 6.0]
+    for rng_mode in (STREAM, HASH):
+        ra, ro, rst = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=rng_mode))
+        for accel in (LBVH, GRID, LBVH_OCT, BRUTE):
+            a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=accel, rng_mode=rng_mode, builder=builder)
+            assert renderer.scene_array(8)["n_big"] == 0
+            assert_same(a, o, ra, ro)
+            assert (st.segments, st.samples) == rst[:2]
+
+
+@pytest.mark.parametrize("builder", [None, "gpu"])
 def test_grid_one_layer_and_layered_forms(rtvk, renderer, torch, oracle, builder):
     """The grid walks have a one-layer form (the grid one cell thick in y: the DDA steps x and z
     only), picked when the scene's grid has one cell row in y, as the canonical scenes' grids have,
