@@ -63,7 +63,7 @@ struct Tuning {
     double sample_chunks = kUnset;      // forced chunk count (tail count when the LPT order is split)
     double head_chunks = kUnset;        // head / tail split of the LPT order
     double tail_tiles_pm = kUnset;
-    double schedule = kUnset;           // 0 LPT (longest unit chain), 1 row-major, 2 LPT by tile sum
+    double schedule = kUnset;           // 0 LPT (longest unit chain), 1 row-major
     double refill_reserve = kUnset;     // units handed out one by one at the end of the queue
     double isolate_tiles = kUnset;      // reference stream: waves on the first LPT blocks take no more
     double sah_knobs = kUnset;          // host SAH builder variants (rt_bvh.h)
@@ -1234,8 +1234,8 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
         P.fixed = ctx->fixed;
     }
     // Longest-processing-time-first hand-out from the last launch of this band geometry: tiles
-    // in descending order of their longest unit chain (tuning schedule 1 = row-major, 2 = by the
-    // tile's summed chains: A/B only); this launch records the next costs.
+    // in descending order of their longest unit chain (tuning schedule 1 = row-major; the summed
+    // chains instead: an -DRT_TILE_COST_SUM build, A/B only); this launch records the next costs.
     if (accel != rt::ACCEL_BRUTE) {
         rt::TileSchedule& sc = ctx->sched;
         RT_HIP(rt::schedule_reserve(sc, uint32_t(n_tiles), st));
@@ -1245,8 +1245,8 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
             RT_HIP(rt::schedule_order(sc, st));
             P.tile_order = sc.order;
         }
-        P.tile_cost = sc.cost[sc.cur];   // zeroed by the launch's prep kernel
-        P.tile_cost_sum = sched == 2 ? 1u : 0u;
+        P.tile_cost = sc.cost[sc.cur];   // zeroed by the launch's prep kernel (-DRT_TILE_COST_SUM
+                                         // builds record the tile's summed chains instead of the longest)
     }
     // Head and tail of the LPT order (HASH): the frame's tail is made of the units
     // still running when the queue runs dry, so only the last ranks (the shortest fifth of the

@@ -218,7 +218,6 @@ struct TraceParams {
     const uint32_t* tile_order;    // optional: hand-out rank -> 8x8 tile index (null: row-major)
     uint32_t* tile_cost;           // optional: per 8x8 tile, traced segments of its longest unit
                                    // (zeroed by the host)
-    uint32_t tile_cost_sum;        // A/B only: record the tile's total instead
     // scene
     uint32_t n_spheres;
     const GeomRec* geom;

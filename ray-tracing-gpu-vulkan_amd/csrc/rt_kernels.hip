@@ -914,11 +914,15 @@ __device__ __forceinline__ bool shade(const rt::TraceParams& P, const Camera& ca
 // frame ends with the longest chain.
 template <int MODE>
 __device__ __forceinline__ void record_tile_cost(const rt::TraceParams& P, const Path& ps) {
-    if (!P.tile_cost) return;
+    // (P.tile_cost is set for every walk kernel, the only callers)
     if (MODE == rt::MODE_HASH && (ps.px & 0x00010001u)) return;
     const uint32_t lx = ps.px & 0xffffu, ly = ps.px >> 16;
     uint32_t* c = &P.tile_cost[(ly >> 3) * P.tiles_x + (lx >> 3)];
-    if (P.tile_cost_sum) atomicAdd(c, ps.segs); else atomicMax(c, ps.segs);
+#ifdef RT_TILE_COST_SUM   // A/B build: order tiles by their summed chains instead
+    atomicAdd(c, ps.segs);
+#else
+    atomicMax(c, ps.segs);
+#endif
 }
 
 // Waves per SIMD the register budget is sized for. Brute force: 6 (71 VGPRs, no spills). LBVH:
@@ -1094,7 +1098,7 @@ __device__ __forceinline__ void big_group(Ray& r, const float (&sb)[16], const u
 }
 
 // New segment: hoisted per-ray terms and the exhaustive big spheres.
-__device__ __forceinline__ void setup_ray(const rt::TraceParams& P, Ray& r, uint32_t& n_sph) {
+__device__ __forceinline__ void setup_ray(const rt::TraceParams& P, Ray& r) {
     // records and ids through the scalar cache (TraceParams::big_tab, SGPR operands, no LDS round
     // trip: config 3 -1.6 %, reference stream -1.7 %, config 5 -2.2 % against an LDS table); the
     // four discriminants stay in registers for the candidate passes, which run per sphere with a
@@ -1130,7 +1134,6 @@ __device__ __forceinline__ void setup_ray(const rt::TraceParams& P, Ray& r, uint
         for (uint32_t k = 0; k < 4; ++k) ib[k] = gid[k0 + k];
         big_group(r, sb, ib);
     }
-    n_sph += P.n_big;
     r.limit = cull_limit(P, r.best);
     r.walk = P.nodes != nullptr || P.cell_start != nullptr;
 }
@@ -1776,7 +1779,10 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
         STAMP(1);
         UTIL(8, st == ST_TRACING);
         const uint32_t box0 = n_box;
-        if (st == ST_TRACING) setup_ray(P, r, n_sph);
+        // every lane (a lane that is not tracing computes on its last ray and discards the result):
+        // inside a per-lane branch the big-sphere loop's launch-uniform bound became a spilled lane mask
+        setup_ray(P, r);
+        if (COUNT && st == ST_TRACING) n_sph += P.n_big;
         // Grid kernels always have a grid to walk: a compile-time fact instead of the launch test
         // (a loop-invariant lane mask the compiler spilled and reloaded every segment). With the
         // two changes beside it (the inert big-sphere records, the regate flag as a scalar select):
