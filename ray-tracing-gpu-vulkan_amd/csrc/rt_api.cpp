@@ -970,14 +970,15 @@ uint32_t choose_accel(const rt_context* ctx, bool brute, uint32_t form, float ca
         // the LDS grid kernel also stages the winner's gate and shading records ({c, r} + the
         // material record, 48 B per sphere) when two blocks per CU still fit;
         // tuning grid_rec = 0: not (A/B)
-        const size_t rec_bytes = size_t(d.n_spheres) * 48u;
+        // (the kernel's static table of kRecStatic records: scenes of at most that many spheres)
+        const size_t rec_bytes = d.n_spheres <= rt::kRecStatic ? size_t(rt::kRecStatic) * 48u : kMaxLdsBytes;
         // the wave-wide candidate queue: form 16, or tuning grid_cq = 1
         const bool cq = accel == rt::ACCEL_GRID && (form == 16u || (form == 0u && Tuning::get(tu.grid_cq, 0) == 1));
         const size_t cq_bytes = cq ? rt::kCqLdsBytes : 0u;
         if (accel == rt::ACCEL_GRID && Tuning::get(tu.grid_rec, 1) != 0 &&
             ctx->grid_bytes + rec_bytes + rt::kLaneSumLdsBytes + cq_bytes <= kTwoBlockLdsBytes) {
             accel = cq ? rt::ACCEL_GRID_REC_CQ : rt::ACCEL_GRID_REC;
-            lds = ctx->grid_bytes + rec_bytes;
+            lds = ctx->grid_bytes;   // (the records: static LDS of the kernel)
         } else if (cq && ctx->grid_bytes + rt::kLaneSumLdsBytes + cq_bytes <= kMaxLdsBytes) {
             accel = rt::ACCEL_GRID_CQ;
         }

@@ -262,6 +262,7 @@ constexpr uint32_t kFixedFlush = 128;
 // records (center, radius) and ids into TraceParams::big_tab before each launch; the walk kernels
 // read them through the scalar cache (rt_kernels.hip setup_ray).
 constexpr uint32_t kBigMax = 64;
+constexpr uint32_t kRecStatic = 512;   // spheres of the REC grid kernels' static LDS record table
 constexpr uint32_t kNoRowsLds = 0xffffffffu;
 constexpr uint32_t kHashMaxSpp = 1u << 19;
 

@@ -809,6 +809,15 @@ __device__ __forceinline__ HitRec load_hit(const float4* __restrict__ geom4, con
     return HitRec{geom4[bi], mat4[2 * bi], mat4[2 * bi + 1]};
 }
 
+// The REC grid kernels' gate and shading records, {c, r} + the material record of a sphere side by
+// side (48 B), in a static LDS table at a fixed address: a record's address is 48 bi with no base
+// register (the dynamic table's two bases were spilled SGPRs reloaded every segment: config 3
+// -0.5 %). Scenes of at most kRecStatic spheres (the host's choice of the form).
+__shared__ float4 s_rec[3 * rt::kRecStatic];
+__device__ __forceinline__ HitRec load_hit_rec(uint32_t bi) {
+    return HitRec{s_rec[3 * bi], s_rec[3 * bi + 1], s_rec[3 * bi + 2]};
+}
+
 // hr: the records of sphere bi (load_hit), loaded by the caller so that they can travel with the
 // winner gate's loads (lbvh_loop); unused on a miss.
 template <int MODE, bool LSUM>
@@ -1803,7 +1812,8 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
         HitRec hr{};
         float rad = 0.0f;
         if (st == ST_TRACING && r.bi != 0xffffffffu) {
-            hr = load_hit(geom4, mat4, r.bi);
+            if constexpr (REC) hr = load_hit_rec(r.bi);
+            else hr = load_hit(geom4, mat4, r.bi);
             rad = REC ? hr.g.w : P.radius[r.bi];
         }
         // (the test-only flag replaces the ballot by a scalar select: folded into the per-lane
@@ -1813,7 +1823,10 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
         if (P.force_regate) regate = __ballot(st == ST_TRACING);
         if (__builtin_expect(regate != 0ull, 0)) {
             regate_brute<COUNT>(P, reinterpret_cast<const float4*>(P.geom), lane, regate, r);
-            if (((regate >> lane) & 1ull) && r.bi != 0xffffffffu) hr = load_hit(geom4, mat4, r.bi);
+            if (((regate >> lane) & 1ull) && r.bi != 0xffffffffu) {
+                if constexpr (REC) hr = load_hit_rec(r.bi);
+                else hr = load_hit(geom4, mat4, r.bi);
+            }
         }
         if (COUNT && st == ST_TRACING) {   // walk-length histogram (diagnostic, COUNT builds only)
             const uint32_t len = min(n_box - box0, 63u);
@@ -1925,7 +1938,8 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
 }
 
 // Grid kernel (ACCEL_GRID): the grid's cell offsets and references staged in LDS once per
-// persistent block: [references (float4) | reference ids | cell offsets | shading records (REC)].
+// persistent block: [references (float4) | reference ids | cell offsets] in dynamic LDS, and with
+// REC the shading records in the static table s_rec.
 // FLAT: the grid is one cell thick in y, as every grid of a scene whose small spheres lie in one
 // layer is (configs 3 and 5): the DDA steps x and z only (grid_walk; launch_trace picks it).
 template <bool COUNT, int MODE, bool IN_LDS, bool COOP = false, bool REC = false, bool CQ = false, bool FLAT = false>
@@ -1944,7 +1958,7 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
         return;
     }
     const uint32_t nr = P.grid.n_refs, nc1 = P.grid.n_cells + 1u;
-    const uint32_t n_id4 = (nr + 3u) / 4u, n_cs4 = (nc1 + 3u) / 4u;
+    const uint32_t n_id4 = (nr + 3u) / 4u;
     const float4* rec = reinterpret_cast<const float4*>(P.grid_rec);
     for (uint32_t i = threadIdx.x; i < nr; i += kTraceBlock) lds[i] = rec[i];
     uint32_t* ids = reinterpret_cast<uint32_t*>(lds + nr);
@@ -1954,18 +1968,17 @@ __global__ __launch_bounds__(kTraceBlock, RT_TRACE_WAVES_PER_SIMD) void rt_trace
     stage_walk_params(P, threadIdx.x);
     stage_rows(P, threadIdx.x, kTraceBlock);
     if (REC) {   // the winner's gate and shading records in LDS too: {cx, cy, cz, r} + 2 x MatRec float4
-        float4* srec = lds + nr + n_id4 + n_cs4;
-        float4* smat = srec + P.n_spheres;
         const float4* mat4 = reinterpret_cast<const float4*>(P.mat);
-        for (uint32_t i = threadIdx.x; i < P.n_spheres; i += kTraceBlock) {
+        const uint32_t n = min(P.n_spheres, rt::kRecStatic);   // the host picks REC only within the table
+        for (uint32_t i = threadIdx.x; i < n; i += kTraceBlock) {
             const rt::GeomRec g = P.geom[i];
-            srec[i] = make_float4(g.cx, g.cy, g.cz, P.radius[i]);
-            smat[2 * i] = mat4[2 * i];
-            smat[2 * i + 1] = mat4[2 * i + 1];
+            s_rec[3 * i] = make_float4(g.cx, g.cy, g.cz, P.radius[i]);
+            s_rec[3 * i + 1] = mat4[2 * i];
+            s_rec[3 * i + 2] = mat4[2 * i + 1];
         }
         __syncthreads();
         lbvh_loop<COUNT, CQ ? LAYOUT_GRID_CQ : LAYOUT_GRID, MODE, true, FLAT>(P, reinterpret_cast<const float4*>(cst), lds,
-                                                                              ids, srec, smat);
+                                                                              ids, s_rec, s_rec);   // (load_hit_rec)
         return;
     }
     __syncthreads();
