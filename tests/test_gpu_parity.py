@@ -322,6 +322,29 @@ def test_grid_lattice_axis_rays(rtvk, renderer, torch, oracle, builder):
             assert_same(a, o, ra, ro)
 
 
+def test_more_than_four_big_spheres(rtvk, renderer, torch, oracle):
+    """The production kernels test the first four big spheres as one group; a scene with more (the
+    canonical scene plus three more radius-1 spheres and one of radius 2.5) takes the general form,
+    which loops over the further groups. Grid, tree and brute-force walks equal the oracle bit for
+    bit, both streams."""
+    sc = oracle.generate_scene()
+    extra = []
+    for k, (x, z, rad) in enumerate([(0.0, 4.0, 1.0), (-4.0, 4.0, 1.0), (4.0, -4.0, 1.0), (-6.0, -6.0, 2.5)]):
+        r = sc[1:2].copy()
+        r[0, :16].view(np.float32)[:] = [x, rad, z, rad]
+        extra.append(r)
+    sc = np.concatenate([sc] + extra)
+    W, H = 40, 24
+    rci = oracle.render_call_info(2, W, H)
+    for rng_mode in (STREAM, HASH):
+        ra, ro, rst = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=rng_mode))
+        for accel in (LBVH, GRID, LBVH_OCT, BRUTE):
+            a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=accel, rng_mode=rng_mode)
+            assert renderer.scene_array(8)["n_big"] > 4
+            assert_same(a, o, ra, ro)
+            assert (st.segments, st.samples) == rst[:2]
+
+
 @pytest.mark.parametrize("builder", [None, "gpu"])
 def test_scene_without_big_spheres(rtvk, renderer, torch, oracle, builder):
     """A scene of small spheres only (no ground): no big sphere, so the segment's exhaustive tests
