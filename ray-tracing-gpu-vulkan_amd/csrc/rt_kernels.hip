@@ -710,7 +710,8 @@ __device__ __forceinline__ void finish_unit(const rt::TraceParams& P, Path& ps) 
 
 // shader.rgen:56-58 + 107-115: camera ray of sample ps.s of the lane's unit: origin o and the
 // direction before normalisation, v = to - from (the caller normalises it).
-template <int MODE>
+// FAST: a launch the host proved pinhole_lf for (the one-layer L2 grid kernel, lbvh_loop SPEC).
+template <int MODE, bool FAST = false>
 __device__ __forceinline__ void camera_ray(const rt::TraceParams& P, const Camera& cam, Path& ps, V3& o, V3& v) {
     UTIL(7, true);
     const uint32_t lx = ps.px & 0xffffu, ly = ps.px >> 16;
@@ -729,7 +730,7 @@ __device__ __forceinline__ void camera_ray(const rt::TraceParams& P, const Camer
     const float lxr = rnd_pm1(ps.seed);
     const float lyr = rnd_pm1(ps.seed);
     V3 from;
-    if (P.pinhole_lf) {   // wave-uniform (launch parameter): the reference camera (aperture 0), every
+    if (FAST || P.pinhole_lf) {   // wave-uniform (launch parameter): the reference camera (aperture 0), every
         // component of lf nonzero, crt and cup finite: rx and ry below are +-0 (or both NaN when the
         // disk sample is (0, 0)), so lf + (rx crt + ry cup) is lf itself (or NaN), without the six
         // products and sums and the 6 SGPRs of crt / cup (config 3 -0.65 %, reference stream -1.5 %,
@@ -764,7 +765,7 @@ __device__ __forceinline__ void camera_ray(const rt::TraceParams& P, const Camer
 
 // First camera ray of a unit just taken. Returns false when the unit has no samples (spp = 0:
 // stored at once); later samples start inside shade().
-template <int MODE, bool LSUM>
+template <int MODE, bool LSUM, bool FAST = false>
 __device__ __forceinline__ bool start_sample(const rt::TraceParams& P, const Camera& cam, Path& ps,
                                              V3& o, V3& d) {
     if (ps.s >= ps.s_end) {
@@ -772,7 +773,7 @@ __device__ __forceinline__ bool start_sample(const rt::TraceParams& P, const Cam
         return false;
     }
     V3 v;
-    camera_ray<MODE>(P, cam, ps, o, v);
+    camera_ray<MODE, FAST>(P, cam, ps, o, v);
     d = normalize(v);
     return true;
 }
@@ -820,7 +821,7 @@ __device__ __forceinline__ HitRec load_hit_rec(uint32_t bi) {
 
 // hr: the records of sphere bi (load_hit), loaded by the caller so that they can travel with the
 // winner gate's loads (lbvh_loop); unused on a miss.
-template <int MODE, bool LSUM>
+template <int MODE, bool LSUM, bool FAST = false>
 __device__ __forceinline__ bool shade_rec(const rt::TraceParams& P, const Camera& cam, const HitRec& hr, Path& ps,
                                           uint32_t bi, float best, V3& o, V3& d, bool& fresh) {
     V3 att;
@@ -899,7 +900,7 @@ __device__ __forceinline__ bool shade_rec(const rt::TraceParams& P, const Camera
     if (!more) {
         sample_end<MODE, LSUM>(P, ps, col);
         if (ps.s < ps.s_end) {   // the unit's next sample
-            camera_ray<MODE>(P, cam, ps, o, v);
+            camera_ray<MODE, FAST>(P, cam, ps, o, v);
             more = fresh = true;
         }
     }
@@ -1107,6 +1108,7 @@ __device__ __forceinline__ void big_group(Ray& r, const float (&sb)[16], const u
 }
 
 // New segment: hoisted per-ray terms and the exhaustive big spheres.
+template <bool FAST = false>   // FAST: at most 4 big spheres (the one-layer L2 grid kernel, lbvh_loop SPEC)
 __device__ __forceinline__ void setup_ray(const rt::TraceParams& P, Ray& r) {
     // records and ids through the scalar cache (TraceParams::big_tab, SGPR operands, no LDS round
     // trip: config 3 -1.6 %, reference stream -1.7 %, config 5 -2.2 % against an LDS table); the
@@ -1134,7 +1136,7 @@ __device__ __forceinline__ void setup_ray(const rt::TraceParams& P, Ray& r) {
     r.best = 10000.0f;
     r.bi = 0xffffffffu;
     big_group(r, sb0, ib0);   // (without big spheres the table holds four inert records: no test)
-    for (uint32_t k0 = 4; k0 < P.n_big; k0 += 4) {
+    for (uint32_t k0 = 4; !FAST && k0 < P.n_big; k0 += 4) {
         float sb[16];
         uint32_t ib[4];
 #pragma unroll
@@ -1739,6 +1741,11 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
                                           const float4* __restrict__ leaf4,
                                           const uint32_t* __restrict__ leaf_ids,
                                           const float4* __restrict__ geom4, const float4* __restrict__ mat4) {
+    // the one-layer L2 grid kernel (config 5's) also takes pinhole_lf and at most four big spheres
+    // as compile-time facts (flat_grid_form: the host proves both): no camera test and no further
+    // big-sphere groups in its segment loop (config 5 -0.5 %; the same for the LDS kernels measured
+    // +0.64 % on config 3)
+    constexpr bool SPEC = FLAT && LAYOUT == LAYOUT_GRID_L2;
     constexpr bool LSUM = MODE == rt::MODE_HASH &&
                           (LAYOUT == LAYOUT_GRID || LAYOUT == LAYOUT_GRID_L2 || LAYOUT == LAYOUT_GRID_COOP ||
                            LAYOUT == LAYOUT_GRID_CQ);
@@ -1771,7 +1778,7 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
         STAMP(4);
         bool started = false;
         if (st == ST_NEED_SAMPLE) {
-            if (start_sample<MODE, LSUM>(P, cam, ps, r.o, r.d)) {
+            if (start_sample<MODE, LSUM, SPEC>(P, cam, ps, r.o, r.d)) {
                 st = ST_TRACING;
                 started = true;
             } else {   // empty unit (spp = 0): stored at once
@@ -1790,7 +1797,7 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
         const uint32_t box0 = n_box;
         // every lane (a lane that is not tracing computes on its last ray and discards the result):
         // inside a per-lane branch the big-sphere loop's launch-uniform bound became a spilled lane mask
-        setup_ray(P, r);
+        setup_ray<SPEC>(P, r);
         if (COUNT && st == ST_TRACING) n_sph += P.n_big;
         // Grid kernels always have a grid to walk: a compile-time fact instead of the launch test
         // (a loop-invariant lane mask the compiler spilled and reloaded every segment). With the
@@ -1841,7 +1848,7 @@ __device__ __forceinline__ void lbvh_loop(const rt::TraceParams& P, const float4
         bool fresh = false;   // a sample started inside shade()
         if (st == ST_TRACING) {
             ps.segs++;
-            if (!shade_rec<MODE, LSUM>(P, cam, hr, ps, r.bi, r.best, r.o, r.d, fresh)) {
+            if (!shade_rec<MODE, LSUM, SPEC>(P, cam, hr, ps, r.bi, r.best, r.o, r.d, fresh)) {
                 // The unit's last sample ended: finish it here, and the lane asks for a unit at
                 // the top of the next iteration.
                 finish_unit<MODE, LSUM>(P, ps);
@@ -2223,6 +2230,7 @@ static const void* pick(uint32_t accel, bool count, int mode, bool flat) {
 }
 
 bool flat_grid_form(const TraceParams& P, uint32_t accel, bool count) {
+    if (accel == ACCEL_GRID_GLOBAL && !(P.n_big <= 4u && P.pinhole_lf)) return false;   // (lbvh_loop SPEC)
     return !count && P.cell_start != nullptr && P.grid.n[1] == 1u &&
            (accel == ACCEL_GRID || accel == ACCEL_GRID_REC || accel == ACCEL_GRID_GLOBAL);
 }

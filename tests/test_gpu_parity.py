@@ -322,7 +322,8 @@ def test_grid_lattice_axis_rays(rtvk, renderer, torch, oracle, builder):
             assert_same(a, o, ra, ro)
 
 
-def test_more_than_four_big_spheres(rtvk, renderer, torch, oracle):
+@pytest.mark.parametrize("builder", [None, "gpu"])
+def test_more_than_four_big_spheres(rtvk, renderer, torch, oracle, builder):
     """The production kernels test the first four big spheres as one group; a scene with more (the
     canonical scene plus three more radius-1 spheres and one of radius 2.5) takes the general form,
     which loops over the further groups. Grid, tree and brute-force walks equal the oracle bit for
@@ -339,7 +340,7 @@ def test_more_than_four_big_spheres(rtvk, renderer, torch, oracle):
     for rng_mode in (STREAM, HASH):
         ra, ro, rst = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=rng_mode))
         for accel in (LBVH, GRID, LBVH_OCT, BRUTE):
-            a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=accel, rng_mode=rng_mode)
+            a, o, st = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=accel, rng_mode=rng_mode, builder=builder)
             assert renderer.scene_array(8)["n_big"] > 4
             assert_same(a, o, ra, ro)
             assert (st.segments, st.samples) == rst[:2]
@@ -695,7 +696,8 @@ def test_far_and_grazing_cameras(rtvk, renderer, torch, oracle, cam):
     assert_same(a, o, ra, ro)
 
 
-def test_pinhole_origin_shortcut_and_fallback(rtvk, renderer, torch, oracle):
+@pytest.mark.parametrize("builder", [None, "gpu"])
+def test_pinhole_origin_shortcut_and_fallback(rtvk, renderer, torch, oracle, builder):
     """Camera rays start at the camera position itself (lf) when the host proves lf + rx crt + ry cup
     is lf (aperture 0, every lf component nonzero); a camera position with a zero component takes
     the general form. Both equal the oracle bit for bit, both streams, grid and brute force."""
@@ -710,7 +712,8 @@ def test_pinhole_origin_shortcut_and_fallback(rtvk, renderer, torch, oracle):
         for rng_mode in (STREAM, HASH):
             ra, ro, _ = oracle.render(sc, rci, W, H, opts=oracle.options(rng_mode=rng_mode))
             for accel in (LBVH, BRUTE):
-                a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=accel, rng_mode=rng_mode)
+                a, o, _ = gpu_render(rtvk, renderer, torch, sc, rci, W, H, accel=accel, rng_mode=rng_mode,
+                                     builder=builder)
                 assert renderer.launch_info()["pinhole_origin"] == shortcut, cam
                 assert_same(a, o, ra, ro)
 
