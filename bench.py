@@ -5,7 +5,8 @@ One step = one frame of the hot path: every pixel of the image traced at `spp` s
 on the canonical scene (generateRandomScene(t=0): 488 spheres, camera (13,11,-3) -> origin),
 rebuilding the acceleration structure as the reference does every frame. Default workload:
 BASELINE config 3 (1920x1080, 10 000 spp, LBVH + persistent threads); on N GPUs the same frame is
-tiled into 8-row strips over the ranks and gathered to rank 0 over RCCL (config 4 at N = 8):
+tiled into row-exact strips over the ranks, re-dealt from their kernel times, and gathered to
+rank 0 over RCCL (config 4 at N = 8):
 strong scaling. `--config 2` (100 spp, brute force) and `--config 5` (3840x2160, 99 860 spheres,
 1 000 spp) select the other BASELINE configs.
 
@@ -520,7 +521,7 @@ def main() -> int:
 
     import rtvk
     from rtvk import abi
-    from rtvk.dist import DistributedRenderer, hip_assembler, hip_band_renderer, hip_resolver, strip_rows
+    from rtvk.dist import DistributedRenderer, hip_assembler, hip_band_renderer, hip_band_timer, hip_resolver
 
     launched = "WORLD_SIZE" in os.environ
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -592,8 +593,9 @@ def main() -> int:
 
     multi_info = None
     if mode == "multi":
-        # One process drives every GPU through the C-ABI (rt_multi: ncclCommInitAll, 8-row strips
-        # dealt round robin, grouped ncclSend / ncclRecv of every strip to GPU 0, reorder there):
+        # One process drives every GPU through the C-ABI (rt_multi: ncclCommInitAll, row-exact
+        # strips re-dealt from the devices' kernel times, grouped ncclSend / ncclRecv of every
+        # device's rows to GPU 0, reorder there):
         # the code the reference's ray_trace(gpu_count) binds (src/ray_trace.cpp:42-105, :922-972).
         mr = rtvk.MultiRenderer(n_gpus)
         if mr.device_count != n_gpus:
@@ -621,9 +623,12 @@ def main() -> int:
                 self.renderer = rtvk.Renderer(local)
                 self.stream = torch.cuda.Stream(device=dev)
                 with torch.cuda.stream(self.stream):
+                    # rows re-dealt between frames from every rank's kernel time and per-row work of
+                    # the frame two before (rtvk.dist, rt_partition_rebalance)
                     self.dr = DistributedRenderer(W, H, dev, hip_band_renderer(self.renderer, rci, opts),
                                                   hip_assembler(self.renderer),
-                                                  resolve=hip_resolver(self.renderer, spp))
+                                                  resolve=hip_resolver(self.renderer, spp),
+                                                  timer=hip_band_timer(self.renderer))
                 self.launches = 0
 
             def frame(self):
@@ -782,15 +787,16 @@ def main() -> int:
         default_shape = (W, H, spp, grid, accel_name) == CONFIGS[args.config]
         walk = "brute-force sphere list (scalar cache)" if form == "brute" else WALK_NAMES.get(form, (form, form))[1]
         if mode == "multi":
-            par = (f"rt_multi (C-ABI, one process): {multi_info['devices']} GPUs, {multi_info['strip_rows']}-row "
-                   f"strips dealt round robin, "
+            par = (f"rt_multi (C-ABI, one process): {multi_info['devices']} GPUs, row-exact interleaved "
+                   f"{multi_info['strip_rows']}-row strips re-dealt between frames from the devices' kernel times, "
                    + (f"RCCL grouped ncclSend/ncclRecv gather of every other GPU's accumulator strips to GPU 0 "
                       f"(ncclCommInitAll communicator of {multi_info['rccl_ranks']} ranks) + device reorder + "
                       f"resolve on GPU 0" if multi_info["devices"] > 1 else
                       "one GPU renders straight into the caller's buffers (no communicator, no collective)"))
         elif mode == "per-process":
-            par = (f"torch.distributed ({backend}): {world} processes, one per GPU, 8-row strips round robin + "
-                   f"gather of the float4 accumulator strips to rank 0 + device reorder + rgba8 resolve on rank 0")
+            par = (f"torch.distributed ({backend}): {world} processes, one per GPU, row-exact interleaved 8-row "
+                   f"strips re-dealt between frames from the ranks' kernel times (gloo exchange of per-row costs) + "
+                   f"gather of the float4 accumulator rows to rank 0 + device reorder + rgba8 resolve on rank 0")
         else:
             par = "1 GPU"
         result = {
@@ -850,10 +856,17 @@ def main() -> int:
                 mean = sum(per_device_ms) / len(per_device_ms)
                 result["per_device_kernel_ms"] = [round(v, 3) for v in per_device_ms]
                 result["imbalance"] = round(max(per_device_ms) / mean, 4) if mean > 0 else None
-                result["rows_per_device"] = [len(strip_rows(r, n_gpus, H)) for r in range(n_gpus)]
+                if mode == "multi":
+                    result["rows_per_device"] = [len(p) for p in mr.partition(H)]
+                    result["balance"] = mr.balance_info()
+                else:
+                    result["rows_per_device"] = dr.rows_per_rank()
+                    result["balance"] = {"frames": dr.launches, "rebalances": dr.rebalances,
+                                         "rows_moved": dr.rows_moved, "predicted_imbalance": round(dr.predicted, 5)}
                 result["imbalance_basis"] = ("max / mean over devices of each device's mean trace-kernel ms over "
                                              "the timed frames (HIP events on its launch stream); rows_per_device: "
-                                             "8-row strips dealt round robin")
+                                             "the balancer's partition after the timed frames (row-exact strips "
+                                             "re-dealt from the kernel times of the frame two before)")
         if n_gpus == 1:
             frame_np = (fa.cpu().numpy(), fo.cpu().numpy())
     # Side lines (single GPU): the same frame with the other random stream and with the LBVH walk

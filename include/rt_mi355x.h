@@ -28,9 +28,14 @@
  *   rt_multi_*()             one process driving N devices (src/ray_trace.cpp:42-105 creates one
  *                            Vulkan device per GPU, :74-93 splits the image into bands): one RCCL
  *                            communicator over the devices (ncclCommInitAll; none for one device,
- *                            whose frame has no collective), the image tiled into
- *                            8-row strips dealt round robin, every device's strips gathered to
- *                            device 0 over xGMI (grouped ncclSend/ncclRecv) and reordered there.
+ *                            whose frame has no collective), the image tiled into row-exact
+ *                            interleaved 8-row strips, every device's rows gathered to
+ *                            device 0 over xGMI (grouped ncclSend/ncclRecv) and reordered there,
+ *                            the rows re-dealt from measured device times between frames.
+ *   rt_partition_*()         the row split and its re-deal (src/ray_trace.cpp:74-81 band extents,
+ *                            src/workload_tuner.hpp:38-104 get_workload fed by the per-GPU frame
+ *                            times of src/ray_trace.cpp:750-762), host only, for callers that run
+ *                            one process per GPU (rtvk/dist.py).
  *   rt_render()              host-pointer convenience wrapper (one call = one frame); rci_count > 1
  *                            renders one band per GPU like src/ray_trace.cpp:74-93, gathered by RCCL.
  *
@@ -179,6 +184,17 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
                      uint8_t* out_rgba8, const rt_options* opt, void* stream);
 /* Statistics of the last completed rt_render_device (synchronises ctx's last stream). */
 int rt_get_stats(rt_context* ctx, rt_stats* out);
+/* Trace-kernel duration (ms, HIP events on the launch stream) of ctx's launch `back` launches
+ * before its most recent one (0 = the most recent; the last 64 are kept). Waits for that launch's
+ * end only, not for launches queued after it: a frame loop reads the launch of two frames ago
+ * without draining its queue (the per-GPU frame times the reference's tuner reads,
+ * src/ray_trace.cpp:636-644, :750-762). */
+int rt_launch_ms(rt_context* ctx, uint32_t back, float* ms);
+/* Per band row of the same launch (one of ctx's last 4 grid / LBVH launches; band_rows = its band
+ * height), the row's share of the launch's work as its 8x8 tile-cost record estimates it (each
+ * tile's longest unit chain x the sample chunks it ran in, split evenly over the tile's rows; the
+ * unit is arbitrary, only ratios matter). Waits for that launch's record copy only. */
+int rt_launch_row_weights(rt_context* ctx, uint32_t back, double* weights, uint32_t band_rows);
 /*
  * Scatter band rows into a full image on the device: dst_row[rows[i]] = src_row[i]
  * (the reorder after the multi-GPU gather). dst has dst_rows rows of `width`
@@ -217,9 +233,13 @@ int rt_multi_device_count(const rt_multi* m, uint32_t* n);
  * and uploaded to every device. */
 int rt_multi_set_scene(rt_multi* m, const Sphere* spheres, uint32_t count);
 /*
- * One frame of the whole image rci->image_size (rci->offset ignored). The rows are cut into
- * 8-row strips, strip k rendered by device k % n (rt_render_device with a rows map, global
- * seeds); every other device's float4 accumulator strips travel to device 0 in one RCCL group
+ * One frame of the whole image rci->image_size (rci->offset ignored). The rows start as
+ * rt_partition_strips' row-exact strips (device d renders its rows through rt_render_device with
+ * a rows map, global seeds) and are re-dealt between frames: each frame reads every device's
+ * trace-kernel time of the frame two before (rt_launch_ms), rescales per-row cost estimates to
+ * them and moves band-end rows from the slowest device to the fastest (rt_partition_rebalance's
+ * rule; the move rewrites rows maps only, waiting for queued frames once); every other device's
+ * float4 accumulator rows travel to device 0 in one RCCL group
  * (ncclSend / ncclRecv; device 0's own strips never go through RCCL) and are reordered into
  * accum_rgba32f, then device 0 tonemaps the whole accumulator into out_rgba8 (rt_resolve_rgba8:
  * the rgba8 bytes are a function of the float sum, so they are not sent). accum_rgba32f /
@@ -245,6 +265,33 @@ int rt_multi_kernel_times(rt_multi* m, float* out_ms, uint32_t capacity, uint32_
 /* The same for each of the last `frames` frames (at most 64): out_ms[f * devices + d], oldest frame
  * first; *count = frames x devices that rendered rows (synchronises). */
 int rt_multi_kernel_times_frames(rt_multi* m, uint32_t frames, float* out_ms, uint32_t capacity, uint32_t* count);
+/* The partition the next frame renders with: counts[d] rows on device d (n entries), and with rows
+ * non-NULL (capacity >= image height) the rows, device 0's first, each device's in band order. */
+int rt_multi_partition(const rt_multi* m, uint32_t* rows, uint32_t* counts, uint32_t capacity);
+
+/* ---- row partition across devices (host only, no device needed) --------------------- */
+/* A partition of `height` rows over n devices is rows[] (height entries: device 0's rows, then
+ * device 1's, ...; each device's in band order) + counts[] (n entries).
+ * rt_partition_strips: the row-exact interleaved strips every multi-device frame starts from: the
+ * rows of the R = floor(height / (8 n)) full rounds are 8-row strips dealt round robin (strip k on
+ * device k % n), the rest are n contiguous runs (the first (rest % n) one row longer), run d on
+ * device d; every device holds floor(height / n) or ceil(height / n) rows (the reference gives the
+ * remainder to the first band, src/ray_trace.cpp:74-81). */
+int rt_partition_strips(uint32_t n_devices, uint32_t height, uint32_t* rows, uint32_t* counts);
+/* One balancing step (src/workload_tuner.hpp:38-104, without its random moves and without the
+ * teardown, src/ray_trace.cpp:774): with a measurement (meas_rows / meas_counts: the partition a
+ * frame ran with, meas_ms: each device's trace-kernel ms of that frame; all three NULL for none),
+ * row_cost (height doubles, ms per row; <= 0: unknown, in / out) is rescaled so that each measured
+ * device's rows sum to its time (unknown rows at the mean of its known ones). Then rows / counts
+ * (the current partition, in / out) are re-dealt: while the most loaded device is above
+ * (1 + tolerance) x the mean load, one of its last min(8, rows) band rows moves to the end of the
+ * least loaded device's band, the row that leaves the pair most even, as long as that lowers the
+ * pair's larger load. Deterministic: every rank of a one-process-per-GPU job that calls it with
+ * the same inputs gets the same partition. *moved = rows moved; *predicted_imbalance = max / mean
+ * load afterwards (either may be NULL). */
+int rt_partition_rebalance(uint32_t n_devices, uint32_t height, uint32_t* rows, uint32_t* counts, double* row_cost,
+                           const uint32_t* meas_rows, const uint32_t* meas_counts, const float* meas_ms,
+                           double tolerance, uint32_t* moved, double* predicted_imbalance);
 
 /* ---- host-pointer convenience ------------------------------------------------------ */
 /*
@@ -266,7 +313,7 @@ int rt_store_ppm(const char* path, const uint8_t* rgba8, uint32_t width, uint32_
 const char* rt_build_info(void);
 
 /* src/ray_trace.h:9-15 — identical symbol and parameter list. Renders the canonical scene once
- * (t = 0) on min(gpu_count, visible) GPUs through rt_multi (8-row strips, RCCL gather, global
+ * (t = 0) on min(gpu_count, visible) GPUs through rt_multi (row-exact strips, RCCL gather, global
  * seeds, so the image does not depend on gpu_count), prints the frame time, stores `render.ppm`
  * when storeRenderResult, and returns. Random stream: the reference's per-pixel LCG stream, or
  * RT_RNG_SAMPLE_HASH when the environment holds RT_RNG=hash (the signature has no parameter for

@@ -96,6 +96,27 @@ int rt_debug_scene(rt_context* ctx, uint32_t what, void* out, uint64_t capacity,
 int rt_debug_multi_plan(uint32_t n_devices, uint32_t width, uint32_t height, const uint32_t* band_starts,
                         uint32_t n_bands, uint32_t accumulate, uint32_t* out, uint64_t capacity,
                         uint64_t* count);
+/* The same plan for an explicit partition (rows / counts as rt_partition_strips writes them: every
+ * row of [0, height) exactly once), e.g. one the balancer re-dealt. */
+int rt_debug_multi_plan_rows(uint32_t n_devices, uint32_t width, uint32_t height, const uint32_t* rows,
+                             const uint32_t* counts, uint32_t accumulate, uint32_t* out, uint64_t capacity,
+                             uint64_t* count);
+/* Tests on a one-GPU box: an rt_multi of n_devices LOGICAL devices, all on device 0 (one context
+ * and one stream each), executing the same frame plans as rt_multi_create's, with every RCCL
+ * send / receive pair of a group replaced by one device copy on the receiver's stream, ordered
+ * after the sender's earlier work and before its later work (the group boundaries of the plan).
+ * No communicator (rt_multi_info reports 0 ranks). */
+int rt_debug_multi_create_logical(uint32_t n_devices, rt_multi** out);
+/* The balancer of m's strip frames: "balance" (1 on, 0 off), "tolerance" (re-deal above
+ * (1 + tolerance) x the mean device time; default 0.0005), "lag" (frames between the measured frame
+ * and the one it re-deals; default 2); -1 restores the default. */
+int rt_debug_multi_tune(rt_multi* m, const char* key, double value);
+/* Feeds n device times (ms) as if measured on the current partition: the next rt_multi_render
+ * re-deals from them instead of its own measurement (tests: forced re-deals). */
+int rt_debug_multi_feedback(rt_multi* m, const float* device_ms, uint32_t n);
+/* {strip frames rendered since the partition was set up, re-deals, rows moved, predicted max / mean
+ * device time after the last re-deal}. */
+int rt_debug_multi_balance_info(const rt_multi* m, double* out4);
 
 #ifdef __cplusplus
 }  /* extern "C" */

@@ -163,6 +163,20 @@ struct rt_context {
     static constexpr uint32_t kKernelEvents = 64;
     hipEvent_t kev[kKernelEvents][2] = {};
     uint64_t kev_count = 0;                      // launches recorded so far
+    // Host copies of the last launches' tile-cost records (and the LPT order they ran in), copied
+    // after the kernel on the launch stream: the cross-device balancer reads a launch's per-row
+    // work from them two frames later without a wait on queued work (rt_launch_row_weights).
+    struct CostSnap {
+        uint32_t* host = nullptr;                // pinned: cost[n], then order[n] when has_order
+        uint32_t cap = 0;                        // tiles it holds
+        hipEvent_t ev = nullptr;                 // after the copies
+        bool pending = false;
+        uint64_t launch = ~0ull;                 // launch index the record belongs to
+        uint32_t n = 0, tiles_x = 0, band_h = 0, head_tiles = 0, head_chunks = 1, chunks = 1;
+        bool has_order = false;
+    };
+    static constexpr uint32_t kSnaps = 4;
+    CostSnap snap[kSnaps];
 };
 
 namespace {
@@ -544,6 +558,10 @@ int rt_context_destroy(rt_context* ctx) {
     for (auto& pr : ctx->kev)
         for (hipEvent_t e : pr)
             if (e) (void)hipEventDestroy(e);
+    for (auto& sn : ctx->snap) {
+        if (sn.host) (void)hipHostFree(sn.host);
+        if (sn.ev) (void)hipEventDestroy(sn.ev);
+    }
     if (ctx->d_spheres) (void)hipFree(ctx->d_spheres);
     if (ctx->fixed) (void)hipFree(ctx->fixed);
     if (ctx->counters) (void)hipFree(ctx->counters);
@@ -1322,6 +1340,33 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     ctx->kev_count++;
     if (mode == rt::MODE_HASH)
         RT_HIP(rt::launch_resolve_fixed(ctx->fixed, texels, P.accumulate, spp, accum, out, st));
+    if (P.tile_cost) {   // this launch's record (+ the order it ran in) for rt_launch_row_weights
+        rt_context::CostSnap& sn = ctx->snap[(ctx->kev_count - 1) % rt_context::kSnaps];
+        if (sn.pending) RT_HIP(hipEventSynchronize(sn.ev));   // four launches old
+        sn.pending = false;
+        sn.launch = ~0ull;
+        if (sn.cap < n_tiles) {
+            if (sn.host) RT_HIP(hipHostFree(sn.host));
+            sn.host = nullptr;
+            sn.cap = 0;
+            RT_HIP(hipHostMalloc(reinterpret_cast<void**>(&sn.host), size_t(n_tiles) * 8, hipHostMallocDefault));
+            sn.cap = uint32_t(n_tiles);
+        }
+        if (!sn.ev) RT_HIP(hipEventCreateWithFlags(&sn.ev, hipEventDisableTiming));
+        RT_HIP(hipMemcpyAsync(sn.host, P.tile_cost, size_t(n_tiles) * 4, hipMemcpyDeviceToHost, st));
+        if (P.tile_order)
+            RT_HIP(hipMemcpyAsync(sn.host + n_tiles, P.tile_order, size_t(n_tiles) * 4, hipMemcpyDeviceToHost, st));
+        RT_HIP(hipEventRecord(sn.ev, st));
+        sn.pending = true;
+        sn.launch = ctx->kev_count - 1;
+        sn.n = uint32_t(n_tiles);
+        sn.tiles_x = uint32_t(tiles_x);
+        sn.band_h = band_height;
+        sn.head_tiles = P.head_tiles;
+        sn.head_chunks = P.head_chunks;
+        sn.chunks = P.chunks;
+        sn.has_order = P.tile_order != nullptr;
+    }
     if (P.tile_cost) {
         ctx->sched.cur ^= 1;
         ctx->sched.valid = true;
@@ -1352,7 +1397,8 @@ int rt_resolve_rgba8(rt_context* ctx, const float* accum, uint64_t n_texels, uin
     if (!ctx) return fail(RT_ERR_INVALID_ARGUMENT, "ctx is NULL");
     if (n_texels == 0) return RT_OK;
     if (!accum || !out) return fail(RT_ERR_INVALID_ARGUMENT, "accum or out is NULL");
-    if (spp == 0) return fail(RT_ERR_INVALID_ARGUMENT, "spp is zero");
+    // spp 0 is accepted: the same expression as the trace kernel's store of a 0-sample frame, so
+    // a multi-device frame resolves to the bytes a one-device render stores
     DeviceGuard g(ctx->device);
     RT_HIP(rt::launch_tonemap(accum, n_texels, spp, out, static_cast<hipStream_t>(stream)));
     return RT_OK;
@@ -1488,6 +1534,75 @@ int rt_debug_kernel_times(rt_context* ctx, float* out_ms, uint32_t capacity, uin
     *count = n;
     return RT_OK;
 }
+
+// Trace-kernel duration of ctx's launch `back` launches before its most recent one: waits for
+// that launch's end event only, so a caller reading a launch two frames old does not drain the
+// frames queued behind it (the cross-device balancer of rt_multi / rtvk.dist).
+int rt_launch_row_weights(rt_context* ctx, uint32_t back, double* weights, uint32_t band_rows) {
+    if (!ctx || (!weights && band_rows)) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (back >= ctx->kev_count) return fail(RT_ERR_INVALID_ARGUMENT, "no such launch recorded");
+    std::vector<double> w;
+    if (int rc = rt::launch_row_weights(ctx, ctx->kev_count - 1 - back, w)) return rc;
+    if (w.size() != band_rows) return fail(RT_ERR_INVALID_ARGUMENT, "band_rows differs from the launch's band");
+    std::copy(w.begin(), w.end(), weights);
+    return RT_OK;
+}
+
+int rt_launch_ms(rt_context* ctx, uint32_t back, float* ms) {
+    if (!ctx || !ms) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (back >= ctx->kev_count || back >= rt_context::kKernelEvents)
+        return fail(RT_ERR_INVALID_ARGUMENT, "no such launch recorded");
+    return rt::launch_ms_at(ctx, ctx->kev_count - 1 - back, ms);
+}
+
+}  // extern "C"
+
+namespace rt {
+uint64_t launch_count(const rt_context* ctx) { return ctx ? ctx->kev_count : 0; }
+int launch_row_weights(rt_context* ctx, uint64_t index, std::vector<double>& w) {
+    w.clear();
+    if (!ctx) return fail(RT_ERR_INVALID_ARGUMENT, "ctx is NULL");
+    for (rt_context::CostSnap& sn : ctx->snap) {
+        if (sn.launch != index || !sn.pending) continue;
+        DeviceGuard g(ctx->device);
+        RT_HIP(hipEventSynchronize(sn.ev));
+        // a tile's record is its longest unit chain; x the chunk count of the rank it ran at (the
+        // LPT head / tail split) it estimates its longest pixel's chain, the key the LPT order uses
+        std::vector<uint32_t> rank;
+        if (sn.has_order && sn.head_tiles) {
+            rank.assign(sn.n, 0u);
+            for (uint32_t r = 0; r < sn.n; r++)
+                if (sn.host[sn.n + r] < sn.n) rank[sn.host[sn.n + r]] = r;
+        }
+        const uint32_t tiles_y = sn.tiles_x ? sn.n / sn.tiles_x : 0;
+        std::vector<double> tile_row(tiles_y, 0.0);
+        for (uint32_t t = 0; t < sn.n && sn.tiles_x; t++) {
+            const double mult = rank.empty() ? 1.0 : double(rank[t] < sn.head_tiles ? sn.head_chunks : sn.chunks);
+            if (t / sn.tiles_x < tiles_y) tile_row[t / sn.tiles_x] += double(sn.host[t]) * mult;
+        }
+        w.assign(sn.band_h, 0.0);
+        for (uint32_t i = 0; i < sn.band_h; i++) {
+            const uint32_t ty = i / 8u;
+            const uint32_t rows_in = std::min<uint32_t>(8u, sn.band_h - ty * 8u);
+            if (ty < tiles_y) w[i] = tile_row[ty] / double(rows_in);
+        }
+        return RT_OK;
+    }
+    return fail(RT_ERR_INVALID_ARGUMENT, "no tile-cost record kept for that launch");
+}
+int launch_ms_at(rt_context* ctx, uint64_t index, float* ms) {
+    if (!ctx || !ms) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (index >= ctx->kev_count || ctx->kev_count - index > rt_context::kKernelEvents)
+        return fail(RT_ERR_INVALID_ARGUMENT, "launch not recorded");
+    DeviceGuard g(ctx->device);
+    hipEvent_t* e = ctx->kev[index % rt_context::kKernelEvents];
+    RT_HIP(hipEventSynchronize(e[1]));
+    RT_HIP(hipEventElapsedTime(ms, e[0], e[1]));
+    return RT_OK;
+}
+}  // namespace rt
+
+extern "C" {
 
 #ifndef RT_BUILD_ARCH
 #define RT_BUILD_ARCH "unknown"

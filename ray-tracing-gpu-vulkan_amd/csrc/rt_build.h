@@ -88,7 +88,9 @@ struct TileSchedule {
     // estimate, comparable between head and tail tiles)
     uint32_t rec_head_tiles[2] = {0, 0}, rec_head_chunks[2] = {1, 1}, rec_chunks[2] = {1, 1};
 };
-// (Re)allocates for n tiles when the geometry changes (tables zeroed, valid = false).
+// (Re)allocates for n tiles when the geometry changes. A valid record of the last launch is carried
+// over (tiles below both counts keep their chunk-normalised cost, new tiles cost 0), so a band that
+// gains or loses rows at its end keeps its LPT order; without one the tables are zeroed.
 hipError_t schedule_reserve(TileSchedule& s, uint32_t n, hipStream_t st);
 void schedule_release(TileSchedule& s);
 // order = tiles by descending cost of the last launch (stable: ties in tile order).

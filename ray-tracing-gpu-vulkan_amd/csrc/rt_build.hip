@@ -679,9 +679,30 @@ void schedule_release(TileSchedule& s) {
     s = TileSchedule{};
 }
 
+// The last launch's record carried over to a new tile count (a band that gained or lost rows at its
+// end, rt_multi's balancer): tile t < min(old, new) keeps its cost x the chunk count its rank ran
+// with (the normalisation k_cost_norm would apply), tiles beyond the old count start at 0 (they
+// are handed out last). The carried record is then marked as one chunk count (rec_* = 1).
+__global__ void k_cost_resize(const uint32_t* __restrict__ old_cost, const uint32_t* __restrict__ old_order,
+                              uint32_t n_old, uint32_t head_tiles, uint32_t head_chunks, uint32_t chunks,
+                              uint32_t* __restrict__ new_cost, uint32_t n_new) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n_old) {
+        const uint32_t t = head_tiles ? old_order[i] : i;
+        if (t < n_new) {
+            const uint64_t v = uint64_t(old_cost[t]) * (head_tiles ? (i < head_tiles ? head_chunks : chunks) : 1u);
+            new_cost[t] = v > 0xffffffffull ? 0xffffffffu : uint32_t(v);
+        }
+    } else if (i < n_new) {
+        new_cost[i] = 0u;
+    }
+}
+
 hipError_t schedule_reserve(TileSchedule& s, uint32_t n, hipStream_t st) {
     if (s.n == n && s.cost[0]) return hipSuccess;
-    schedule_release(s);
+    TileSchedule old = s;   // released after its record is carried over
+    const bool carry = old.valid && old.cost[0] && old.n && n;
+    s = TileSchedule{};
     hipError_t e = hipSuccess;
     if (e == hipSuccess) e = alloc(&s.cost[0], n);
     if (e == hipSuccess) e = alloc(&s.cost[1], n);
@@ -699,6 +720,20 @@ hipError_t schedule_reserve(TileSchedule& s, uint32_t n, hipStream_t st) {
         k_iota<<<blocks(n), kBlock, 0, st>>>(s.iota, n);
         e = hipGetLastError();
     }
+    if (e == hipSuccess && carry) {   // the last launch's costs keep ordering the band's tiles
+        const int last = old.cur ^ 1;
+        k_cost_resize<<<blocks(std::max(old.n, n)), kBlock, 0, st>>>(
+            old.cost[last], old.order, old.n, old.rec_head_tiles[last], old.rec_head_chunks[last],
+            old.rec_chunks[last], s.cost[last], n);
+        e = hipGetLastError();
+        if (e == hipSuccess) {
+            s.cur = old.cur;
+            s.valid = true;
+            s.rec_head_tiles[last] = 0;
+            s.rec_head_chunks[last] = s.rec_chunks[last] = 1;
+        }
+    }
+    schedule_release(old);
     if (e != hipSuccess) {
         schedule_release(s);
         return e;

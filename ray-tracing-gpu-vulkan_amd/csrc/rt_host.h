@@ -6,6 +6,7 @@
 
 #include <memory>
 #include <string>
+#include <vector>
 
 #include "../../include/rt_mi355x.h"
 
@@ -23,6 +24,14 @@ using HostPackagePtr = std::unique_ptr<HostPackage, HostPackageDeleter>;
 // grid. Every begin that succeeds must be followed by end on the same context.
 int set_scene_begin(rt_context* ctx, const Sphere* spheres, uint32_t count, void* stream, HostPackagePtr* shared);
 int set_scene_end(rt_context* ctx);
+
+// Trace launches recorded on ctx so far, and the trace-kernel duration of launch `index` (0 = the
+// context's first; only the last 64 are kept), waiting for that launch's end event only.
+uint64_t launch_count(const rt_context* ctx);
+int launch_ms_at(rt_context* ctx, uint64_t index, float* ms);
+// Per band row of launch `index` (one of the last 4), its share of the launch's work as the
+// tile-cost record estimates it (rt_launch_row_weights); waits for that launch's copy only.
+int launch_row_weights(rt_context* ctx, uint64_t index, std::vector<double>& w);
 
 // Message of the calling thread's last failure (rt_last_error()).
 extern thread_local std::string g_last_error;

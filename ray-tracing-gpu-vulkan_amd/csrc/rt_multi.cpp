@@ -2,29 +2,41 @@
 // the host-buffer frame rt_render(), and the reference's entry point ray_trace().
 //
 // The reference creates one Vulkan device per GPU (src/ray_trace.cpp:42-105), gives each a
-// contiguous row band (:74-93, tuned by src/workload_tuner.hpp) and never moves pixels between
-// GPUs (each device presents its own window). Here the image is tiled into 8-row strips dealt
-// round robin over the devices (interleaving balances sky-heavy and sphere-heavy rows without a
-// tuner), each device renders its strips through a rows map (global pixel seeds, so the image
-// does not depend on the device count), one RCCL group moves every other device's float4
-// accumulator strips to device 0 over xGMI (ncclSend / ncclRecv; device 0's own strips are not
-// sent), one kernel per source puts them in place (rt_scatter_rows) and device 0 tonemaps the
-// whole accumulator to rgba8 once (rt_resolve_rgba8: the rgba8 bytes are a function of the float
-// sum, shader.rgen:65-66, so they need not travel). A single device holding every row renders
-// straight into the caller's buffers. SURVEY.md §8(e).
+// contiguous row band (:74-93) and moves rows between GPUs from their measured frame times
+// (src/workload_tuner.hpp:38-104, hooked at src/ray_trace.cpp:750-775), tearing down and
+// rebuilding every Vulkan object on each move (:774, :778-916); it never moves pixels between
+// GPUs (each device presents its own window). Here the image starts as row-exact interleaved
+// 8-row strips (rt_plan.h strip_parts: every device within one row of H / N), each device renders
+// its rows through a rows map (global pixel seeds, so the image does not depend on the partition),
+// one RCCL group moves every other device's float4 accumulator rows to device 0 over xGMI
+// (ncclSend / ncclRecv; device 0's own rows are not sent), one kernel per source puts them in
+// place (rt_scatter_rows) and device 0 tonemaps the whole accumulator to rgba8 once
+// (rt_resolve_rgba8: the rgba8 bytes are a function of the float sum, shader.rgen:65-66, so they
+// need not travel). A single device holding every row renders straight into the caller's buffers.
+// SURVEY.md §8(e).
 //
-// A frame is a FramePlan: the partition (device + global rows per part) and the ordered list of
-// steps (row loads / stores on device 0, grouped sends / receives, renders, the resolve) that
-// rt_multi_render executes. The plan is host-only data, so the CPU tests check it for every device
-// count and height without a GPU (rt_debug_multi_plan, tests/test_multi_plan.py).
+// Balancing: every frame reads each device's trace-kernel time of the frame
+// two before it (its end event has long passed: no host wait on queued work), rescales per-row
+// cost estimates to those times and moves band-end rows from the slowest device to the fastest
+// (rt_plan.h rebalance). A move rewrites rows maps only: the contexts, scenes, buffers (grown when
+// needed) and each band's LPT tile costs stay (rows leave and join at a band's end, so its other
+// tiles keep their index).
+//
+// A frame is a FramePlan (rt_plan.h): the partition and the ordered steps rt_multi_render executes.
+// The plan is host-only data, so the CPU tests check it for every device count and height without
+// a GPU (rt_debug_multi_plan*, tests/test_multi_plan.py). rt_debug_multi_create_logical runs the
+// same executor over N logical devices on GPU 0, with each send / receive pair a device copy
+// ordered by the same group boundaries, so the one-GPU pool executes every step of the N > 1 plan.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <exception>
 #include <memory>
 #include <string>
@@ -36,9 +48,11 @@
 #include "../../include/rt_mi355x_debug.h"
 #include "rt_host.h"
 #include "rt_internal.h"
+#include "rt_plan.h"
 
 using rt::DeviceGuard;
 using rt::fail;
+using namespace rt::plan;
 
 #define RT_NCCL(call)                                                                       \
     do {                                                                                    \
@@ -49,125 +63,13 @@ using rt::fail;
 
 namespace {
 
-constexpr uint32_t kStrip = 8;   // rows per strip: one 8x8 pixel tile high, the kernel's wave tile
-
-// ---- the frame plan ----------------------------------------------------------------------
-// Buffers a step names: the caller's accumulator / rgba8 image on device 0 (W x H), each part's
-// band on its device (rows x W), and each remote part's stage on device 0 (rows x W float4).
-enum PlanOp : uint32_t {
-    OP_LOAD_ROWS = 1,   // device 0: the part's rows of the caller's accumulator -> its band (a part
-                        // of device 0) or its stage (accumulating frames: the running sums)
-    OP_GROUP_START = 2, // ncclGroupStart
-    OP_SEND = 3,        // dev -> peer: `count` floats of the part's band (dev != 0) or stage (dev 0)
-    OP_RECV = 4,        // dev <- peer: `count` floats into the part's band (dev != 0) or stage (dev 0)
-    OP_GROUP_END = 5,   // ncclGroupEnd
-    OP_RENDER = 6,      // dev renders the part; flags bit 0: straight into the caller's buffers
-    OP_STORE_ROWS = 7,  // device 0: the part's band (device 0) or stage -> its rows of the accumulator
-    OP_RESOLVE = 8,     // device 0: rgba8 of the whole accumulator (`count` texels)
-};
-constexpr uint32_t kDirect = 1u;
-
-struct PlanPart {
-    uint32_t dev = 0;
-    std::vector<uint32_t> rows;   // global rows, band order
-    bool whole = false;           // device 0, every row in order: renders into the caller's buffers
-};
-struct PlanStep {
-    uint32_t op, dev, peer, part, flags;
-    uint64_t count;
-};
-struct FramePlan {
-    std::vector<PlanPart> parts;
-    std::vector<PlanStep> steps;
-};
-using Parts = std::vector<std::pair<uint32_t, std::vector<uint32_t>>>;
-
-// Strips k = 0, 1, ... of kStrip rows, strip k on device k % n (rtvk.dist.strip_rows).
-Parts strip_parts(uint32_t n, uint32_t H) {
-    Parts parts(n);
-    for (uint32_t d = 0; d < n; d++) parts[d].first = d;
-    for (uint32_t y = 0; y < H; y++) parts[(y / kStrip) % n].second.push_back(y);
-    return parts;
-}
-
-// The reference's contiguous bands (src/ray_trace.cpp:74-93): band i = rows [start[i], start[i+1])
-// (the last to H), on device i % n. Empty when the starts do not tile [0, H) top to bottom.
-Parts band_parts(uint32_t n, uint32_t H, const uint32_t* start, uint32_t n_bands) {
-    Parts parts(n_bands);
-    for (uint32_t i = 0; i < n_bands; i++) {
-        const uint32_t y0 = start[i], y1 = i + 1 < n_bands ? start[i + 1] : H;
-        if (y1 < y0 || y1 > H || (i == 0 && y0 != 0)) return Parts{};
-        parts[i].first = i % n;
-        for (uint32_t y = y0; y < y1; y++) parts[i].second.push_back(y);
-    }
-    return parts;
-}
-
-// The steps of one frame over `parts` (W x H). accumulate: every part starts from its rows of the
-// caller's accumulator (rt_render_device's accumulate semantics for the whole image, at any
-// device count): device 0 loads them into its own bands and into the stages of the other
-// devices' parts, and sends those in one group. Then every part renders; one group brings the
-// other devices' accumulator bands to device 0's stages; device 0 stores every band in place and
-// tonemaps the whole image. A part of device 0 never goes through RCCL; a `whole` part renders
-// into the caller's buffers and needs nothing else (the one-device frame).
-FramePlan make_plan(uint32_t W, uint32_t H, Parts&& parts, bool accumulate) {
-    FramePlan p;
-    for (auto& pr : parts) {
-        PlanPart q;
-        q.dev = pr.first;
-        q.rows = std::move(pr.second);
-        q.whole = q.dev == 0 && q.rows.size() == H;
-        for (uint32_t y = 0; q.whole && y < H; y++) q.whole = q.rows[y] == y;
-        p.parts.push_back(std::move(q));
-    }
-    const uint32_t np = uint32_t(p.parts.size());
-    auto live = [&](uint32_t i) { return !p.parts[i].rows.empty(); };
-    auto floats = [&](uint32_t i) { return uint64_t(p.parts[i].rows.size()) * W * 4u; };
-    auto add = [&](uint32_t op, uint32_t dev, uint32_t peer, uint32_t part, uint32_t flags, uint64_t count) {
-        p.steps.push_back(PlanStep{op, dev, peer, part, flags, count});
-    };
-    bool whole = false, remote = false;
-    for (uint32_t i = 0; i < np; i++) {
-        whole |= live(i) && p.parts[i].whole;
-        remote |= live(i) && p.parts[i].dev != 0;
-    }
-    if (accumulate && !whole) {
-        for (uint32_t i = 0; i < np; i++)
-            if (live(i)) add(OP_LOAD_ROWS, 0, 0, i, 0, floats(i));
-        if (remote) {
-            add(OP_GROUP_START, 0, 0, 0, 0, 0);
-            for (uint32_t i = 0; i < np; i++) {
-                if (!live(i) || p.parts[i].dev == 0) continue;
-                add(OP_SEND, 0, p.parts[i].dev, i, 0, floats(i));
-                add(OP_RECV, p.parts[i].dev, 0, i, 0, floats(i));
-            }
-            add(OP_GROUP_END, 0, 0, 0, 0, 0);
-        }
-    }
-    for (uint32_t i = 0; i < np; i++)
-        if (live(i)) add(OP_RENDER, p.parts[i].dev, p.parts[i].dev, i, p.parts[i].whole ? kDirect : 0u, 0);
-    if (whole) return p;
-    if (remote) {
-        add(OP_GROUP_START, 0, 0, 0, 0, 0);
-        for (uint32_t i = 0; i < np; i++) {
-            if (!live(i) || p.parts[i].dev == 0) continue;
-            add(OP_SEND, p.parts[i].dev, 0, i, 0, floats(i));
-            add(OP_RECV, 0, p.parts[i].dev, i, 0, floats(i));
-        }
-        add(OP_GROUP_END, 0, 0, 0, 0, 0);
-    }
-    for (uint32_t i = 0; i < np; i++)
-        if (live(i)) add(OP_STORE_ROWS, 0, 0, i, 0, floats(i));
-    add(OP_RESOLVE, 0, 0, 0, 0, uint64_t(W) * H);
-    return p;
-}
-
 // One part of a multi-device frame on its device (its own context), with its buffers.
 struct Launch {
-    uint32_t dev = 0;
+    uint32_t dev = 0;                    // logical device
     std::vector<uint32_t> rows;          // global rows, band order
     bool whole = false;
     rt_context* ctx = nullptr;           // on dev
+    uint32_t cap = 0;                    // rows the buffers below hold
     uint32_t* rows_dev = nullptr;        // rows on dev (the kernel's map)
     uint32_t* rows_root = nullptr;       // rows on device 0 (the row loads / stores)
     float* acc = nullptr;                // band on dev: rows x W float4 (not for a whole part)
@@ -175,13 +77,23 @@ struct Launch {
     float* stage_acc = nullptr;          // dev != 0: the band's copy on device 0
 };
 
+// A rendered strip frame, for the balancer: its partition and each part's launch index on its
+// context (UINT64_MAX: the part rendered nothing).
+struct FrameRecord {
+    Parts parts;
+    std::vector<uint64_t> launch;
+};
+
 }  // namespace
 
 struct rt_multi {
     uint32_t n = 0;
-    std::vector<hipStream_t> stream;     // one per device
+    std::vector<int> phys;               // HIP device of each logical device
+    bool logical = false;                // N logical devices on GPU 0: no communicator, device copies
+    std::vector<hipStream_t> stream;     // one per logical device
     std::vector<ncclComm_t> comm;        // one per device, rank = device index
     hipEvent_t ev_in = nullptr, ev_out = nullptr;   // device 0: caller stream <-> stream[0]
+    std::vector<hipEvent_t> xev;         // logical transport: two per transfer of a group
     std::vector<Sphere> spheres;         // the scene, for contexts created later
     bool scene_set = false;
     // cached partition (geometry + kind): strips of W x H, or explicit bands
@@ -189,28 +101,52 @@ struct rt_multi {
     std::string key;
     std::vector<Launch> launches;        // one per plan part, same index
     FramePlan plan[2];                   // steps without / with accumulation
+    struct Balancer {
+        bool enabled = true;
+        double tolerance = 0.0005;       // re-deal when the slowest device is above (1 + tol) x mean
+        uint32_t lag = 2;                // frames between a measured frame and the frame it re-deals
+        std::vector<double> cost;        // per global row, ms
+        std::deque<FrameRecord> history; // strip frames rendered since the partition was set up
+        std::vector<float> injected;     // rt_debug_multi_feedback: times of the current partition
+        uint64_t frames = 0, rebalances = 0, moved = 0;
+        double predicted = 1.0;          // predicted max / mean after the last re-deal
+    } bal;
 };
 
 namespace {
 
+int phys_of(const rt_multi* m, uint32_t dev) { return m->phys[dev]; }
+
+void free_buffers(rt_multi* m, Launch& l) {
+    {
+        DeviceGuard g(phys_of(m, l.dev));
+        (void)hipDeviceSynchronize();
+        if (l.rows_dev) (void)hipFree(l.rows_dev);
+        if (l.acc) (void)hipFree(l.acc);
+        if (l.out) (void)hipFree(l.out);
+    }
+    DeviceGuard g0(phys_of(m, 0));
+    (void)hipDeviceSynchronize();
+    if (l.rows_root) (void)hipFree(l.rows_root);
+    if (l.stage_acc) (void)hipFree(l.stage_acc);
+    l.rows_dev = l.rows_root = nullptr;
+    l.acc = l.stage_acc = nullptr;
+    l.out = nullptr;
+    l.cap = 0;
+}
+
 void free_launches(rt_multi* m) {
     for (Launch& l : m->launches) {
-        {
-            DeviceGuard g(static_cast<int>(l.dev));
-            (void)hipDeviceSynchronize();
-            if (l.rows_dev) (void)hipFree(l.rows_dev);
-            if (l.acc) (void)hipFree(l.acc);
-            if (l.out) (void)hipFree(l.out);
-            rt_context_destroy(l.ctx);
-        }
-        DeviceGuard g0(0);
-        (void)hipDeviceSynchronize();
-        if (l.rows_root) (void)hipFree(l.rows_root);
-        if (l.stage_acc) (void)hipFree(l.stage_acc);
+        free_buffers(m, l);
+        DeviceGuard g(phys_of(m, l.dev));
+        rt_context_destroy(l.ctx);
     }
     m->launches.clear();
     m->plan[0] = m->plan[1] = FramePlan{};
     m->key.clear();
+    m->bal.history.clear();
+    m->bal.cost.clear();
+    m->bal.injected.clear();
 }
 
 // The scene on every device: each device's build is issued before any is waited for (device-built
@@ -233,8 +169,39 @@ int set_scene_all(rt_multi* m) {
     return rc;
 }
 
+// The part's buffers for its rows (grown, never shrunk; a move of a few rows reuses them), and its
+// rows maps on its device and on device 0. Callers have drained the streams that read them.
+int fit_buffers(rt_multi* m, Launch& l) {
+    const uint32_t nr = uint32_t(l.rows.size()), W = m->W;
+    if (!nr || l.whole) return RT_OK;
+    if (l.cap < nr) {
+        free_buffers(m, l);
+        // room for the rows a balancer moves in (a few percent of a band) without reallocating
+        const uint32_t cap = std::min<uint32_t>(m->H, nr + std::max<uint32_t>(kStrip, nr / 16));
+        const size_t texels = size_t(cap) * W;
+        {
+            DeviceGuard g(phys_of(m, l.dev));
+            RT_HIP(hipMalloc(&l.rows_dev, size_t(cap) * 4));
+            RT_HIP(hipMalloc(&l.acc, texels * 16));
+            RT_HIP(hipMalloc(&l.out, texels * 4));
+        }
+        DeviceGuard g0(phys_of(m, 0));
+        RT_HIP(hipMalloc(&l.rows_root, size_t(cap) * 4));
+        if (l.dev != 0) RT_HIP(hipMalloc(&l.stage_acc, texels * 16));
+        l.cap = cap;
+    }
+    {
+        DeviceGuard g(phys_of(m, l.dev));
+        RT_HIP(hipMemcpy(l.rows_dev, l.rows.data(), size_t(nr) * 4, hipMemcpyHostToDevice));
+    }
+    DeviceGuard g0(phys_of(m, 0));
+    RT_HIP(hipMemcpy(l.rows_root, l.rows.data(), size_t(nr) * 4, hipMemcpyHostToDevice));
+    return RT_OK;
+}
+
 // (Re)builds the launches for `key` from the partition: one per part (device + global rows), its
-// context and buffers, and the frame's plans with and without accumulation.
+// context and buffers, and the frame's plans with and without accumulation. Same key and size:
+// nothing to do.
 int set_partition(rt_multi* m, const std::string& key, uint32_t W, uint32_t H, Parts&& parts) {
     if (m->key == key && m->W == W && m->H == H) return RT_OK;
     free_launches(m);
@@ -251,23 +218,130 @@ int set_partition(rt_multi* m, const std::string& key, uint32_t W, uint32_t H, P
         m->launches.push_back(std::move(l));
     }
     for (Launch& l : m->launches) {
-        const size_t nr = l.rows.size(), texels = nr * W;
-        if (int rc = rt_context_create(int(l.dev), &l.ctx)) return rc;
-        if (!nr || l.whole) continue;
-        {
-            DeviceGuard g(static_cast<int>(l.dev));
-            RT_HIP(hipMalloc(&l.rows_dev, nr * 4));
-            RT_HIP(hipMemcpy(l.rows_dev, l.rows.data(), nr * 4, hipMemcpyHostToDevice));
-            RT_HIP(hipMalloc(&l.acc, texels * 16));
-            RT_HIP(hipMalloc(&l.out, texels * 4));
-        }
-        DeviceGuard g0(0);
-        RT_HIP(hipMalloc(&l.rows_root, nr * 4));
-        RT_HIP(hipMemcpy(l.rows_root, l.rows.data(), nr * 4, hipMemcpyHostToDevice));
-        if (l.dev != 0) RT_HIP(hipMalloc(&l.stage_acc, texels * 16));
+        if (int rc = rt_context_create(phys_of(m, l.dev), &l.ctx)) return rc;
+        if (int rc = fit_buffers(m, l)) return rc;
     }
     m->key = key;
     return m->scene_set ? set_scene_all(m) : RT_OK;
+}
+
+// A new partition of the same parts (devices unchanged): rows maps and plans only. Waits for every
+// device's queued work first (the maps are read by queued launches); a re-deal happens a few times
+// while a run's balance settles, not per frame.
+int repartition(rt_multi* m, const Parts& parts) {
+    for (uint32_t d = 0; d < m->n; d++) {
+        DeviceGuard g(phys_of(m, d));
+        RT_HIP(hipStreamSynchronize(m->stream[d]));
+    }
+    Parts copy = parts, copy2 = parts;
+    m->plan[0] = make_plan(m->W, m->H, std::move(copy), false);
+    m->plan[1] = make_plan(m->W, m->H, std::move(copy2), true);
+    for (size_t i = 0; i < m->launches.size(); i++) {
+        Launch& l = m->launches[i];
+        l.rows = m->plan[0].parts[i].rows;
+        l.whole = m->plan[0].parts[i].whole;
+        if (int rc = fit_buffers(m, l)) return rc;
+    }
+    return RT_OK;
+}
+
+Parts current_parts(const rt_multi* m) {
+    Parts p;
+    for (const Launch& l : m->launches) p.emplace_back(l.dev, l.rows);
+    return p;
+}
+
+// The balancer step before a strip frame: feedback from the frame `lag` frames back (or injected
+// times of the current partition), then a re-deal of the current partition.
+int balance_step(rt_multi* m) {
+    auto& b = m->bal;
+    if (!b.enabled || m->n < 2 || m->launches.size() < 2) return RT_OK;
+    if (b.cost.size() != m->H) b.cost.assign(m->H, 0.0);
+    std::vector<float> ms;
+    Parts measured;
+    std::vector<std::vector<double>> weights;
+    if (!b.injected.empty()) {
+        measured = current_parts(m);
+        ms = b.injected;
+        ms.resize(measured.size(), 0.0f);
+        b.injected.clear();
+    } else {
+        if (b.history.size() < std::max<uint32_t>(1, b.lag)) return RT_OK;
+        const FrameRecord& r = b.history[b.history.size() - std::max<uint32_t>(1, b.lag)];
+        measured = r.parts;
+        ms.assign(measured.size(), 0.0f);
+        weights.resize(measured.size());
+        for (size_t i = 0; i < measured.size(); i++) {
+            if (r.launch[i] == UINT64_MAX) continue;
+            if (int rc = rt::launch_ms_at(m->launches[i].ctx, r.launch[i], &ms[i])) return rc;
+            // the launch's per-row work from its tile costs (none kept, e.g. brute force: the
+            // device time alone rescales the rows' estimates)
+            const std::string keep = rt::g_last_error;
+            if (rt::launch_row_weights(m->launches[i].ctx, r.launch[i], weights[i]) != RT_OK) weights[i].clear();
+            rt::g_last_error = keep;
+        }
+    }
+    update_costs(measured, ms.data(), b.cost, weights.empty() ? nullptr : &weights);
+    Parts next = current_parts(m);
+    std::vector<double> loads;
+    const uint32_t moved = rebalance(next, b.cost, b.tolerance, &loads);
+    if (!moved) return RT_OK;
+    b.rebalances++;
+    b.moved += moved;
+    b.predicted = imbalance(next, b.cost);
+    return repartition(m, next);
+}
+
+// A send / receive pair of the logical transport (one GPU): a device copy on the receiver's stream
+// after the sender's earlier work, and the sender's later work after the copy.
+int logical_transfers(rt_multi* m, const std::vector<PlanStep>& group) {
+    size_t ev = 0;
+    for (const PlanStep& r : group) {
+        if (r.op != OP_RECV) continue;
+        const PlanStep* s = nullptr;
+        for (const PlanStep& c : group)
+            if (c.op == OP_SEND && c.dev == r.peer && c.peer == r.dev && c.part == r.part) s = &c;
+        if (!s || s->count != r.count) return fail(RT_ERR_INVALID_ARGUMENT, "unpaired receive in the plan");
+        Launch& l = m->launches[r.part];
+        const float* src = s->dev == 0 ? l.stage_acc : l.acc;
+        float* dst = r.dev == 0 ? l.stage_acc : l.acc;
+        while (m->xev.size() < ev + 2) {
+            hipEvent_t e = nullptr;
+            DeviceGuard g(phys_of(m, 0));
+            RT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            m->xev.push_back(e);
+        }
+        DeviceGuard g(phys_of(m, r.dev));
+        RT_HIP(hipEventRecord(m->xev[ev], m->stream[s->dev]));
+        RT_HIP(hipStreamWaitEvent(m->stream[r.dev], m->xev[ev], 0));
+        RT_HIP(hipMemcpyAsync(dst, src, r.count * 4, hipMemcpyDeviceToDevice, m->stream[r.dev]));
+        RT_HIP(hipEventRecord(m->xev[ev + 1], m->stream[r.dev]));
+        RT_HIP(hipStreamWaitEvent(m->stream[s->dev], m->xev[ev + 1], 0));
+        ev += 2;
+    }
+    return RT_OK;
+}
+
+// The rgba8 resolve of the whole accumulator: one launch when every part shares one spp, else each
+// part's contiguous row runs with its own RenderCallInfo's spp (rt_render's bands).
+int resolve_all(rt_multi* m, rt_context* c0, const RenderCallInfo* rcis, size_t n_rci, float* acc, uint8_t* out) {
+    const uint32_t W = m->W;
+    bool same = true;
+    for (size_t i = 1; i < n_rci; i++) same &= rcis[i].samplesPerRenderCall == rcis[0].samplesPerRenderCall;
+    if (same) return rt_resolve_rgba8(c0, acc, uint64_t(W) * m->H, rcis[0].samplesPerRenderCall, out, m->stream[0]);
+    for (size_t p = 0; p < m->launches.size(); p++) {
+        const std::vector<uint32_t>& rows = m->launches[p].rows;
+        const uint32_t spp = rcis[n_rci == 1 ? 0 : p].samplesPerRenderCall;
+        for (size_t k = 0; k < rows.size();) {
+            size_t e = k + 1;
+            while (e < rows.size() && rows[e] == rows[e - 1] + 1) e++;
+            const size_t off = size_t(rows[k]) * W;
+            if (int rc = rt_resolve_rgba8(c0, acc + off * 4, uint64_t(e - k) * W, spp, out + off * 4, m->stream[0]))
+                return rc;
+            k = e;
+        }
+    }
+    return RT_OK;
 }
 
 // A context on device 0 (the row loads / stores and the resolve run on stream[0]).
@@ -285,6 +359,7 @@ int run_plan(rt_multi* m, const FramePlan& p, const RenderCallInfo* rcis, size_t
     const uint32_t W = m->W, H = m->H;
     rt_context* c0 = root_ctx(m);
     bool in_group = false;
+    std::vector<PlanStep> group;   // logical transport: the group's sends / receives
     auto body = [&]() -> int {
         for (const PlanStep& s : p.steps) {
             Launch& l = m->launches[s.part];
@@ -293,16 +368,25 @@ int run_plan(rt_multi* m, const FramePlan& p, const RenderCallInfo* rcis, size_t
             const uint32_t nr = uint32_t(l.rows.size());
             switch (s.op) {
                 case OP_GROUP_START:
-                    RT_NCCL(ncclGroupStart());
+                    if (!m->logical) RT_NCCL(ncclGroupStart());
+                    group.clear();
                     in_group = true;
                     break;
                 case OP_GROUP_END:
                     in_group = false;
-                    RT_NCCL(ncclGroupEnd());
+                    if (m->logical) {
+                        if (int rc = logical_transfers(m, group)) return rc;
+                    } else {
+                        RT_NCCL(ncclGroupEnd());
+                    }
                     break;
                 case OP_SEND:
                 case OP_RECV: {
-                    DeviceGuard g(static_cast<int>(s.dev));
+                    if (m->logical) {
+                        group.push_back(s);
+                        break;
+                    }
+                    DeviceGuard g(phys_of(m, s.dev));
                     const ncclResult_t e =
                         s.op == OP_SEND
                             ? ncclSend(dev_buf, s.count, ncclFloat32, int(s.peer), m->comm[s.dev], m->stream[s.dev])
@@ -328,8 +412,7 @@ int run_plan(rt_multi* m, const FramePlan& p, const RenderCallInfo* rcis, size_t
                     break;
                 }
                 case OP_RESOLVE:
-                    if (int rc = rt_resolve_rgba8(c0, acc, s.count, rcis[0].samplesPerRenderCall, out, m->stream[0]))
-                        return rc;
+                    if (int rc = resolve_all(m, c0, rcis, n_rci, acc, out)) return rc;
                     break;
                 default:
                     return fail(RT_ERR_INVALID_ARGUMENT, "bad plan step");
@@ -338,32 +421,19 @@ int run_plan(rt_multi* m, const FramePlan& p, const RenderCallInfo* rcis, size_t
         return RT_OK;
     };
     const int rc = body();
-    if (in_group) (void)ncclGroupEnd();   // a failure inside a group still closes it
+    if (in_group && !m->logical) (void)ncclGroupEnd();   // a failure inside a group still closes it
     return rc;
 }
 
-// Flat form of a plan (rt_debug_multi_plan): {n_parts, n_steps}, then per part {dev, whole,
-// n_rows, rows...}, then per step {op, dev, peer, part, flags, count low, count high}.
-std::vector<uint32_t> serialize(const FramePlan& p) {
-    std::vector<uint32_t> v{uint32_t(p.parts.size()), uint32_t(p.steps.size())};
-    for (const PlanPart& q : p.parts) {
-        v.push_back(q.dev);
-        v.push_back(q.whole ? 1u : 0u);
-        v.push_back(uint32_t(q.rows.size()));
-        v.insert(v.end(), q.rows.begin(), q.rows.end());
-    }
-    for (const PlanStep& s : p.steps) {
-        const uint32_t w[7] = {s.op, s.dev, s.peer, s.part, s.flags, uint32_t(s.count), uint32_t(s.count >> 32)};
-        v.insert(v.end(), w, w + 7);
-    }
-    return v;
+int copy_plan(std::vector<uint32_t>&& v, uint32_t* out, uint64_t capacity, uint64_t* count) {
+    *count = v.size();
+    if (!out) return RT_OK;   // size query
+    if (capacity < v.size()) return fail(RT_ERR_INVALID_ARGUMENT, "capacity");
+    std::memcpy(out, v.data(), v.size() * 4);
+    return RT_OK;
 }
 
-}  // namespace
-
-extern "C" {
-
-int rt_multi_create(uint32_t gpu_count, rt_multi** out) {
+int create(uint32_t gpu_count, bool logical, rt_multi** out) {
     if (!out) return fail(RT_ERR_INVALID_ARGUMENT, "out is NULL");
     *out = nullptr;
     int nd = 0;
@@ -376,22 +446,25 @@ int rt_multi_create(uint32_t gpu_count, rt_multi** out) {
     }
     // every failure below releases what was created so far (streams, events, comms)
     auto body = [&]() -> int {
-        m->n = std::max(1u, std::min(gpu_count, uint32_t(nd)));
+        m->logical = logical;
+        m->n = logical ? std::max(1u, gpu_count) : std::max(1u, std::min(gpu_count, uint32_t(nd)));
+        m->phys.assign(m->n, 0);
+        for (uint32_t d = 0; d < m->n; d++) m->phys[d] = logical ? 0 : int(d);
         m->stream.assign(m->n, nullptr);
         m->comm.assign(m->n, nullptr);
         for (uint32_t d = 0; d < m->n; d++) {
-            DeviceGuard g(static_cast<int>(d));
+            DeviceGuard g(phys_of(m, d));
             RT_HIP(hipStreamCreateWithFlags(&m->stream[d], hipStreamNonBlocking));
         }
         {
-            DeviceGuard g(0);
+            DeviceGuard g(phys_of(m, 0));
             RT_HIP(hipEventCreateWithFlags(&m->ev_in, hipEventDisableTiming));
             RT_HIP(hipEventCreateWithFlags(&m->ev_out, hipEventDisableTiming));
         }
         // A single device's frame plan holds no send or receive (tests/test_multi_plan.py), so
         // one device needs no communicator: the drop-in ray_trace(..., 1) does not pay RCCL's
-        // initialisation on its cold call.
-        if (m->n > 1) {
+        // initialisation on its cold call. Logical devices share GPU 0 and copy instead.
+        if (m->n > 1 && !logical) {
             std::vector<int> devs(m->n);
             for (uint32_t d = 0; d < m->n; d++) devs[d] = int(d);
             RT_NCCL(ncclCommInitAll(m->comm.data(), int(m->n), devs.data()));
@@ -414,19 +487,31 @@ int rt_multi_create(uint32_t gpu_count, rt_multi** out) {
     return RT_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
+int rt_multi_create(uint32_t gpu_count, rt_multi** out) { return create(gpu_count, false, out); }
+
+int rt_debug_multi_create_logical(uint32_t n_devices, rt_multi** out) {
+    if (n_devices == 0 || n_devices > 64) return fail(RT_ERR_INVALID_ARGUMENT, "n_devices must be 1..64");
+    return create(n_devices, true, out);
+}
+
 int rt_multi_destroy(rt_multi* m) {
     if (!m) return RT_OK;
-    free_launches(m);
-    for (uint32_t d = 0; d < m->n; d++) {
-        DeviceGuard g(static_cast<int>(d));
+    if (!m->phys.empty()) free_launches(m);
+    for (uint32_t d = 0; d < m->n && d < m->phys.size(); d++) {
+        DeviceGuard g(phys_of(m, d));
         (void)hipDeviceSynchronize();
         if (d < m->comm.size() && m->comm[d]) (void)ncclCommDestroy(m->comm[d]);
         if (d < m->stream.size() && m->stream[d]) (void)hipStreamDestroy(m->stream[d]);
     }
-    {
-        DeviceGuard g(0);
+    if (!m->phys.empty()) {
+        DeviceGuard g(phys_of(m, 0));
         if (m->ev_in) (void)hipEventDestroy(m->ev_in);
         if (m->ev_out) (void)hipEventDestroy(m->ev_out);
+        for (hipEvent_t e : m->xev) (void)hipEventDestroy(e);
     }
     delete m;
     return RT_OK;
@@ -460,20 +545,72 @@ int rt_multi_render(rt_multi* m, const RenderCallInfo* rci, const rt_options* op
     if (!accum || !out) return fail(RT_ERR_INVALID_ARGUMENT, "accum or out is NULL");
     try {
         if (int rc = set_partition(m, "strips", W, H, strip_parts(m->n, H))) return rc;
+        if (int rc = balance_step(m)) return rc;
     } catch (const std::exception& e) {
         return fail(RT_ERR_OUT_OF_MEMORY, e.what());
     }
     hipStream_t st = static_cast<hipStream_t>(stream);
     {   // the frame starts after the caller's earlier work on `stream` (device 0)
-        DeviceGuard g0(0);
+        DeviceGuard g0(phys_of(m, 0));
         RT_HIP(hipEventRecord(m->ev_in, st));
         for (uint32_t d = 0; d < m->n; d++) RT_HIP(hipStreamWaitEvent(m->stream[d], m->ev_in, 0));
     }
     const bool acc_mode = opt && opt->accumulate;
     if (int rc = run_plan(m, m->plan[acc_mode ? 1 : 0], rci, 1, opt, accum, out)) return rc;
-    DeviceGuard g0(0);
+    try {   // the balancer's record of this frame
+        FrameRecord r;
+        r.parts = current_parts(m);
+        for (const Launch& l : m->launches)
+            r.launch.push_back(l.rows.empty() ? UINT64_MAX : rt::launch_count(l.ctx) - 1);
+        m->bal.history.push_back(std::move(r));
+        while (m->bal.history.size() > 8) m->bal.history.pop_front();
+        m->bal.frames++;
+    } catch (const std::exception& e) {
+        return fail(RT_ERR_OUT_OF_MEMORY, e.what());
+    }
+    DeviceGuard g0(phys_of(m, 0));
     RT_HIP(hipEventRecord(m->ev_out, m->stream[0]));   // the caller's later work waits for it
     RT_HIP(hipStreamWaitEvent(st, m->ev_out, 0));
+    return RT_OK;
+}
+
+int rt_multi_partition(const rt_multi* m, uint32_t* rows, uint32_t* counts, uint32_t capacity) {
+    if (!m || !counts) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    uint64_t total = 0;
+    for (uint32_t d = 0; d < m->n; d++) counts[d] = 0;
+    for (const Launch& l : m->launches) total += l.rows.size();
+    if (rows && capacity < total) return fail(RT_ERR_INVALID_ARGUMENT, "capacity below the image height");
+    uint64_t at = 0;
+    for (const Launch& l : m->launches) {
+        if (l.dev < m->n) counts[l.dev] += uint32_t(l.rows.size());
+        if (rows) std::memcpy(rows + at, l.rows.data(), l.rows.size() * 4);
+        at += l.rows.size();
+    }
+    return RT_OK;
+}
+
+int rt_debug_multi_tune(rt_multi* m, const char* key, double value) {
+    if (!m || !key) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    const std::string k = key;
+    if (k == "balance") m->bal.enabled = value < 0 ? true : value != 0.0;
+    else if (k == "tolerance") m->bal.tolerance = value < 0 ? 0.0005 : value;
+    else if (k == "lag") m->bal.lag = value < 0 ? 2u : std::max<uint32_t>(1, uint32_t(value));
+    else return fail(RT_ERR_INVALID_ARGUMENT, "unknown key " + k);
+    return RT_OK;
+}
+
+int rt_debug_multi_feedback(rt_multi* m, const float* device_ms, uint32_t n) {
+    if (!m || (!device_ms && n)) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    m->bal.injected.assign(device_ms, device_ms + n);
+    return RT_OK;
+}
+
+int rt_debug_multi_balance_info(const rt_multi* m, double* out4) {
+    if (!m || !out4) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    out4[0] = double(m->bal.frames);
+    out4[1] = double(m->bal.rebalances);
+    out4[2] = double(m->bal.moved);
+    out4[3] = m->bal.predicted;
     return RT_OK;
 }
 
@@ -483,24 +620,82 @@ int rt_debug_multi_plan(uint32_t n_devices, uint32_t width, uint32_t height, con
     *count = 0;
     if (n_devices == 0 || width == 0 || height == 0) return fail(RT_ERR_INVALID_ARGUMENT, "zero size");
     if (band_starts && n_bands == 0) return fail(RT_ERR_INVALID_ARGUMENT, "no bands");
-    std::vector<uint32_t> v;
     try {
         Parts parts = band_starts ? band_parts(n_devices, height, band_starts, n_bands) : strip_parts(n_devices, height);
         if (parts.empty()) return fail(RT_ERR_INVALID_ARGUMENT, "bands must tile the image top to bottom");
-        v = serialize(make_plan(width, height, std::move(parts), accumulate != 0));
+        return copy_plan(serialize(make_plan(width, height, std::move(parts), accumulate != 0)), out, capacity, count);
     } catch (const std::exception& e) {
         return fail(RT_ERR_OUT_OF_MEMORY, e.what());
     }
-    *count = v.size();
-    if (!out) return RT_OK;   // size query
-    if (capacity < v.size()) return fail(RT_ERR_INVALID_ARGUMENT, "capacity");
-    std::memcpy(out, v.data(), v.size() * 4);
+}
+
+int rt_debug_multi_plan_rows(uint32_t n_devices, uint32_t width, uint32_t height, const uint32_t* rows,
+                             const uint32_t* counts, uint32_t accumulate, uint32_t* out, uint64_t capacity,
+                             uint64_t* count) {
+    if (!count) return fail(RT_ERR_INVALID_ARGUMENT, "count is NULL");
+    *count = 0;
+    if (n_devices == 0 || width == 0 || height == 0 || !rows || !counts)
+        return fail(RT_ERR_INVALID_ARGUMENT, "zero size or NULL partition");
+    try {
+        Parts parts = row_parts(n_devices, height, rows, counts);
+        if (parts.empty()) return fail(RT_ERR_INVALID_ARGUMENT, "the partition must hold every row exactly once");
+        return copy_plan(serialize(make_plan(width, height, std::move(parts), accumulate != 0)), out, capacity, count);
+    } catch (const std::exception& e) {
+        return fail(RT_ERR_OUT_OF_MEMORY, e.what());
+    }
+}
+
+int rt_partition_strips(uint32_t n_devices, uint32_t height, uint32_t* rows, uint32_t* counts) {
+    if (n_devices == 0 || !rows || !counts) return fail(RT_ERR_INVALID_ARGUMENT, "zero devices or NULL output");
+    try {
+        const Parts parts = strip_parts(n_devices, height);
+        uint64_t at = 0;
+        for (uint32_t d = 0; d < n_devices; d++) {
+            counts[d] = uint32_t(parts[d].second.size());
+            std::memcpy(rows + at, parts[d].second.data(), parts[d].second.size() * 4);
+            at += parts[d].second.size();
+        }
+    } catch (const std::exception& e) {
+        return fail(RT_ERR_OUT_OF_MEMORY, e.what());
+    }
+    return RT_OK;
+}
+
+int rt_partition_rebalance(uint32_t n_devices, uint32_t height, uint32_t* rows, uint32_t* counts, double* row_cost,
+                           const uint32_t* meas_rows, const uint32_t* meas_counts, const float* meas_ms,
+                           double tolerance, uint32_t* moved, double* predicted_imbalance) {
+    if (n_devices == 0 || !rows || !counts || !row_cost) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    if ((meas_rows || meas_counts || meas_ms) && !(meas_rows && meas_counts && meas_ms))
+        return fail(RT_ERR_INVALID_ARGUMENT, "a measurement needs its rows, counts and times");
+    try {
+        Parts cur = row_parts(n_devices, height, rows, counts);
+        if (cur.empty() && height) return fail(RT_ERR_INVALID_ARGUMENT, "the partition must hold every row exactly once");
+        std::vector<double> cost(row_cost, row_cost + height);
+        if (meas_rows) {
+            Parts meas = row_parts(n_devices, height, meas_rows, meas_counts);
+            if (meas.empty() && height)
+                return fail(RT_ERR_INVALID_ARGUMENT, "the measured partition must hold every row exactly once");
+            update_costs(meas, meas_ms, cost);
+        }
+        const uint32_t k = rebalance(cur, cost, tolerance, nullptr);
+        if (moved) *moved = k;
+        if (predicted_imbalance) *predicted_imbalance = imbalance(cur, cost);
+        std::memcpy(row_cost, cost.data(), size_t(height) * sizeof(double));
+        uint64_t at = 0;
+        for (uint32_t d = 0; d < n_devices; d++) {
+            counts[d] = uint32_t(cur[d].second.size());
+            std::memcpy(rows + at, cur[d].second.data(), cur[d].second.size() * 4);
+            at += cur[d].second.size();
+        }
+    } catch (const std::exception& e) {
+        return fail(RT_ERR_OUT_OF_MEMORY, e.what());
+    }
     return RT_OK;
 }
 
 int rt_multi_info(const rt_multi* m, uint32_t* out4) {
     if (!m || !out4) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
-    int ranks = 0;   // 0: one device, no communicator
+    int ranks = 0;   // 0: one device or logical devices, no communicator
     if (m->comm[0]) RT_NCCL(ncclCommCount(m->comm[0], &ranks));
     uint32_t launches = 0;
     for (const Launch& l : m->launches) launches += l.rows.empty() ? 0u : 1u;
@@ -560,7 +755,8 @@ int rt_multi_stats(rt_multi* m, rt_stats* out) {
 }
 
 // Host-buffer frame: the reference's contiguous bands (one per RenderCallInfo, band i on device
-// i % n), gathered to device 0 by the same RCCL path, then copied to the host.
+// i % n), gathered to device 0 by the same RCCL path, then copied to the host. Each band is
+// tonemapped with its own samplesPerRenderCall (the reference's per-band RenderCallInfo).
 int rt_render(const Sphere* spheres, uint32_t sphere_count, const RenderCallInfo* rci, uint32_t rci_count,
               float* accum, uint8_t* out, const rt_options* opt, rt_stats* stats) {
     if (!rci || rci_count == 0) return fail(RT_ERR_INVALID_ARGUMENT, "no RenderCallInfo");
@@ -573,9 +769,6 @@ int rt_render(const Sphere* spheres, uint32_t sphere_count, const RenderCallInfo
         if (rci[i].image_size.x != W || rci[i].image_size.y != H || rci[i].offset.x != 0 || y1 < y0 || y1 > H ||
             (i == 0 && y0 != 0))
             return fail(RT_ERR_INVALID_ARGUMENT, "bands must tile the image top to bottom");
-        // device 0 tonemaps the gathered image once (rt_resolve_rgba8), with one spp
-        if (rci[i].samplesPerRenderCall != rci[0].samplesPerRenderCall)
-            return fail(RT_ERR_INVALID_ARGUMENT, "every band must have the same samplesPerRenderCall");
     }
     rt_multi* m = nullptr;
     if (int rc = rt_multi_create(rci_count, &m)) return rc;
@@ -587,7 +780,7 @@ int rt_render(const Sphere* spheres, uint32_t sphere_count, const RenderCallInfo
         std::vector<uint32_t> starts(rci_count);
         for (uint32_t i = 0; i < rci_count; i++) starts[i] = rci[i].offset.y;
         if (int rc = set_partition(m, "bands", W, H, band_parts(m->n, H, starts.data(), rci_count))) return rc;
-        DeviceGuard g0(0);
+        DeviceGuard g0(phys_of(m, 0));
         RT_HIP(hipMalloc(&dacc, size_t(W) * H * 16));
         RT_HIP(hipMalloc(&dout, size_t(W) * H * 4));
         const bool acc_mode = opt && opt->accumulate;
@@ -618,7 +811,7 @@ int rt_render(const Sphere* spheres, uint32_t sphere_count, const RenderCallInfo
     } catch (const std::exception& e) {
         rc = fail(RT_ERR_OUT_OF_MEMORY, e.what());
     }
-    DeviceGuard g0(0);
+    DeviceGuard g0(phys_of(m, 0));
     if (dacc) (void)hipFree(dacc);
     if (dout) (void)hipFree(dout);
     return rc;

@@ -26,7 +26,7 @@ __all__ = [
     "DIFFUSE", "METAL", "REFRACTIVE", "SOLID", "CHECKERED", "Sphere", "Scene", "RenderCallInfo",
     "Options", "Stats", "RtError", "generateRandomScene", "canonical_render_call_info",
     "make_options", "Renderer", "MultiRenderer", "render", "ray_trace", "store_ppm", "spheres_to_numpy",
-    "load_library", "HASH", "STREAM", "multi_plan",
+    "load_library", "HASH", "STREAM", "multi_plan", "partition_strips", "partition_rebalance",
 ]
 
 STREAM = abi.RT_RNG_PIXEL_STREAM   # the reference's per-pixel LCG stream (random.glsl)
@@ -295,6 +295,20 @@ class Renderer:
         check(self._lib.rt_resolve_rgba8(self._ctx, accum.data_ptr(), n, spp, out.data_ptr(),
                                          _stream_ptr(stream, self.device)))
 
+    def launch_ms(self, back: int = 0) -> float:
+        """Trace-kernel ms of the launch `back` launches before the most recent one (rt_launch_ms:
+        waits for that launch only, not for the ones queued after it)."""
+        v = ctypes.c_float()
+        check(self._lib.rt_launch_ms(self._ctx, back, ctypes.byref(v)))
+        return float(v.value)
+
+    def launch_row_weights(self, band_rows: int, back: int = 0) -> np.ndarray:
+        """Per band row of the launch `back` launches before the most recent one, its share of the
+        launch's work from the tile-cost record (rt_launch_row_weights; ratios only)."""
+        w = np.zeros(max(1, band_rows), np.float64)
+        check(self._lib.rt_launch_row_weights(self._ctx, back, w.ctypes.data, band_rows))
+        return w[:band_rows]
+
     def kernel_times(self, n: int = 64) -> list:
         """Trace-kernel durations (ms) of the last `n` launches (at most 64 kept), oldest first:
         HIP events recorded around the kernel on its launch stream (rt_debug_kernel_times)."""
@@ -306,14 +320,19 @@ class Renderer:
 
 class MultiRenderer:
     """One process driving `gpu_count` GPUs (rt_multi): one context + stream per device and one
-    RCCL communicator over them. A frame tiles the image into 8-row strips dealt round robin over
-    the devices and gathers every device's strips to device 0 over xGMI (grouped ncclSend /
-    ncclRecv), where they are reordered; the image equals the one-GPU image bit for bit."""
+    RCCL communicator over them. A frame tiles the image into row-exact interleaved strips
+    (partition_strips), re-dealt between frames from the devices' measured kernel times, and
+    gathers every device's rows to device 0 over xGMI (grouped ncclSend / ncclRecv), where they
+    are reordered; the image equals the one-GPU image bit for bit.
 
-    def __init__(self, gpu_count: int = 1):
+    logical=True (tests on a one-GPU box): `gpu_count` logical devices on GPU 0 running the same
+    frame plans, each RCCL send / receive pair a device copy (rt_debug_multi_create_logical)."""
+
+    def __init__(self, gpu_count: int = 1, logical: bool = False):
         self._lib = load_library()
         self._m = ctypes.c_void_p()
-        check(self._lib.rt_multi_create(gpu_count, ctypes.byref(self._m)))
+        create = self._lib.rt_debug_multi_create_logical if logical else self._lib.rt_multi_create
+        check(create(gpu_count, ctypes.byref(self._m)))
         n = ctypes.c_uint32()
         check(self._lib.rt_multi_device_count(self._m, ctypes.byref(n)))
         self.device_count = n.value
@@ -378,24 +397,111 @@ class MultiRenderer:
         check(self._lib.rt_multi_stats(self._m, ctypes.byref(st)))
         return st
 
+    def partition(self, height: int) -> list:
+        """The rows each device renders in the next frame (band order), one uint32 array per
+        device (rt_multi_partition)."""
+        counts = np.zeros(self.device_count, np.uint32)
+        rows = np.zeros(max(1, height), np.uint32)
+        check(self._lib.rt_multi_partition(self._m, rows.ctypes.data, counts.ctypes.data, height))
+        return _split(rows, counts)
+
+    def tune(self, **kv) -> None:
+        """Balancer settings (rt_debug_multi_tune): balance=0/1, tolerance, lag; None restores."""
+        for k, v in kv.items():
+            check(self._lib.rt_debug_multi_tune(self._m, k.encode(), -1.0 if v is None else float(v)))
+
+    def feedback(self, device_ms: Sequence[float]) -> None:
+        """Device times the next frame re-deals from, as if measured (rt_debug_multi_feedback)."""
+        buf = (ctypes.c_float * max(1, len(device_ms)))(*device_ms)
+        check(self._lib.rt_debug_multi_feedback(self._m, buf, len(device_ms)))
+
+    def balance_info(self) -> dict:
+        v = (ctypes.c_double * 4)()
+        check(self._lib.rt_debug_multi_balance_info(self._m, v))
+        return {"frames": int(v[0]), "rebalances": int(v[1]), "rows_moved": int(v[2]),
+                "predicted_imbalance": float(v[3])}
+
+
+def _split(rows: np.ndarray, counts: np.ndarray) -> list:
+    out, at = [], 0
+    for c in counts:
+        out.append(rows[at:at + int(c)].copy())
+        at += int(c)
+    return out
+
+
+def _flat(parts: Sequence) -> tuple:
+    counts = np.asarray([len(p) for p in parts], np.uint32)
+    rows = np.ascontiguousarray(np.concatenate([np.asarray(p, np.uint32) for p in parts])
+                                if len(parts) else np.zeros(0, np.uint32), np.uint32)
+    return rows, counts
+
+
+def partition_strips(n_devices: int, height: int) -> list:
+    """The row-exact interleaved strips every multi-device frame starts from (rt_partition_strips):
+    one uint32 array of global rows per device, band order."""
+    counts = np.zeros(n_devices, np.uint32)
+    rows = np.zeros(max(1, height), np.uint32)
+    check(load_library().rt_partition_strips(n_devices, height, rows.ctypes.data, counts.ctypes.data))
+    return _split(rows, counts)
+
+
+def partition_rebalance(parts: Sequence, cost: np.ndarray, measured: Optional[Sequence] = None,
+                        device_ms: Optional[Sequence[float]] = None, tolerance: float = 0.0005) -> tuple:
+    """One balancing step (rt_partition_rebalance): rescale the per-row costs `cost` (float64 [H],
+    <= 0 unknown; updated in place) to the device times `device_ms` measured on partition
+    `measured`, then re-deal `parts`. Returns (new parts, rows moved, predicted max / mean)."""
+    lib = load_library()
+    n, H = len(parts), int(cost.shape[0])
+    if cost.dtype != np.float64 or not cost.flags.c_contiguous:
+        raise ValueError("cost must be a contiguous float64 array")
+    rows, counts = _flat(parts)
+    if len(rows) != H:
+        raise ValueError("the partition must hold every row exactly once")
+    m_rows = m_counts = m_ms = None
+    keep = []
+    if measured is not None:
+        mr, mc = _flat(measured)
+        ms = np.ascontiguousarray(np.asarray(device_ms, np.float32))
+        if len(ms) != n or len(mc) != n:
+            raise ValueError("one measured time per device")
+        keep = [mr, mc, ms]
+        m_rows, m_counts, m_ms = mr.ctypes.data, mc.ctypes.data, ms.ctypes.data
+    moved = ctypes.c_uint32(0)
+    pred = ctypes.c_double(1.0)
+    check(lib.rt_partition_rebalance(n, H, rows.ctypes.data, counts.ctypes.data, cost.ctypes.data, m_rows, m_counts,
+                                     m_ms, float(tolerance), ctypes.byref(moved), ctypes.byref(pred)))
+    del keep
+    return _split(rows, counts), int(moved.value), float(pred.value)
+
 
 PLAN_OPS = {1: "load_rows", 2: "group_start", 3: "send", 4: "recv", 5: "group_end", 6: "render",
             7: "store_rows", 8: "resolve"}
 
 
 def multi_plan(n_devices: int, width: int, height: int, band_starts: Optional[Sequence[int]] = None,
-               accumulate: bool = False) -> dict:
+               accumulate: bool = False, parts: Optional[Sequence] = None) -> dict:
     """The frame plan rt_multi executes (rt_debug_multi_plan; host only, no GPU needed): the parts
     [(device, whole, rows)] and the ordered steps [{op, dev, peer, part, flags, count}]. band_starts
-    None: 8-row strips dealt round robin (rt_multi_render); else the bands of rt_render."""
+    None: the row-exact strips (rt_multi_render's first frame); else the bands of rt_render; parts:
+    an explicit partition (one row array per device, e.g. a re-dealt one; rt_debug_multi_plan_rows)."""
     lib = load_library()
-    bs = None if band_starts is None else (ctypes.c_uint32 * len(band_starts))(*band_starts)
-    nb = 0 if band_starts is None else len(band_starts)
     n = ctypes.c_uint64(0)
-    check(lib.rt_debug_multi_plan(n_devices, width, height, bs, nb, int(accumulate), None, 0, ctypes.byref(n)))
+    if parts is not None:
+        rows, counts = _flat(parts)
+        if len(counts) != n_devices:
+            raise ValueError("one row array per device")
+        call = lambda out, cap: lib.rt_debug_multi_plan_rows(n_devices, width, height, rows.ctypes.data,  # noqa: E731
+                                                              counts.ctypes.data, int(accumulate), out, cap,
+                                                              ctypes.byref(n))
+    else:
+        bs = None if band_starts is None else (ctypes.c_uint32 * len(band_starts))(*band_starts)
+        nb = 0 if band_starts is None else len(band_starts)
+        call = lambda out, cap: lib.rt_debug_multi_plan(n_devices, width, height, bs, nb, int(accumulate),  # noqa: E731
+                                                         out, cap, ctypes.byref(n))
+    check(call(None, 0))
     buf = np.zeros(n.value, np.uint32)
-    check(lib.rt_debug_multi_plan(n_devices, width, height, bs, nb, int(accumulate), buf.ctypes.data, n.value,
-                                  ctypes.byref(n)))
+    check(call(buf.ctypes.data, n.value))
     n_parts, n_steps = int(buf[0]), int(buf[1])
     at, parts, steps = 2, [], []
     for _ in range(n_parts):

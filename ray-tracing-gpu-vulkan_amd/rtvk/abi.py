@@ -110,6 +110,8 @@ EXPORTS = {
     "rt_render_device": (_I, [_P, ctypes.POINTER(RenderCallInfo), _P, _U32, _U32, _P, _P,
                               ctypes.POINTER(Options), _P]),
     "rt_get_stats": (_I, [_P, ctypes.POINTER(Stats)]),
+    "rt_launch_ms": (_I, [_P, _U32, ctypes.POINTER(ctypes.c_float)]),
+    "rt_launch_row_weights": (_I, [_P, _U32, _P, _U32]),
     "rt_scatter_rows": (_I, [_P, _P, _P, _P, _U32, _U32, _U32, _P, _P, _P]),
     "rt_resolve_rgba8": (_I, [_P, _P, ctypes.c_uint64, _U32, _P, _P]),
     "rt_gather_rows": (_I, [_P, _P, _P, _U32, _U32, _U32, _P, _P]),
@@ -122,6 +124,10 @@ EXPORTS = {
     "rt_multi_info": (_I, [_P, _P]),
     "rt_multi_kernel_times": (_I, [_P, _P, _U32, ctypes.POINTER(_U32)]),
     "rt_multi_kernel_times_frames": (_I, [_P, _U32, _P, _U32, ctypes.POINTER(_U32)]),
+    "rt_multi_partition": (_I, [_P, _P, _P, _U32]),
+    "rt_partition_strips": (_I, [_U32, _U32, _P, _P]),
+    "rt_partition_rebalance": (_I, [_U32, _U32, _P, _P, _P, _P, _P, _P, ctypes.c_double, ctypes.POINTER(_U32),
+                                    ctypes.POINTER(ctypes.c_double)]),
     "rt_render": (_I, [_P, _U32, _P, _U32, _P, _P, ctypes.POINTER(Options), ctypes.POINTER(Stats)]),
     "rt_store_ppm": (_I, [ctypes.c_char_p, _P, _U32, _U32]),
     "rt_debug_math": (_I, [_I, _I, _P, _P, _U32]),
@@ -143,6 +149,12 @@ EXPORTS = {
     # include/rt_mi355x_debug.h (diagnostics, A/B, the multi-GPU frame plan)
     "rt_debug_multi_plan": (_I, [_U32, _U32, _U32, _P, _U32, _U32, _P, ctypes.c_uint64,
                                  ctypes.POINTER(ctypes.c_uint64)]),
+    "rt_debug_multi_plan_rows": (_I, [_U32, _U32, _U32, _P, _P, _U32, _P, ctypes.c_uint64,
+                                      ctypes.POINTER(ctypes.c_uint64)]),
+    "rt_debug_multi_create_logical": (_I, [_U32, ctypes.POINTER(_P)]),
+    "rt_debug_multi_tune": (_I, [_P, ctypes.c_char_p, ctypes.c_double]),
+    "rt_debug_multi_feedback": (_I, [_P, _P, _U32]),
+    "rt_debug_multi_balance_info": (_I, [_P, _P]),
 }
 
 _lib = None

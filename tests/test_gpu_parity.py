@@ -542,18 +542,19 @@ def test_host_rt_render_bands(rtvk, oracle, rng_mode):
 
 
 @pytest.mark.parametrize("rng_mode", [STREAM, HASH])
-def test_multi_renderer_rccl(rtvk, torch, oracle, rng_mode):
-    """rt_multi (one process, every visible GPU up to 8, one RCCL communicator): 8-row strips
-    dealt round robin, every other device's strips sent to device 0 in one RCCL group and
-    reordered there (one device holding every row renders straight into the caller's buffers);
-    two frames (the second with the LPT order) equal the one-device oracle frame bit for bit, and
-    the statistics are summed over the devices."""
+def test_multi_renderer_visible_devices(rtvk, torch, oracle, rng_mode):
+    """rt_multi over every visible GPU (up to 8): on a multi-GPU box one RCCL communicator, the
+    row-exact strips and every other device's rows sent to device 0 in one RCCL group; on a one-GPU
+    box one device holding every row renders straight into the caller's buffers (no communicator).
+    Two frames (the second with the LPT order) equal the one-device oracle frame bit for bit, and
+    the statistics are summed over the devices. (test_multi_logical_devices runs the N > 1 steps
+    on one GPU.)"""
     W, H, spp = 72, 43, 3
     sc = oracle.generate_scene()
     rci_np = oracle.render_call_info(spp, W, H)
     ra, ro, rs = oracle.render(sc, rci_np, W, H, opts=oracle.options(rng_mode=rng_mode))
     with rtvk.MultiRenderer(8) as m:
-        assert m.device_count == torch.cuda.device_count() or m.device_count == 8
+        assert m.device_count == min(8, torch.cuda.device_count())
         m.set_scene(sc)
         rci = rtvk.RenderCallInfo.from_buffer_copy(rci_np.tobytes())
         for _ in range(2):
@@ -564,6 +565,136 @@ def test_multi_renderer_rccl(rtvk, torch, oracle, rng_mode):
             assert_same(acc.cpu().numpy(), out.cpu().numpy(), ra, ro)
             st = m.stats()
             assert (st.segments, st.samples) == rs[:2]
+        info = m.info()
+        if m.device_count > 1:   # the frame reached the RCCL group: every device rendered rows
+            assert info["rccl_ranks"] == m.device_count and info["launches"] == m.device_count
+        else:
+            assert info["rccl_ranks"] == 0 and info["launches"] == 1
+
+
+LOGICAL_W, LOGICAL_H = 48, 1080
+
+
+@pytest.fixture(scope="module")
+def logical_refs(oracle):
+    """Oracle frames of the logical-device tests: 48 x 1080 at 2 spp (frame 0) and 2 more samples
+    accumulated on top (frame 1), in both streams."""
+    sc = oracle.generate_scene()
+    rci = oracle.render_call_info(2, LOGICAL_W, LOGICAL_H)
+    refs = {}
+    for mode in (STREAM, HASH):
+        base = 2 if mode != STREAM else 0
+        a0, o0, s0 = oracle.render(sc, rci, LOGICAL_W, LOGICAL_H, opts=oracle.options(rng_mode=mode), threads=16)
+        a1, o1, _ = oracle.render(sc, rci, LOGICAL_W, LOGICAL_H, accum=a0, threads=16,
+                                  opts=oracle.options(rng_mode=mode, accumulate=1, sample_base=base))
+        refs[mode] = ((a0, o0, s0), (a1, o1))
+    return sc, rci, refs
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+@pytest.mark.parametrize("rng_mode", [STREAM, HASH])
+def test_multi_logical_devices(rtvk, torch, logical_refs, n, rng_mode):
+    """rt_multi's N > 1 frame on one GPU (rt_debug_multi_create_logical): n logical devices with
+    their own contexts and streams, the row-exact strips, the send / receive pairs of each RCCL
+    group as device copies in the group's order, device 0's stage / band buffer selection, the row
+    loads and stores and the one resolve: a plain frame and an accumulating frame on top equal the
+    oracle bit for bit (the reference's per-GPU band loop, src/ray_trace.cpp:42-105)."""
+    sc, rci_np, refs = logical_refs
+    (ra0, ro0, rs0), (ra1, ro1) = refs[rng_mode]
+    rci = rtvk.RenderCallInfo.from_buffer_copy(rci_np.tobytes())
+    with rtvk.MultiRenderer(n, logical=True) as m:
+        assert m.device_count == n and m.info()["rccl_ranks"] == 0
+        m.tune(balance=0)
+        m.set_scene(sc)
+        parts = m.partition(LOGICAL_H)
+        sizes = [len(p) for p in parts]
+        assert sum(sizes) == LOGICAL_H and max(sizes) - min(sizes) <= 1
+        acc = torch.zeros((LOGICAL_H, LOGICAL_W, 4), dtype=torch.float32, device="cuda:0")
+        out = torch.zeros((LOGICAL_H, LOGICAL_W, 4), dtype=torch.uint8, device="cuda:0")
+        m.render(rci, acc, out, options=rtvk.make_options(rng_mode=rng_mode))
+        torch.cuda.synchronize()
+        assert_same(acc.cpu().numpy(), out.cpu().numpy(), ra0, ro0)
+        st = m.stats()
+        assert (st.segments, st.samples) == rs0[:2]
+        assert m.info()["launches"] == n
+        base = 2 if rng_mode != STREAM else 0
+        m.render(rci, acc, out, options=rtvk.make_options(rng_mode=rng_mode, accumulate=True, sample_base=base))
+        torch.cuda.synchronize()
+        assert_same(acc.cpu().numpy(), out.cpu().numpy(), ra1, ro1)
+
+
+@pytest.mark.parametrize("rng_mode", [STREAM, HASH])
+def test_multi_logical_rebalance(rtvk, torch, logical_refs, rng_mode):
+    """The balancer's re-deals on 8 logical devices: device times fed every frame (device 0 and 3
+    slow, rt_debug_multi_feedback) move rows between the devices' bands (rows maps rewritten,
+    buffers grown, the LPT records carried over); every frame, plain and accumulating, stays equal
+    to the oracle bit for bit, and the partition always holds every row once."""
+    sc, rci_np, refs = logical_refs
+    (ra0, ro0, _), (ra1, ro1) = refs[rng_mode]
+    rci = rtvk.RenderCallInfo.from_buffer_copy(rci_np.tobytes())
+    base = 2 if rng_mode != STREAM else 0
+    with rtvk.MultiRenderer(8, logical=True) as m:
+        m.set_scene(sc)
+        start = [p.copy() for p in m.partition(LOGICAL_H)]
+        acc = torch.zeros((LOGICAL_H, LOGICAL_W, 4), dtype=torch.float32, device="cuda:0")
+        out = torch.zeros((LOGICAL_H, LOGICAL_W, 4), dtype=torch.uint8, device="cuda:0")
+        for f in range(6):
+            parts = m.partition(LOGICAL_H)
+            assert sorted(np.concatenate(parts).tolist()) == list(range(LOGICAL_H))
+            ms = [float(len(p)) * (1.3 if d in (0, 3) else 1.0) for d, p in enumerate(parts)]
+            m.feedback(ms)
+            m.render(rci, acc, out, options=rtvk.make_options(rng_mode=rng_mode))
+            torch.cuda.synchronize()
+            assert_same(acc.cpu().numpy(), out.cpu().numpy(), ra0, ro0)
+            m.feedback(ms)
+            m.render(rci, acc, out, options=rtvk.make_options(rng_mode=rng_mode, accumulate=True, sample_base=base))
+            torch.cuda.synchronize()
+            assert_same(acc.cpu().numpy(), out.cpu().numpy(), ra1, ro1)
+        info = m.balance_info()
+        assert info["rebalances"] >= 2 and info["rows_moved"] >= 8
+        end = m.partition(LOGICAL_H)
+        assert len(end[0]) < len(start[0]) and len(end[3]) < len(start[3])
+
+
+@pytest.mark.parametrize("rng_mode", [STREAM, HASH])
+def test_multi_zero_spp_matches_one_device(rtvk, torch, oracle, rng_mode):
+    """samplesPerRenderCall = 0 renders the same bytes at every device count (the
+    multi-device resolve used to refuse spp 0 that the one-device frame accepts)."""
+    W, H = 24, 40
+    sc = oracle.generate_scene()
+    rci = rtvk.RenderCallInfo.from_buffer_copy(oracle.render_call_info(0, W, H).tobytes())
+    got = []
+    for n, logical in ((1, False), (3, True)):
+        with rtvk.MultiRenderer(n, logical=logical) as m:
+            m.set_scene(sc)
+            acc = torch.full((H, W, 4), 3.0, dtype=torch.float32, device="cuda:0")
+            out = torch.full((H, W, 4), 9, dtype=torch.uint8, device="cuda:0")
+            m.render(rci, acc, out, options=rtvk.make_options(rng_mode=rng_mode))
+            torch.cuda.synchronize()
+            got.append((acc.cpu().numpy(), out.cpu().numpy()))
+    np.testing.assert_array_equal(got[0][0].view(np.uint32), got[1][0].view(np.uint32))
+    np.testing.assert_array_equal(got[0][1], got[1][1])
+
+
+def test_host_rt_render_bands_own_spp(rtvk, oracle):
+    """rt_render's bands each carry their own RenderCallInfo (src/ray_trace.cpp:660-676 fills one
+    per GPU): bands of different samplesPerRenderCall are each rendered and tonemapped with their
+    own spp (round 5 refused them)."""
+    W, H = 32, 20
+    sc = oracle.generate_scene()
+    starts, spps = (0, 7, 13), (2, 3, 1)
+    rcis = []
+    for y, spp in zip(starts, spps):
+        r = rtvk.canonical_render_call_info(spp, W, H)
+        r.offset.y = y
+        rcis.append(r)
+    res = rtvk.render(rtvk.generateRandomScene(), rcis, options=rtvk.make_options(rng_mode=STREAM))
+    for i, (y0, spp) in enumerate(zip(starts, spps)):
+        y1 = starts[i + 1] if i + 1 < len(starts) else H
+        rows = np.arange(y0, y1, dtype=np.uint32)
+        ra, ro, _ = oracle.render(sc, oracle.render_call_info(spp, W, H), W, len(rows), rows=rows,
+                                  opts=oracle.options(rng_mode=STREAM))
+        assert_same(res.accum[y0:y1], res.rgba8[y0:y1], ra, ro)
 
 
 @pytest.mark.parametrize("rng_mode", [COUNTER, HASH])

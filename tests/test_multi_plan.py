@@ -4,8 +4,9 @@ rt_multi_render / rt_render execute (rt_debug_multi_plan serialises the same Fra
 tests cover the N > 1 logic that a one-GPU box never runs.
 
 Reference: the bands of src/ray_trace.cpp:74-93 (rt_render) and the per-GPU row split the
-reference records per benchmark window (:750-760); here 8-row strips dealt round robin
-(rtvk.dist.strip_rows, rt_multi_render)."""
+reference records per benchmark window (:750-760) and re-deals (src/workload_tuner.hpp:38-104);
+here row-exact interleaved strips (rtvk.dist.strip_rows, rt_partition_strips) re-dealt by
+rt_partition_rebalance (rt_multi_render, rtvk.dist)."""
 import numpy as np
 import pytest
 
@@ -200,3 +201,114 @@ def test_gather_bytes_config4(rtvk):
     sends = [s for s in plan["steps"] if s["op"] == "send"]
     assert len(sends) == 7
     assert sum(s["count"] for s in sends) * 4 == 1920 * (1080 - len(strip_rows(0, 8, 1080))) * 16
+
+
+def random_partition(rng, n, H):
+    """Every row once, in a random order, over n devices (some possibly empty)."""
+    perm = rng.permutation(H).astype(np.uint32)
+    cuts = np.sort(rng.integers(0, H + 1, n - 1))
+    return [perm[a:b] for a, b in zip(np.r_[0, cuts], np.r_[cuts, H])]
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+@pytest.mark.parametrize("H", [5, 27, 1080])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_plan_for_arbitrary_rows(rtvk, n, H, accumulate):
+    """Any partition (a re-dealt one: rows in any order, devices of any size, empty ones): the plan
+    keeps each device's rows in band order, pairs every send with one receive, and its numpy
+    execution reproduces the frame (+ the running sums)."""
+    rng = np.random.default_rng(n * 7919 + H + accumulate)
+    for trial in range(3):
+        parts = random_partition(rng, n, H)
+        plan = rtvk.multi_plan(n, 1, H, accumulate=accumulate, parts=parts)
+        assert len(plan["parts"]) == n
+        for d, (dev, whole, rows) in enumerate(plan["parts"]):
+            assert dev == d
+            np.testing.assert_array_equal(rows, parts[d])
+        live = [i for i, p in enumerate(plan["parts"]) if len(p[2])]
+        assert sorted(s["part"] for s in plan["steps"] if s["op"] == "render") == live
+        assert all(s["dev"] != s["peer"] for s in plan["steps"] if s["op"] == "send")
+        acc0 = rng.integers(0, 1000, (H, 1, 4)).astype(np.float64) if accumulate else np.full((H, 1, 4), np.nan)
+        frame = rng.integers(0, 1000, (H, 1, 4)).astype(np.float64)
+        acc, resolved = simulate(plan, 1, H, n, accumulate, acc0, frame)
+        np.testing.assert_array_equal(acc, acc0 + frame if accumulate else frame)
+        assert resolved.all()
+
+
+def test_plan_rows_rejects_bad_partitions(rtvk):
+    with pytest.raises(rtvk.RtError):
+        rtvk.multi_plan(2, 4, 6, parts=[np.array([0, 1, 2]), np.array([2, 3, 4, 5])])   # row 2 twice
+    with pytest.raises(rtvk.RtError):
+        rtvk.multi_plan(2, 4, 6, parts=[np.array([0, 1, 2]), np.array([3, 4])])          # row 5 missing
+    with pytest.raises(rtvk.RtError):
+        rtvk.multi_plan(2, 4, 6, parts=[np.array([0, 1, 2]), np.array([3, 4, 9])])       # row 9 of 6
+
+
+def loads(parts, cost):
+    return np.array([cost[p].sum() for p in parts])
+
+
+@pytest.mark.parametrize("n,H", [(2, 1080), (3, 1080), (8, 1080), (8, 2160), (7, 1080), (8, 27), (8, 7)])
+def test_rebalance_properties(rtvk, n, H):
+    """rt_partition_rebalance: every row still once; rows leave only from a band's last 8 rows (a
+    device that gives k rows changes from index len - 8 - k on) and join at its end, so every other
+    tile keeps its index and LPT record; each step lowers the most loaded device's load;
+    deterministic; a balanced partition is left alone."""
+    rng = np.random.default_rng(n * 31 + H)
+    parts = rtvk.partition_strips(n, H)
+    true = 1.0 + rng.random(H) * 2.0   # per-row ms, sky-to-sphere spread
+    cost = true.copy()
+    prev_max = loads(parts, cost).max()
+    for it in range(6):
+        before = [p.copy() for p in parts]
+        new, moved, pred = rtvk.partition_rebalance(parts, cost, tolerance=0.0)
+        again, moved2, pred2 = rtvk.partition_rebalance(before, cost.copy(), tolerance=0.0)
+        for a, b in zip(new, again):   # deterministic
+            np.testing.assert_array_equal(a, b)
+        assert (moved, pred) == (moved2, pred2)
+        assert sorted(np.concatenate(new).tolist()) == list(range(H))
+        for old, nw in zip(before, new):
+            gave = len(set(old.tolist()) - set(nw.tolist()))
+            keep = max(0, len(old) - 8 - gave) if gave else len(old)
+            np.testing.assert_array_equal(nw[:keep], old[:keep])
+        L = loads(new, cost)
+        assert L.max() <= prev_max + 1e-9
+        assert pred == pytest.approx(L.max() / L.mean(), rel=1e-9)
+        prev_max = L.max()
+        parts = new
+        if not moved:
+            break
+    if H >= 8 * n:   # enough rows: within one row's cost of the mean
+        L = loads(parts, cost)
+        assert L.max() - L.mean() <= true.max() + 1e-9
+
+
+def test_rebalance_measured_feedback(rtvk):
+    """Config 4's shape: the device times of round 5's N = 8 band probe (rank 7 faster) fed as a
+    measurement of the row-exact strips: rows leave the slow devices, the predicted imbalance drops
+    below the measured one, and an even measurement moves nothing."""
+    parts = rtvk.partition_strips(8, 1080)
+    ms = [139.0, 138.5, 138.7, 139.2, 138.4, 138.9, 139.1, 131.4]
+    cost = np.zeros(1080)
+    new, moved, pred = rtvk.partition_rebalance(parts, cost, measured=parts, device_ms=ms)
+    assert moved > 0 and pred < max(ms) / np.mean(ms)
+    for p, t in zip(parts, ms):   # the estimates sum to each device's measured time
+        assert cost[p].sum() == pytest.approx(float(np.float32(t)), rel=1e-9)   # times travel as f32
+    assert len(new[7]) > len(parts[7])
+    cost2 = np.zeros(1080)
+    same, moved0, pred0 = rtvk.partition_rebalance(parts, cost2, measured=parts, device_ms=[100.0] * 8)
+    assert moved0 == 0 and pred0 == pytest.approx(1.0)
+    for a, b in zip(same, parts):
+        np.testing.assert_array_equal(a, b)
+
+
+def test_rebalance_rejects_bad_input(rtvk):
+    parts = rtvk.partition_strips(2, 16)
+    dup = parts[1].copy()
+    dup[-1] = parts[0][0]
+    with pytest.raises(rtvk.RtError):
+        rtvk.partition_rebalance([parts[0], dup], np.zeros(16))               # a row twice, one missing
+    with pytest.raises(ValueError):
+        rtvk.partition_rebalance([parts[0], parts[1][:-1]], np.zeros(16))     # a row missing
+    with pytest.raises(ValueError):
+        rtvk.partition_rebalance(parts, np.zeros(16, np.float32))             # cost not float64
