@@ -266,7 +266,8 @@ int rt_multi_kernel_times(rt_multi* m, float* out_ms, uint32_t capacity, uint32_
  * first; *count = frames x devices that rendered rows (synchronises). */
 int rt_multi_kernel_times_frames(rt_multi* m, uint32_t frames, float* out_ms, uint32_t capacity, uint32_t* count);
 /* The partition the next frame renders with: counts[d] rows on device d (n entries), and with rows
- * non-NULL (capacity >= image height) the rows, device 0's first, each device's in band order. */
+ * non-NULL (capacity >= image height) the rows, device 0's first, each device's in band order.
+ * Set up by the first rt_multi_render of an image size (all counts 0 before it). */
 int rt_multi_partition(const rt_multi* m, uint32_t* rows, uint32_t* counts, uint32_t capacity);
 
 /* ---- row partition across devices (host only, no device needed) --------------------- */

@@ -4,8 +4,8 @@ kernel's duration (HIP events on the launch stream) and the tail after the work 
 (s_memrealtime stamps of the launch, rt_debug_lane_hist), per setting. Every setting renders the
 same image (checked against the first setting's, bit for bit).
 
-usage: python scripts/band_tune.py [N=8] [spp=10000] [--rank 0] [--rounds 3]
-       [--set name:key=v,key=v ...] (default sets below)"""
+usage: python scripts/band_tune.py [N=8] [spp=10000] [--rank 0] [--rounds 3] [--full]
+       [--width W --height H --grid K] [--set name:key=v,key=v ...] (default sets below)"""
 import argparse
 import ctypes
 import json
@@ -19,7 +19,7 @@ import torch  # noqa: E402
 
 import rtvk  # noqa: E402
 from rtvk import abi  # noqa: E402
-from rtvk.dist import strip_rows  # noqa: E402
+
 
 DEFAULT_SETS = [
     "default:",
@@ -37,9 +37,12 @@ ap.add_argument("spp", type=int, nargs="?", default=10000)
 ap.add_argument("--rank", type=int, default=0)
 ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--full", action="store_true", help="the whole frame instead of one band")
+ap.add_argument("--width", type=int, default=1920)
+ap.add_argument("--height", type=int, default=1080)
+ap.add_argument("--grid", type=int, default=11)
 ap.add_argument("--set", nargs="*", default=None)
 args = ap.parse_args()
-W, H = 1920, 1080
+W, H = args.width, args.height
 sets = []
 for spec in (args.set or DEFAULT_SETS):
     name, _, kv = spec.partition(":")
@@ -49,10 +52,10 @@ for spec in (args.set or DEFAULT_SETS):
         d[k] = float(v)
     sets.append((name, d))
 lib = abi.load_library()
-scene = rtvk.generateRandomScene()
+scene = rtvk.generateRandomScene(0.0, args.grid)
 rci = rtvk.canonical_render_call_info(args.spp, W, H)
 opt = rtvk.make_options(accel=abi.RT_ACCEL_LBVH, rng_mode=rtvk.HASH)
-rows_np = None if args.full else strip_rows(args.rank, args.n, H)
+rows_np = None if args.full else rtvk.partition_strips(args.n, H)[args.rank].astype(np.int32)
 n = H if rows_np is None else len(rows_np)
 rows = None if rows_np is None else torch.from_numpy(rows_np).cuda()
 ctxs = []

@@ -606,14 +606,14 @@ def test_multi_logical_devices(rtvk, torch, logical_refs, n, rng_mode):
         assert m.device_count == n and m.info()["rccl_ranks"] == 0
         m.tune(balance=0)
         m.set_scene(sc)
-        parts = m.partition(LOGICAL_H)
-        sizes = [len(p) for p in parts]
-        assert sum(sizes) == LOGICAL_H and max(sizes) - min(sizes) <= 1
         acc = torch.zeros((LOGICAL_H, LOGICAL_W, 4), dtype=torch.float32, device="cuda:0")
         out = torch.zeros((LOGICAL_H, LOGICAL_W, 4), dtype=torch.uint8, device="cuda:0")
         m.render(rci, acc, out, options=rtvk.make_options(rng_mode=rng_mode))
         torch.cuda.synchronize()
         assert_same(acc.cpu().numpy(), out.cpu().numpy(), ra0, ro0)
+        parts = m.partition(LOGICAL_H)   # the row-exact strips the frame rendered
+        for a, b in zip(parts, rtvk.partition_strips(n, LOGICAL_H)):
+            np.testing.assert_array_equal(a, b)
         st = m.stats()
         assert (st.segments, st.samples) == rs0[:2]
         assert m.info()["launches"] == n
@@ -635,9 +635,12 @@ def test_multi_logical_rebalance(rtvk, torch, logical_refs, rng_mode):
     base = 2 if rng_mode != STREAM else 0
     with rtvk.MultiRenderer(8, logical=True) as m:
         m.set_scene(sc)
-        start = [p.copy() for p in m.partition(LOGICAL_H)]
+        start = rtvk.partition_strips(8, LOGICAL_H)
         acc = torch.zeros((LOGICAL_H, LOGICAL_W, 4), dtype=torch.float32, device="cuda:0")
         out = torch.zeros((LOGICAL_H, LOGICAL_W, 4), dtype=torch.uint8, device="cuda:0")
+        m.render(rci, acc, out, options=rtvk.make_options(rng_mode=rng_mode))   # sets up the strips
+        torch.cuda.synchronize()
+        assert_same(acc.cpu().numpy(), out.cpu().numpy(), ra0, ro0)
         for f in range(6):
             parts = m.partition(LOGICAL_H)
             assert sorted(np.concatenate(parts).tolist()) == list(range(LOGICAL_H))
