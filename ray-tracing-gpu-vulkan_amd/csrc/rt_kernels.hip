@@ -1241,6 +1241,49 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
     float tz = bound_t(cz, sz, 2, r.o.z, r.inv.z);
     // linear cell index (a step adds the stepped axis's stride, dda_step)
     uint32_t cell = FLAT ? uint32_t(cz) * n0 + uint32_t(cx) : (uint32_t(cz) * n1 + uint32_t(cy)) * n0 + uint32_t(cx);
+#if RT_GRID_SINGLE
+    // Single-loop form (A/B): every iteration a lane either tests its next
+    // reference or, its cell done, takes its DDA step and fetches the next cell's run, so a wave
+    // iterates max over lanes of (references + cells) instead of the sum over cells of the per-cell
+    // maxima. Per lane the cells, the references and their order are the nested form's: bit-exact.
+    uint32_t j, e;
+    {
+        const uint32_t* cp = cstart + cell;
+        j = PAIRS ? cp[0] : cstart[cell];
+        e = PAIRS ? cp[1] : cstart[cell + 1];
+        if (COUNT) {
+            n_cell++;
+            n_empty += j == e ? 1u : 0u;
+        }
+    }
+    for (;;) {
+        if (j < e) {
+            UTIL(1, true);
+            const float4 s0 = rec[j];
+            const uint32_t i0 = ids[j];
+            test1<true>(s0, [&] { return i0; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
+            if (COUNT) n_sph++;
+            ++j;
+            continue;
+        }
+        UTIL(0, true);
+        const float tm = fminf(fminf(tx, ty), tz);
+        if (!(tm <= r.limit)) break;
+        if (FLAT) {
+            if (!dda_step_xz(tm, tx, ty, tz, cx, cz, sx, sz, cell, r.o, r.inv)) break;
+        } else if (!dda_step(tm, tx, ty, tz, cx, cy, cz, sx, sy, sz, cell, r.o, r.inv)) {
+            break;
+        }
+        const uint32_t* cp = cstart + cell;
+        j = PAIRS ? cp[0] : cstart[cell];
+        e = PAIRS ? cp[1] : cstart[cell + 1];
+        if (COUNT) {
+            n_cell++;
+            n_empty += j == e ? 1u : 0u;
+        }
+    }
+    return;
+#endif
     for (;;) {
         // the cell's reference run [b, e): from L2 through one address, so both offsets come in one
         // 8-byte load (config 5 -1.0 %); the LDS pair is one ds_read2 either way
