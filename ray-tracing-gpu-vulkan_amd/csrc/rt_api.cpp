@@ -1245,8 +1245,13 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
             ctx->fixed = nullptr;
             ctx->fixed_cap = 0;
             void* p = nullptr;
-            RT_HIP(hipMalloc(&p, texels * 3 * sizeof(unsigned long long)));
-            RT_HIP(hipMemsetAsync(p, 0, texels * 3 * sizeof(unsigned long long), st));
+#if RT_FIXED_AOS
+            constexpr size_t kPlanes = 4;   // A/B: texel-major, one 32-byte sector per texel
+#else
+            constexpr size_t kPlanes = 3;
+#endif
+            RT_HIP(hipMalloc(&p, texels * kPlanes * sizeof(unsigned long long)));
+            RT_HIP(hipMemsetAsync(p, 0, texels * kPlanes * sizeof(unsigned long long), st));
             ctx->fixed = static_cast<unsigned long long*>(p);
             ctx->fixed_cap = texels;
         }

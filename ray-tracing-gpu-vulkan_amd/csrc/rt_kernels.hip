@@ -438,10 +438,18 @@ __device__ __forceinline__ uint32_t sample_fixed(float c) {
 __device__ __forceinline__ void add_fixed(const rt::TraceParams& P, const Path& ps, unsigned long long x,
                                           unsigned long long y, unsigned long long z) {
     const uint32_t lx = ps.px & 0xffffu, ly = ps.px >> 16;
-    const size_t n = size_t(P.band_w) * P.band_h, texel = size_t(ly) * P.band_w + lx;
+    const size_t texel = size_t(ly) * P.band_w + lx;
+#if RT_FIXED_AOS   // A/B: a texel's three sums in one 32-byte sector
+    unsigned long long* q = P.fixed + 4 * texel;
+    __hip_atomic_fetch_add(q, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(q + 1, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(q + 2, z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    const size_t n = size_t(P.band_w) * P.band_h;
     __hip_atomic_fetch_add(P.fixed + texel, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_fetch_add(P.fixed + n + texel, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_fetch_add(P.fixed + 2 * n + texel, z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
 }
 
 // Per-lane 64-bit unit sums in LDS (LSUM kernels: the grid kernels, whose LDS has room for them,
@@ -2112,10 +2120,15 @@ __global__ __launch_bounds__(256) void rt_resolve_fixed_kernel(unsigned long lon
                                                                float4* __restrict__ accum,
                                                                uint32_t* __restrict__ out) {
     for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
+#if RT_FIXED_AOS
+        const unsigned long long q0 = fixed[4 * i], q1 = fixed[4 * i + 1], q2 = fixed[4 * i + 2];
+        fixed[4 * i] = fixed[4 * i + 1] = fixed[4 * i + 2] = 0ull;
+#else
         const unsigned long long q0 = fixed[i], q1 = fixed[n + i], q2 = fixed[2 * n + i];
         fixed[i] = 0ull;
         fixed[n + i] = 0ull;
         fixed[2 * n + i] = 0ull;
+#endif
         const float4 a = accumulate ? accum[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         const float s0 = float(double(a.x) + double(q0) * 0x1p-24);
         const float s1 = float(double(a.y) + double(q1) * 0x1p-24);
