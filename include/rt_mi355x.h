@@ -215,6 +215,7 @@ int rt_gather_rows(rt_context* ctx, const float* src_accum, const uint32_t* rows
 /*
  * Tonemap a summed accumulator to rgba8 on the device, exactly as the trace kernel's store
  * (shader.rgen:65-66): rgba8 = round(clamp(sqrt(sum / spp), 0, 1) * 255) per channel, alpha 255.
+ * spp 0 is accepted and gives the bytes the trace kernel stores for a 0-sample frame.
  * accum_rgba32f: n_texels float4 (DEVICE); out_rgba8: n_texels x 4 bytes (DEVICE).
  */
 int rt_resolve_rgba8(rt_context* ctx, const float* accum_rgba32f, uint64_t n_texels, uint32_t spp,
@@ -298,7 +299,9 @@ int rt_partition_rebalance(uint32_t n_devices, uint32_t height, uint32_t* rows, 
 /*
  * One frame over the full image rci[0].image_size with host buffers. rci_count bands, band i
  * spanning rows [rci[i].offset.y, rci[i+1].offset.y) (last band to image height), band i on
- * device i % device_count, gathered to device 0 by RCCL (rt_multi), then copied to the host.
+ * device i % device_count, gathered to device 0 by RCCL (rt_multi), then copied to the host. Each
+ * band renders and is tonemapped with its own RenderCallInfo (its own samplesPerRenderCall, as the
+ * reference fills one per GPU, src/ray_trace.cpp:660-676).
  * accum_rgba32f: W*H*4 floats (read first when opt->accumulate), out_rgba8: W*H*4 bytes.
  */
 int rt_render(const Sphere* spheres, uint32_t sphere_count, const RenderCallInfo* rci,

@@ -1264,6 +1264,8 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
             n_empty += j == e ? 1u : 0u;
         }
     }
+    // One back edge: both paths meet at one latch (an inline-asm marker keeps the compiler from
+    // folding it into them; with a back edge per path LLVM splits the loop into the nested form).
     for (;;) {
         if (j < e) {
             UTIL(1, true);
@@ -1272,23 +1274,24 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
             test1<true>(s0, [&] { return i0; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
             if (COUNT) n_sph++;
             ++j;
-            continue;
+        } else {
+            UTIL(0, true);
+            const float tm = fminf(fminf(tx, ty), tz);
+            if (!(tm <= r.limit)) break;
+            if (FLAT) {
+                if (!dda_step_xz(tm, tx, ty, tz, cx, cz, sx, sz, cell, r.o, r.inv)) break;
+            } else if (!dda_step(tm, tx, ty, tz, cx, cy, cz, sx, sy, sz, cell, r.o, r.inv)) {
+                break;
+            }
+            const uint32_t* cp = cstart + cell;
+            j = PAIRS ? cp[0] : cstart[cell];
+            e = PAIRS ? cp[1] : cstart[cell + 1];
+            if (COUNT) {
+                n_cell++;
+                n_empty += j == e ? 1u : 0u;
+            }
         }
-        UTIL(0, true);
-        const float tm = fminf(fminf(tx, ty), tz);
-        if (!(tm <= r.limit)) break;
-        if (FLAT) {
-            if (!dda_step_xz(tm, tx, ty, tz, cx, cz, sx, sz, cell, r.o, r.inv)) break;
-        } else if (!dda_step(tm, tx, ty, tz, cx, cy, cz, sx, sy, sz, cell, r.o, r.inv)) {
-            break;
-        }
-        const uint32_t* cp = cstart + cell;
-        j = PAIRS ? cp[0] : cstart[cell];
-        e = PAIRS ? cp[1] : cstart[cell + 1];
-        if (COUNT) {
-            n_cell++;
-            n_empty += j == e ? 1u : 0u;
-        }
+        asm volatile("; grid_walk single-loop latch" ::: "memory");
     }
     return;
 #endif
