@@ -1213,10 +1213,14 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     uint64_t chunks = 1;
     bool chunks_forced = false;
     if (mode == rt::MODE_HASH && spp > 1) {
-        // units of >= 128 samples (256 until round 5): a band of the N = 8 frame (136 rows at
-        // 10 000 spp) is capped by this floor, not by the lanes, and its 256-sample tail units
-        // left a tail after the queue ran dry of 4.9 % of the band
-        uint64_t per_lane = 128, min_samples = 128;
+        // units of >= spp / 32 samples, between 32 and 128 (256 until round 5; 128 for every spp
+        // until round 6): a band of the N = 8 frame (135 rows at 10 000 spp) is capped by this
+        // floor, not by the lanes, and its 256-sample tail units left a tail after the queue ran
+        // dry of 4.9 % of the band; config 5's 270-row band at 1 000 spp had 7
+        // chunks of 143 samples under the 128 floor, a 6-7 ms tail of a 68 ms band: 15 chunks
+        // (32-sample floor) -1.1 / -2.0 % on two bands, configs 3 / 4 unchanged (10 000 / 32 >
+        // 128; profiles/r06d_tune2_*.txt)
+        uint64_t per_lane = 128, min_samples = std::min<uint64_t>(128, std::max<uint64_t>(32, spp / 32));
         if (accel == rt::ACCEL_BRUTE) min_samples = std::min<uint64_t>(256, std::max<uint64_t>(4, 2560 / std::max(1u, d.n_spheres)));
         per_lane = std::max<uint64_t>(1, uint64_t(Tuning::get(ctx->tune.units_per_lane, double(per_lane))));
         min_samples = std::max<uint64_t>(1, uint64_t(Tuning::get(ctx->tune.unit_min_samples, double(min_samples))));
@@ -1245,11 +1249,7 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
             ctx->fixed = nullptr;
             ctx->fixed_cap = 0;
             void* p = nullptr;
-#if RT_FIXED_AOS
-            constexpr size_t kPlanes = 4;   // A/B: texel-major, one 32-byte sector per texel
-#else
-            constexpr size_t kPlanes = 3;
-#endif
+            constexpr size_t kPlanes = 3;   // (texel-major, one 32-B sector per texel: +22 % WRITE_SIZE)
             RT_HIP(hipMalloc(&p, texels * kPlanes * sizeof(unsigned long long)));
             RT_HIP(hipMemsetAsync(p, 0, texels * kPlanes * sizeof(unsigned long long), st));
             ctx->fixed = static_cast<unsigned long long*>(p);

@@ -438,18 +438,10 @@ __device__ __forceinline__ uint32_t sample_fixed(float c) {
 __device__ __forceinline__ void add_fixed(const rt::TraceParams& P, const Path& ps, unsigned long long x,
                                           unsigned long long y, unsigned long long z) {
     const uint32_t lx = ps.px & 0xffffu, ly = ps.px >> 16;
-    const size_t texel = size_t(ly) * P.band_w + lx;
-#if RT_FIXED_AOS   // A/B: a texel's three sums in one 32-byte sector
-    unsigned long long* q = P.fixed + 4 * texel;
-    __hip_atomic_fetch_add(q, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(q + 1, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(q + 2, z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-    const size_t n = size_t(P.band_w) * P.band_h;
+    const size_t n = size_t(P.band_w) * P.band_h, texel = size_t(ly) * P.band_w + lx;
     __hip_atomic_fetch_add(P.fixed + texel, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_fetch_add(P.fixed + n + texel, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_fetch_add(P.fixed + 2 * n + texel, z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
 }
 
 // Per-lane 64-bit unit sums in LDS (LSUM kernels: the grid kernels, whose LDS has room for them,
@@ -1249,52 +1241,6 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
     float tz = bound_t(cz, sz, 2, r.o.z, r.inv.z);
     // linear cell index (a step adds the stepped axis's stride, dda_step)
     uint32_t cell = FLAT ? uint32_t(cz) * n0 + uint32_t(cx) : (uint32_t(cz) * n1 + uint32_t(cy)) * n0 + uint32_t(cx);
-#if RT_GRID_SINGLE
-    // Single-loop form (A/B): every iteration a lane either tests its next
-    // reference or, its cell done, takes its DDA step and fetches the next cell's run, so a wave
-    // iterates max over lanes of (references + cells) instead of the sum over cells of the per-cell
-    // maxima. Per lane the cells, the references and their order are the nested form's: bit-exact.
-    uint32_t j, e;
-    {
-        const uint32_t* cp = cstart + cell;
-        j = PAIRS ? cp[0] : cstart[cell];
-        e = PAIRS ? cp[1] : cstart[cell + 1];
-        if (COUNT) {
-            n_cell++;
-            n_empty += j == e ? 1u : 0u;
-        }
-    }
-    // One back edge: both paths meet at one latch (an inline-asm marker keeps the compiler from
-    // folding it into them; with a back edge per path LLVM splits the loop into the nested form).
-    for (;;) {
-        if (j < e) {
-            UTIL(1, true);
-            const float4 s0 = rec[j];
-            const uint32_t i0 = ids[j];
-            test1<true>(s0, [&] { return i0; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
-            if (COUNT) n_sph++;
-            ++j;
-        } else {
-            UTIL(0, true);
-            const float tm = fminf(fminf(tx, ty), tz);
-            if (!(tm <= r.limit)) break;
-            if (FLAT) {
-                if (!dda_step_xz(tm, tx, ty, tz, cx, cz, sx, sz, cell, r.o, r.inv)) break;
-            } else if (!dda_step(tm, tx, ty, tz, cx, cy, cz, sx, sy, sz, cell, r.o, r.inv)) {
-                break;
-            }
-            const uint32_t* cp = cstart + cell;
-            j = PAIRS ? cp[0] : cstart[cell];
-            e = PAIRS ? cp[1] : cstart[cell + 1];
-            if (COUNT) {
-                n_cell++;
-                n_empty += j == e ? 1u : 0u;
-            }
-        }
-        asm volatile("; grid_walk single-loop latch" ::: "memory");
-    }
-    return;
-#endif
     for (;;) {
         // the cell's reference run [b, e): from L2 through one address, so both offsets come in one
         // 8-byte load (config 5 -1.0 %); the LDS pair is one ds_read2 either way
@@ -2123,15 +2069,10 @@ __global__ __launch_bounds__(256) void rt_resolve_fixed_kernel(unsigned long lon
                                                                float4* __restrict__ accum,
                                                                uint32_t* __restrict__ out) {
     for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
-#if RT_FIXED_AOS
-        const unsigned long long q0 = fixed[4 * i], q1 = fixed[4 * i + 1], q2 = fixed[4 * i + 2];
-        fixed[4 * i] = fixed[4 * i + 1] = fixed[4 * i + 2] = 0ull;
-#else
         const unsigned long long q0 = fixed[i], q1 = fixed[n + i], q2 = fixed[2 * n + i];
         fixed[i] = 0ull;
         fixed[n + i] = 0ull;
         fixed[2 * n + i] = 0ull;
-#endif
         const float4 a = accumulate ? accum[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         const float s0 = float(double(a.x) + double(q0) * 0x1p-24);
         const float s1 = float(double(a.y) + double(q1) * 0x1p-24);
