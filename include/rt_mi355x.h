@@ -286,9 +286,10 @@ int rt_partition_strips(uint32_t n_devices, uint32_t height, uint32_t* rows, uin
  * row_cost (height doubles, ms per row; <= 0: unknown, in / out) is rescaled so that each measured
  * device's rows sum to its time (unknown rows at the mean of its known ones). Then rows / counts
  * (the current partition, in / out) are re-dealt: while the most loaded device is above
- * (1 + tolerance) x the mean load, one of its last min(8, rows) band rows moves to the end of the
- * least loaded device's band, the row that leaves the pair most even, as long as that lowers the
- * pair's larger load. Deterministic: every rank of a one-process-per-GPU job that calls it with
+ * (1 + tolerance) x the mean load, one of its last min(8, rows) band rows moves to the end of
+ * another device's band, or is swapped with one of that band's last rows, whichever exchange
+ * leaves the pair's larger load lowest, as long as it lowers the most loaded device's load by
+ * more than tolerance x the mean. Deterministic: every rank of a one-process-per-GPU job that calls it with
  * the same inputs gets the same partition. *moved = rows moved; *predicted_imbalance = max / mean
  * load afterwards (either may be NULL). */
 int rt_partition_rebalance(uint32_t n_devices, uint32_t height, uint32_t* rows, uint32_t* counts, double* row_cost,

@@ -83,8 +83,8 @@ int rt_debug_tile_cost(rt_context* ctx, uint32_t* out, uint64_t capacity, uint64
 int rt_debug_scene(rt_context* ctx, uint32_t what, void* out, uint64_t capacity, uint64_t* bytes);
 
 /*
- * The multi-device frame plan rt_multi_render (band_starts NULL: 8-row strips dealt round robin
- * over n_devices) or rt_render (band i = rows [band_starts[i], band_starts[i+1]) on device
+ * The multi-device frame plan rt_multi_render (band_starts NULL: its first frame's row-exact strips,
+ * rt_partition_strips) or rt_render (band i = rows [band_starts[i], band_starts[i+1]) on device
  * i % n_devices) executes for a width x height frame, with or without accumulation. Host only (no
  * device needed). Flat u32 form: {n_parts, n_steps}, per part {device, whole, n_rows, rows...},
  * per step {op, device, peer, part, flags, count low, count high}; ops 1 load rows (device 0:
@@ -108,8 +108,10 @@ int rt_debug_multi_plan_rows(uint32_t n_devices, uint32_t width, uint32_t height
  * No communicator (rt_multi_info reports 0 ranks). */
 int rt_debug_multi_create_logical(uint32_t n_devices, rt_multi** out);
 /* The balancer of m's strip frames: "balance" (1 on, 0 off), "tolerance" (re-deal above
- * (1 + tolerance) x the mean device time; default 0.0005), "lag" (frames between the measured frame
- * and the one it re-deals; default 2); -1 restores the default. */
+ * (1 + tolerance) x the mean device time, by exchanges that gain more than tolerance x the mean;
+ * default 0.001), "blend" (weight of a new measurement in the per-row estimates; default 0.5),
+ * "lag" (frames between the measured frame and the one it re-deals; default 2); -1 restores the
+ * default. */
 int rt_debug_multi_tune(rt_multi* m, const char* key, double value);
 /* Feeds n device times (ms) as if measured on the current partition: the next rt_multi_render
  * re-deals from them instead of its own measurement (tests: forced re-deals). */

@@ -103,7 +103,8 @@ struct rt_multi {
     FramePlan plan[2];                   // steps without / with accumulation
     struct Balancer {
         bool enabled = true;
-        double tolerance = 0.0005;       // re-deal when the slowest device is above (1 + tol) x mean
+        double tolerance = 0.001;        // re-deal when the slowest device is above (1 + tol) x mean
+        double blend = 0.5;              // weight of a new measurement in the per-row estimates
         uint32_t lag = 2;                // frames between a measured frame and the frame it re-deals
         std::vector<double> cost;        // per global row, ms
         std::deque<FrameRecord> history; // strip frames rendered since the partition was set up
@@ -281,7 +282,7 @@ int balance_step(rt_multi* m) {
             rt::g_last_error = keep;
         }
     }
-    update_costs(measured, ms.data(), b.cost, weights.empty() ? nullptr : &weights);
+    update_costs(measured, ms.data(), b.cost, weights.empty() ? nullptr : &weights, b.blend);
     Parts next = current_parts(m);
     std::vector<double> loads;
     const uint32_t moved = rebalance(next, b.cost, b.tolerance, &loads);
@@ -593,7 +594,8 @@ int rt_debug_multi_tune(rt_multi* m, const char* key, double value) {
     if (!m || !key) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     const std::string k = key;
     if (k == "balance") m->bal.enabled = value < 0 ? true : value != 0.0;
-    else if (k == "tolerance") m->bal.tolerance = value < 0 ? 0.0005 : value;
+    else if (k == "tolerance") m->bal.tolerance = value < 0 ? 0.001 : value;
+    else if (k == "blend") m->bal.blend = value < 0 ? 0.5 : std::min(1.0, value);
     else if (k == "lag") m->bal.lag = value < 0 ? 2u : std::max<uint32_t>(1, uint32_t(value));
     else return fail(RT_ERR_INVALID_ARGUMENT, "unknown key " + k);
     return RT_OK;

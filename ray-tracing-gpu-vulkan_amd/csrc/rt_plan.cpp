@@ -125,7 +125,9 @@ std::vector<uint32_t> serialize(const FramePlan& p) {
 }
 
 void update_costs(const Parts& measured, const float* device_ms, std::vector<double>& cost,
-                  const std::vector<std::vector<double>>* weights) {
+                  const std::vector<std::vector<double>>* weights, double blend) {
+    const double keep = blend >= 1.0 || !(blend > 0.0) ? 0.0 : 1.0 - blend;
+    auto set = [&](uint32_t y, double v) { cost[y] = cost[y] > 0.0 && keep > 0.0 ? keep * cost[y] + (1.0 - keep) * v : v; };
     for (size_t i = 0; i < measured.size(); i++) {
         const std::vector<uint32_t>& rows = measured[i].second;
         const double t = double(device_ms[i]);
@@ -141,8 +143,7 @@ void update_costs(const Parts& measured, const float* device_ms, std::vector<dou
                 double sf = 0.0;
                 for (double v : w) sf += std::max(floor_w, std::isfinite(v) ? v : 0.0);
                 for (size_t k = 0; k < rows.size(); k++)
-                    if (rows[k] < cost.size())
-                        cost[rows[k]] = t * std::max(floor_w, std::isfinite(w[k]) ? w[k] : 0.0) / sf;
+                    if (rows[k] < cost.size()) set(rows[k], t * std::max(floor_w, std::isfinite(w[k]) ? w[k] : 0.0) / sf);
                 continue;
             }
         }
@@ -157,7 +158,7 @@ void update_costs(const Parts& measured, const float* device_ms, std::vector<dou
         const double fill = n_known ? known / double(n_known) : 1.0;
         const double est = known + fill * double(rows.size() - n_known);
         const double scale = t / est;
-        for (uint32_t y : rows) {
+        for (uint32_t y : rows) {   // (the time alone: the rescale is the estimate, no average)
             if (y >= cost.size()) continue;
             cost[y] = (cost[y] > 0.0 ? cost[y] : fill) * scale;
         }
@@ -203,7 +204,7 @@ uint32_t rebalance(Parts& parts, const std::vector<double>& cost, double toleran
             std::vector<uint32_t>& src = parts[hi].second;
             // the exchange with any other device that leaves the larger of the pair's loads lowest
             size_t best_j = np, best_a = 0, best_b = 0;   // best_b == rows of j: a move
-            double best_max = L[hi] * (1.0 - 1e-12);
+            double best_max = L[hi] - std::max(tolerance * mean, L[hi] * 1e-12);
             for (size_t j = 0; j < np; j++) {
                 if (j == hi) continue;
                 const std::vector<uint32_t>& dst = parts[j].second;

@@ -79,17 +79,20 @@ std::vector<uint32_t> serialize(const FramePlan& p);
 // (per part, one per band row of the measured frame, e.g. rt_launch_row_weights; an empty or
 // all-zero vector: none), a measured part's rows get its time split in proportion to them.
 // Without, they are rescaled so that they sum to its time, a row never measured taking the mean
-// of its part's known rows (all unknown: the time spread evenly).
+// of its part's known rows (all unknown: the time spread evenly). blend < 1: a known row keeps
+// (1 - blend) of its previous estimate (an exponential average over frames: per-frame kernel times
+// vary by a few tenths of a percent, which a re-deal should not chase).
 void update_costs(const Parts& measured, const float* device_ms, std::vector<double>& cost,
-                  const std::vector<std::vector<double>>* weights = nullptr);
+                  const std::vector<std::vector<double>>* weights = nullptr, double blend = 1.0);
 
 // While the most loaded device is more than (1 + tolerance) x the mean load, applies the exchange
 // with another device that leaves the larger of the pair's loads lowest, if it is below the most
 // loaded device's load (so every step lowers the sum of squared loads): a MOVE
 // of one of the donor's last min(8, rows) band rows (its last tile row, so the band's other tiles
 // keep their index and their LPT cost record) to the end of the receiver's band, or a SWAP of one
-// such row with one of the receiver's last rows (finer than one row). Deterministic (ties to the
-// lowest index). Returns the rows moved (a swap moves two); loads_out (optional, per part)
+// such row with one of the receiver's last rows (finer than one row), when it lowers the most
+// loaded device's load by more than tolerance x the mean load. Deterministic (ties to the lowest
+// index). Returns the rows moved (a swap moves two); loads_out (optional, per part)
 // receives the predicted loads afterwards.
 uint32_t rebalance(Parts& parts, const std::vector<double>& cost, double tolerance, std::vector<double>* loads_out);
 

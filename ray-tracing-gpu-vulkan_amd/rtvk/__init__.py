@@ -447,7 +447,7 @@ def partition_strips(n_devices: int, height: int) -> list:
 
 
 def partition_rebalance(parts: Sequence, cost: np.ndarray, measured: Optional[Sequence] = None,
-                        device_ms: Optional[Sequence[float]] = None, tolerance: float = 0.0005) -> tuple:
+                        device_ms: Optional[Sequence[float]] = None, tolerance: float = 0.001) -> tuple:
     """One balancing step (rt_partition_rebalance): rescale the per-row costs `cost` (float64 [H],
     <= 0 unknown; updated in place) to the device times `device_ms` measured on partition
     `measured`, then re-deal `parts`. Returns (new parts, rows moved, predicted max / mean)."""

@@ -77,6 +77,18 @@ def row_costs(rows: np.ndarray, ms: float, weights: Optional[np.ndarray]) -> np.
     return np.full(n, ms / n)
 
 
+def blend_costs(old: np.ndarray, new: np.ndarray, blend: float) -> np.ndarray:
+    """Rows measured in `new` (> 0) take blend x the new estimate + (1 - blend) x their previous
+    one (csrc/rt_plan.cpp update_costs): per-frame kernel times vary by a few tenths of a
+    percent, which a re-deal should not chase."""
+    out = old.copy()
+    m = new > 0
+    keep = (old > 0) & m & (blend < 1.0)
+    out[m] = new[m]
+    out[keep] = (1.0 - blend) * old[keep] + blend * new[keep]
+    return out
+
+
 class DistributedRenderer:
     """One rank's share of a multi-GPU frame.
 
@@ -89,13 +101,14 @@ class DistributedRenderer:
     force_gather: run the gather + reassembly even on one rank (tests of the collective path).
     timer(back, band_rows) -> (ms, weights | None): this rank's kernel time of its launch `back`
     launches before its most recent one, and that band's per-row work weights; given, the rows are
-    re-dealt between frames (balance; tolerance / lag as rt_multi's balancer).
+    re-dealt between frames (balance; tolerance / lag / blend as rt_multi's balancer).
     """
 
     def __init__(self, width: int, height: int, device, render_band: Callable,
                  assemble: Optional[Callable] = None, strip: int = STRIP, gather_accum: bool = True,
                  force_gather: bool = False, resolve: Optional[Callable] = None,
-                 timer: Optional[Callable] = None, tolerance: float = 0.0005, lag: int = 2):
+                 timer: Optional[Callable] = None, tolerance: float = 0.001, lag: int = 2,
+                 blend: float = 0.5):
         import torch
         import torch.distributed as dist
         self.torch, self.dist = torch, dist
@@ -114,7 +127,7 @@ class DistributedRenderer:
         self.staged = (self.world > 1 and getattr(device, "type", str(device)) != "cpu"
                        and dist.get_backend() == "gloo")
         self.timer = timer if self.world > 1 else None
-        self.tolerance, self.lag = tolerance, max(1, int(lag))
+        self.tolerance, self.lag, self.blend = tolerance, max(1, int(lag)), blend
         self.cost = np.zeros(height, np.float64)
         self.history = deque()      # per frame: (partition, launch index of this rank or None)
         self.launches = 0           # render_band calls that launched (rows present)
@@ -165,9 +178,7 @@ class DistributedRenderer:
             mine[rows] = row_costs(rows, ms, w)
         t = self.torch.from_numpy(mine)
         self.dist.all_reduce(t, group=self.cpu_group)   # disjoint rows: the sum is every rank's estimate
-        cost = t.numpy()
-        measured = cost > 0
-        self.cost[measured] = cost[measured]
+        self.cost = blend_costs(self.cost, t.numpy(), self.blend)
         from . import partition_rebalance
         parts, moved, pred = partition_rebalance(self.parts, self.cost, tolerance=self.tolerance)
         if moved:

@@ -32,7 +32,7 @@ import torch  # noqa: E402
 
 import rtvk  # noqa: E402
 from rtvk import abi  # noqa: E402
-from rtvk.dist import row_costs  # noqa: E402
+from rtvk.dist import blend_costs, row_costs  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("n", type=int, nargs="?", default=8)
@@ -101,13 +101,15 @@ parts = rtvk.partition_strips(N, H)
 cost = np.zeros(H, np.float64)
 for it in range(args.iters + 1):
     row = {"rows": [], "kernel_ms": [], "step_ms": [], "chunks": []}
+    new = np.zeros(H, np.float64)
     for rk in ranks:
         ms, step, info, w = timed(rk, parts[rk])
         row["rows"].append(int(len(parts[rk])))
         row["kernel_ms"].append(round(ms, 3))
         row["step_ms"].append(round(step, 3))
         row["chunks"].append([info["chunks"], info["head_chunks"]])
-        cost[parts[rk]] = row_costs(parts[rk], ms, w)
+        new[parts[rk]] = row_costs(parts[rk], ms, w)
+    cost = blend_costs(cost, new, 0.5)   # as rtvk.dist / rt_multi between frames
     ks = row["kernel_ms"]
     row["max_ms"] = max(ks)
     row["mean_ms"] = round(sum(ks) / len(ks), 3)

@@ -18,9 +18,9 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 rc=$?; tail -2 gpurun_out/${TAG}_smoke.log; fatal $rc smoke
 fi
 if [ "${SKIP_PROBES:-0}" != 1 ]; then
-timeout -k 10 400 python scripts/band_probe.py 8 10000 --iters 4 --reps 4 --json gpurun_out/${TAG}_band_probe_c3_n8.json > gpurun_out/${TAG}_band_probe_c3_n8.log 2>&1
+timeout -k 10 400 python scripts/band_probe.py 8 10000 --iters 6 --reps 4 --json gpurun_out/${TAG}_band_probe_c3_n8.json > gpurun_out/${TAG}_band_probe_c3_n8.log 2>&1
 rc=$?; tail -c 400 gpurun_out/${TAG}_band_probe_c3_n8.log; fatal $rc band_probe_c3
-timeout -k 10 300 python scripts/band_probe.py 8 1000 --width 3840 --height 2160 --grid 158 --iters 3 --rebuild \
+timeout -k 10 300 python scripts/band_probe.py 8 1000 --width 3840 --height 2160 --grid 158 --iters 5 --reps 3 --rebuild \
     --json gpurun_out/${TAG}_band_probe_c5_n8.json > gpurun_out/${TAG}_band_probe_c5_n8.log 2>&1
 rc=$?; tail -c 400 gpurun_out/${TAG}_band_probe_c5_n8.log; fatal $rc band_probe_c5
 fi
