@@ -193,7 +193,10 @@ int rt_launch_ms(rt_context* ctx, uint32_t back, float* ms);
 /* Per band row of the same launch (one of ctx's last 4 grid / LBVH launches; band_rows = its band
  * height), the row's share of the launch's work as its 8x8 tile-cost record estimates it (each
  * tile's longest unit chain x the sample chunks it ran in, split evenly over the tile's rows; the
- * unit is arbitrary, only ratios matter). Waits for that launch's record copy only. */
+ * unit is arbitrary, only ratios matter). Waits for that launch's record copy only. A context
+ * copies its launches' records (two small device-to-host copies after each kernel) only from the
+ * first call on, so the first call finds none (RT_ERR_INVALID_ARGUMENT); rt_multi's contexts keep
+ * them from the start when it drives more than one device. */
 int rt_launch_row_weights(rt_context* ctx, uint32_t back, double* weights, uint32_t band_rows);
 /*
  * Scatter band rows into a full image on the device: dst_row[rows[i]] = src_row[i]

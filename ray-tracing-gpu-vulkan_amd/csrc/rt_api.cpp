@@ -177,6 +177,8 @@ struct rt_context {
     };
     static constexpr uint32_t kSnaps = 4;
     CostSnap snap[kSnaps];
+    bool keep_snaps = false;   // set by the first rt_launch_row_weights (or rt_multi at N > 1):
+                               // a one-device frame loop pays no copies it never reads
 };
 
 namespace {
@@ -1345,7 +1347,7 @@ int rt_render_device(rt_context* ctx, const RenderCallInfo* rci, const uint32_t*
     ctx->kev_count++;
     if (mode == rt::MODE_HASH)
         RT_HIP(rt::launch_resolve_fixed(ctx->fixed, texels, P.accumulate, spp, accum, out, st));
-    if (P.tile_cost) {   // this launch's record (+ the order it ran in) for rt_launch_row_weights
+    if (P.tile_cost && ctx->keep_snaps) {   // this launch's record (+ its order) for rt_launch_row_weights
         rt_context::CostSnap& sn = ctx->snap[(ctx->kev_count - 1) % rt_context::kSnaps];
         if (sn.pending) RT_HIP(hipEventSynchronize(sn.ev));   // four launches old
         sn.pending = false;
@@ -1564,9 +1566,13 @@ int rt_launch_ms(rt_context* ctx, uint32_t back, float* ms) {
 
 namespace rt {
 uint64_t launch_count(const rt_context* ctx) { return ctx ? ctx->kev_count : 0; }
+void keep_row_weights(rt_context* ctx) {
+    if (ctx) ctx->keep_snaps = true;
+}
 int launch_row_weights(rt_context* ctx, uint64_t index, std::vector<double>& w) {
     w.clear();
     if (!ctx) return fail(RT_ERR_INVALID_ARGUMENT, "ctx is NULL");
+    ctx->keep_snaps = true;   // the launches from now on keep their records
     for (rt_context::CostSnap& sn : ctx->snap) {
         if (sn.launch != index || !sn.pending) continue;
         DeviceGuard g(ctx->device);

@@ -31,7 +31,9 @@ uint64_t launch_count(const rt_context* ctx);
 int launch_ms_at(rt_context* ctx, uint64_t index, float* ms);
 // Per band row of launch `index` (one of the last 4), its share of the launch's work as the
 // tile-cost record estimates it (rt_launch_row_weights); waits for that launch's copy only.
+// Launches keep the record copies only once asked for (keep_row_weights, or the first call).
 int launch_row_weights(rt_context* ctx, uint64_t index, std::vector<double>& w);
+void keep_row_weights(rt_context* ctx);
 
 // Message of the calling thread's last failure (rt_last_error()).
 extern thread_local std::string g_last_error;

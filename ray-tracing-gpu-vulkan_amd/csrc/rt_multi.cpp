@@ -220,6 +220,7 @@ int set_partition(rt_multi* m, const std::string& key, uint32_t W, uint32_t H, P
     }
     for (Launch& l : m->launches) {
         if (int rc = rt_context_create(phys_of(m, l.dev), &l.ctx)) return rc;
+        if (m->launches.size() > 1) rt::keep_row_weights(l.ctx);   // the balancer reads them
         if (int rc = fit_buffers(m, l)) return rc;
     }
     m->key = key;

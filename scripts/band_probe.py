@@ -59,6 +59,10 @@ def ctx(key):
     if key not in ctxs:
         r = rtvk.Renderer(0)
         r.set_scene(scene)
+        try:   # the first call switches the context's tile-cost record copies on (finds none)
+            r.launch_row_weights(1, 0)
+        except rtvk.RtError:
+            pass
         ctxs[key] = r
     return ctxs[key]
 

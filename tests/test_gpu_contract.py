@@ -226,7 +226,7 @@ def test_multi_renderer_reports_communicator(rtvk, torch, oracle):
         info = m.info()
         # one device holds no communicator (its frame plan has no send or receive)
         assert info["devices"] == n and info["rccl_ranks"] == (n if n > 1 else 0) and info["strip_rows"] == 8
-        assert info["launches"] == min(n, (H + 7) // 8)
+        assert info["launches"] == min(n, H)   # row-exact strips: every device holds rows
         kt = m.kernel_times()
         assert len(kt) == info["launches"] and all(k > 0 for k in kt)
         m.render(rtvk.canonical_render_call_info(2, W, H), acc, out, options=rtvk.make_options(rng_mode=HASH))
@@ -236,3 +236,39 @@ def test_multi_renderer_reports_communicator(rtvk, torch, oracle):
         with pytest.raises((TypeError, ValueError)):
             bad = torch.zeros((H, W, 4), dtype=torch.float32, device="cpu")
             m.render(rtvk.canonical_render_call_info(2, W, H), bad, out)
+
+
+def test_launch_time_and_row_weights(rtvk, torch, oracle):
+    """rt_launch_ms / rt_launch_row_weights, the balancer's per-launch readings: the first
+    row-weight call switches the context's tile-cost record copies on (it finds none), later
+    launches keep them; the launch time equals rt_debug_kernel_times' record of the same launch, a
+    launch two back stays readable after newer ones, and the weights cover the band's rows (a tile
+    row's rows share its weight)."""
+    r = rtvk.Renderer(0)
+    try:
+        r.set_scene(oracle.generate_scene())
+        W, H = 64, 45
+        rows = torch.arange(H, dtype=torch.int32, device="cuda").flip(0).contiguous()
+        acc = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+        out = torch.zeros((H, W, 4), dtype=torch.uint8, device="cuda")
+        rci = rtvk.canonical_render_call_info(4, W, H)
+        opt = rtvk.make_options(rng_mode=HASH)
+        with pytest.raises(rtvk.RtError):
+            r.launch_ms(0)   # nothing launched yet
+        r.render_device(rci, acc, out, rows=rows, options=opt)
+        with pytest.raises(rtvk.RtError):
+            r.launch_row_weights(H, 0)   # records were not kept for it: this call switches them on
+        for _ in range(3):
+            r.render_device(rci, acc, out, rows=rows, options=opt)
+        torch.cuda.synchronize()
+        kt = r.kernel_times(3)
+        assert [r.launch_ms(b) for b in (2, 1, 0)] == pytest.approx(kt, rel=1e-6)
+        for back in (0, 1, 2):
+            w = r.launch_row_weights(H, back)
+            assert w.shape == (H,) and np.all(w >= 0) and w.sum() > 0
+            for ty in range(H // 8):   # rows of one 8-row tile row share its weight
+                assert np.all(w[8 * ty: 8 * ty + 8] == w[8 * ty])
+        with pytest.raises(rtvk.RtError):
+            r.launch_row_weights(H + 1, 0)   # not that launch's band height
+    finally:
+        r.close()
