@@ -136,7 +136,15 @@ class DistributedRenderer:
         self.predicted = 1.0
         self.cpu_group = None
         if self.timer is not None and dist.get_backend() != "gloo":
-            self.cpu_group = dist.new_group(backend="gloo")   # the per-row costs travel on the host
+            # the per-row costs travel on the host: a device all-reduce would queue behind the
+            # frame's persistent kernel and stall the host for it. Without a gloo group (it is a
+            # collective call, so every rank sees the same outcome) the split stays static.
+            try:
+                self.cpu_group = dist.new_group(backend="gloo")
+            except Exception as e:  # noqa: BLE001
+                import sys
+                print(f"rtvk.dist: no gloo group ({e}); row split static", file=sys.stderr)
+                self.timer = None
         self.cap = 0
         self._set_parts([strip_rows(r, self.world, height, strip) for r in range(self.world)])
 
