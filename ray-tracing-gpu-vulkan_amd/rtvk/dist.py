@@ -126,7 +126,7 @@ class DistributedRenderer:
         # multi-rank path on a shared GPU; RCCL gathers device memory directly).
         self.staged = (self.world > 1 and getattr(device, "type", str(device)) != "cpu"
                        and dist.get_backend() == "gloo")
-        self.timer = timer if self.world > 1 else None
+        self.timer = timer if self.multi else None   # (one rank + force_gather: the exchange path runs, no move)
         self.tolerance, self.lag, self.blend = tolerance, max(1, int(lag)), blend
         self.cost = np.zeros(height, np.float64)
         self.history = deque()      # per frame: (partition, launch index of this rank or None)

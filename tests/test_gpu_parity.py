@@ -956,11 +956,12 @@ def test_scene_swap_between_queued_frames(rtvk, renderer, torch, oracle):
 def test_strips_rccl_world1(rtvk, renderer, torch, oracle, rng_mode, resolve):
     """bench.py's N > 1 path (rtvk.dist.DistributedRenderer: row strips per rank, torch.distributed
     gathers over RCCL, rt_scatter_rows on rank 0, rgba8 resolved from the gathered accumulator by
-    rt_resolve_rgba8 — or both images gathered) on a one-rank NCCL group: the frame equals the
-    one-GPU oracle frame bit for bit."""
+    rt_resolve_rgba8 — or both images gathered — and the balancer's per-frame exchange: the gloo
+    side group beside the NCCL default group, the library's launch timer and row weights) on a
+    one-rank NCCL group: four frames, each equal to the one-GPU oracle frame bit for bit."""
     import socket
     import torch.distributed as dist
-    from rtvk.dist import DistributedRenderer, hip_assembler, hip_band_renderer, hip_resolver
+    from rtvk.dist import DistributedRenderer, hip_assembler, hip_band_renderer, hip_band_timer, hip_resolver
     W, H, spp = 80, 48, 3
     sc = oracle.generate_scene()
     renderer.set_scene(sc)
@@ -974,13 +975,20 @@ def test_strips_rccl_world1(rtvk, renderer, torch, oracle, rng_mode, resolve):
         dr = DistributedRenderer(W, H, torch.device("cuda", 0),
                                  hip_band_renderer(renderer, rci, rtvk.make_options(rng_mode=rng_mode)),
                                  hip_assembler(renderer), force_gather=True,
-                                 resolve=hip_resolver(renderer, spp) if resolve else None)
-        acc, out = dr.step()
-        torch.cuda.synchronize()
+                                 resolve=hip_resolver(renderer, spp) if resolve else None,
+                                 timer=hip_band_timer(renderer))
+        assert dr.cpu_group is not None and dr.timer is not None
+        frames = []
+        for _ in range(4):
+            acc, out = dr.step()
+            torch.cuda.synchronize()
+            frames.append((acc.cpu().numpy(), out.cpu().numpy()))
+        assert dr.rows_per_rank() == [H] and dr.cost.sum() > 0   # measured, nothing to move at one rank
     finally:
         dist.destroy_process_group()
     ra, ro, _ = oracle.render(sc, oracle.render_call_info(spp, W, H), W, H, opts=oracle.options(rng_mode=rng_mode))
-    assert_same(acc.cpu().numpy(), out.cpu().numpy(), ra, ro)
+    for acc, out in frames:
+        assert_same(acc, out, ra, ro)
 
 
 @pytest.mark.parametrize("isolate", ["0", "3", "1000000"])
