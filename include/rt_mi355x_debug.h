@@ -107,6 +107,12 @@ int rt_debug_multi_plan_rows(uint32_t n_devices, uint32_t width, uint32_t height
  * after the sender's earlier work and before its later work (the group boundaries of the plan).
  * No communicator (rt_multi_info reports 0 ranks). */
 int rt_debug_multi_create_logical(uint32_t n_devices, rt_multi** out);
+/* The same logical devices with the transfers through RCCL itself: one communicator of one rank on
+ * device 0 (ncclCommInitAll), every group's sends and receives issued as ncclSend / ncclRecv of
+ * rank 0 to itself on logical device 0's stream (fenced by events against every logical device's
+ * stream before and after the group), so the one-GPU pool runs rt_multi's RCCL branch: the
+ * communicator, the grouped calls and their buffers (rt_multi_info reports 1 rank). */
+int rt_debug_multi_create_logical_rccl(uint32_t n_devices, rt_multi** out);
 /* The balancer of m's strip frames: "balance" (1 on, 0 off), "tolerance" (re-deal above
  * (1 + tolerance) x the mean device time, by exchanges that gain more than tolerance x the mean;
  * default 0.001), "blend" (weight of a new measurement in the per-row estimates; default 0.5),

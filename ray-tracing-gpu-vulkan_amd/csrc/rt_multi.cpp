@@ -89,7 +89,9 @@ struct FrameRecord {
 struct rt_multi {
     uint32_t n = 0;
     std::vector<int> phys;               // HIP device of each logical device
-    bool logical = false;                // N logical devices on GPU 0: no communicator, device copies
+    bool logical = false;                // N logical devices on GPU 0 (tests on a one-GPU box)
+    bool self_rccl = false;              // logical: the transfers through a one-rank communicator
+                                         // (ncclSend / ncclRecv to itself on stream[0]); else copies
     std::vector<hipStream_t> stream;     // one per logical device
     std::vector<ncclComm_t> comm;        // one per device, rank = device index
     hipEvent_t ev_in = nullptr, ev_out = nullptr;   // device 0: caller stream <-> stream[0]
@@ -346,6 +348,28 @@ int resolve_all(rt_multi* m, rt_context* c0, const RenderCallInfo* rcis, size_t 
     return RT_OK;
 }
 
+// self_rccl groups run on stream[0]: before a group it waits for every logical device's stream,
+// after it every stream waits for it (what the per-device streams of real ranks get from RCCL).
+int self_group_fence(rt_multi* m, bool before) {
+    while (m->xev.size() < m->n) {
+        hipEvent_t e = nullptr;
+        DeviceGuard g(phys_of(m, 0));
+        RT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        m->xev.push_back(e);
+    }
+    DeviceGuard g(phys_of(m, 0));
+    if (before) {
+        for (uint32_t d = 1; d < m->n; d++) {
+            RT_HIP(hipEventRecord(m->xev[d], m->stream[d]));
+            RT_HIP(hipStreamWaitEvent(m->stream[0], m->xev[d], 0));
+        }
+    } else {
+        RT_HIP(hipEventRecord(m->xev[0], m->stream[0]));
+        for (uint32_t d = 1; d < m->n; d++) RT_HIP(hipStreamWaitEvent(m->stream[d], m->xev[0], 0));
+    }
+    return RT_OK;
+}
+
 // A context on device 0 (the row loads / stores and the resolve run on stream[0]).
 rt_context* root_ctx(rt_multi* m) {
     for (Launch& l : m->launches)
@@ -370,29 +394,40 @@ int run_plan(rt_multi* m, const FramePlan& p, const RenderCallInfo* rcis, size_t
             const uint32_t nr = uint32_t(l.rows.size());
             switch (s.op) {
                 case OP_GROUP_START:
-                    if (!m->logical) RT_NCCL(ncclGroupStart());
+                    if (m->self_rccl) {   // stream[0] carries the group: after every device's work so far
+                        if (int rc = self_group_fence(m, true)) return rc;
+                    }
+                    if (!m->logical || m->self_rccl) RT_NCCL(ncclGroupStart());
                     group.clear();
                     in_group = true;
                     break;
                 case OP_GROUP_END:
                     in_group = false;
-                    if (m->logical) {
+                    if (m->logical && !m->self_rccl) {
                         if (int rc = logical_transfers(m, group)) return rc;
                     } else {
                         RT_NCCL(ncclGroupEnd());
+                        if (m->self_rccl) {   // every device's later work after the group
+                            if (int rc = self_group_fence(m, false)) return rc;
+                        }
                     }
                     break;
                 case OP_SEND:
                 case OP_RECV: {
-                    if (m->logical) {
+                    if (m->logical && !m->self_rccl) {
                         group.push_back(s);
                         break;
                     }
-                    DeviceGuard g(phys_of(m, s.dev));
+                    // a one-rank communicator (self_rccl): every transfer is rank 0 to itself on
+                    // stream[0]; the k-th send and the k-th receive of a group pair up, as the plan
+                    // orders them (each send beside its receive)
+                    const uint32_t rank_dev = m->self_rccl ? 0u : s.dev;
+                    const int peer = m->self_rccl ? 0 : int(s.peer);
+                    DeviceGuard g(phys_of(m, rank_dev));
                     const ncclResult_t e =
                         s.op == OP_SEND
-                            ? ncclSend(dev_buf, s.count, ncclFloat32, int(s.peer), m->comm[s.dev], m->stream[s.dev])
-                            : ncclRecv(dev_buf, s.count, ncclFloat32, int(s.peer), m->comm[s.dev], m->stream[s.dev]);
+                            ? ncclSend(dev_buf, s.count, ncclFloat32, peer, m->comm[rank_dev], m->stream[rank_dev])
+                            : ncclRecv(dev_buf, s.count, ncclFloat32, peer, m->comm[rank_dev], m->stream[rank_dev]);
                     if (e != ncclSuccess) return fail(RT_ERR_DEVICE, std::string("RCCL: ") + ncclGetErrorString(e));
                     break;
                 }
@@ -423,7 +458,7 @@ int run_plan(rt_multi* m, const FramePlan& p, const RenderCallInfo* rcis, size_t
         return RT_OK;
     };
     const int rc = body();
-    if (in_group && !m->logical) (void)ncclGroupEnd();   // a failure inside a group still closes it
+    if (in_group && (!m->logical || m->self_rccl)) (void)ncclGroupEnd();   // a failure inside a group still closes it
     return rc;
 }
 
@@ -435,7 +470,7 @@ int copy_plan(std::vector<uint32_t>&& v, uint32_t* out, uint64_t capacity, uint6
     return RT_OK;
 }
 
-int create(uint32_t gpu_count, bool logical, rt_multi** out) {
+int create(uint32_t gpu_count, bool logical, bool self_rccl, rt_multi** out) {
     if (!out) return fail(RT_ERR_INVALID_ARGUMENT, "out is NULL");
     *out = nullptr;
     int nd = 0;
@@ -449,6 +484,7 @@ int create(uint32_t gpu_count, bool logical, rt_multi** out) {
     // every failure below releases what was created so far (streams, events, comms)
     auto body = [&]() -> int {
         m->logical = logical;
+        m->self_rccl = logical && self_rccl;
         m->n = logical ? std::max(1u, gpu_count) : std::max(1u, std::min(gpu_count, uint32_t(nd)));
         m->phys.assign(m->n, 0);
         for (uint32_t d = 0; d < m->n; d++) m->phys[d] = logical ? 0 : int(d);
@@ -470,6 +506,9 @@ int create(uint32_t gpu_count, bool logical, rt_multi** out) {
             std::vector<int> devs(m->n);
             for (uint32_t d = 0; d < m->n; d++) devs[d] = int(d);
             RT_NCCL(ncclCommInitAll(m->comm.data(), int(m->n), devs.data()));
+        } else if (m->self_rccl) {   // one rank on GPU 0 (rank 0 = logical device 0)
+            int dev0 = 0;
+            RT_NCCL(ncclCommInitAll(m->comm.data(), 1, &dev0));
         }
         return RT_OK;
     };
@@ -493,11 +532,16 @@ int create(uint32_t gpu_count, bool logical, rt_multi** out) {
 
 extern "C" {
 
-int rt_multi_create(uint32_t gpu_count, rt_multi** out) { return create(gpu_count, false, out); }
+int rt_multi_create(uint32_t gpu_count, rt_multi** out) { return create(gpu_count, false, false, out); }
 
 int rt_debug_multi_create_logical(uint32_t n_devices, rt_multi** out) {
     if (n_devices == 0 || n_devices > 64) return fail(RT_ERR_INVALID_ARGUMENT, "n_devices must be 1..64");
-    return create(n_devices, true, out);
+    return create(n_devices, true, false, out);
+}
+
+int rt_debug_multi_create_logical_rccl(uint32_t n_devices, rt_multi** out) {
+    if (n_devices == 0 || n_devices > 64) return fail(RT_ERR_INVALID_ARGUMENT, "n_devices must be 1..64");
+    return create(n_devices, true, true, out);
 }
 
 int rt_multi_destroy(rt_multi* m) {
@@ -698,7 +742,7 @@ int rt_partition_rebalance(uint32_t n_devices, uint32_t height, uint32_t* rows, 
 
 int rt_multi_info(const rt_multi* m, uint32_t* out4) {
     if (!m || !out4) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
-    int ranks = 0;   // 0: one device or logical devices, no communicator
+    int ranks = 0;   // 0: one device or logical devices with copies, no communicator
     if (m->comm[0]) RT_NCCL(ncclCommCount(m->comm[0], &ranks));
     uint32_t launches = 0;
     for (const Launch& l : m->launches) launches += l.rows.empty() ? 0u : 1u;

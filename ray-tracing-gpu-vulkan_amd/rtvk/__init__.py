@@ -326,12 +326,15 @@ class MultiRenderer:
     are reordered; the image equals the one-GPU image bit for bit.
 
     logical=True (tests on a one-GPU box): `gpu_count` logical devices on GPU 0 running the same
-    frame plans, each RCCL send / receive pair a device copy (rt_debug_multi_create_logical)."""
+    frame plans, each RCCL send / receive pair a device copy (rt_debug_multi_create_logical), or
+    with logical="rccl" RCCL send / receive of a one-rank communicator to itself
+    (rt_debug_multi_create_logical_rccl)."""
 
-    def __init__(self, gpu_count: int = 1, logical: bool = False):
+    def __init__(self, gpu_count: int = 1, logical=False):
         self._lib = load_library()
         self._m = ctypes.c_void_p()
-        create = self._lib.rt_debug_multi_create_logical if logical else self._lib.rt_multi_create
+        create = (self._lib.rt_debug_multi_create_logical_rccl if logical == "rccl"
+                  else self._lib.rt_debug_multi_create_logical if logical else self._lib.rt_multi_create)
         check(create(gpu_count, ctypes.byref(self._m)))
         n = ctypes.c_uint32()
         check(self._lib.rt_multi_device_count(self._m, ctypes.byref(n)))

@@ -152,6 +152,7 @@ EXPORTS = {
     "rt_debug_multi_plan_rows": (_I, [_U32, _U32, _U32, _P, _P, _U32, _P, ctypes.c_uint64,
                                       ctypes.POINTER(ctypes.c_uint64)]),
     "rt_debug_multi_create_logical": (_I, [_U32, ctypes.POINTER(_P)]),
+    "rt_debug_multi_create_logical_rccl": (_I, [_U32, ctypes.POINTER(_P)]),
     "rt_debug_multi_tune": (_I, [_P, ctypes.c_char_p, ctypes.c_double]),
     "rt_debug_multi_feedback": (_I, [_P, _P, _U32]),
     "rt_debug_multi_balance_info": (_I, [_P, _P]),

@@ -623,6 +623,32 @@ def test_multi_logical_devices(rtvk, torch, logical_refs, n, rng_mode):
         assert_same(acc.cpu().numpy(), out.cpu().numpy(), ra1, ro1)
 
 
+@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("rng_mode", [STREAM, HASH])
+def test_multi_logical_rccl(rtvk, torch, logical_refs, n, rng_mode):
+    """rt_multi's RCCL branch on one GPU (rt_debug_multi_create_logical_rccl): ncclCommInitAll of
+    one rank, every group's accumulator transfers issued as grouped ncclSend / ncclRecv of that rank
+    to itself (the plan's buffers: bands on the logical devices, stages on device 0); a plain and
+    an accumulating frame equal the oracle bit for bit."""
+    sc, rci_np, refs = logical_refs
+    (ra0, ro0, rs0), (ra1, ro1) = refs[rng_mode]
+    rci = rtvk.RenderCallInfo.from_buffer_copy(rci_np.tobytes())
+    with rtvk.MultiRenderer(n, logical="rccl") as m:
+        assert m.device_count == n and m.info()["rccl_ranks"] == 1
+        m.tune(balance=0)
+        m.set_scene(sc)
+        acc = torch.zeros((LOGICAL_H, LOGICAL_W, 4), dtype=torch.float32, device="cuda:0")
+        out = torch.zeros((LOGICAL_H, LOGICAL_W, 4), dtype=torch.uint8, device="cuda:0")
+        m.render(rci, acc, out, options=rtvk.make_options(rng_mode=rng_mode))
+        torch.cuda.synchronize()
+        assert_same(acc.cpu().numpy(), out.cpu().numpy(), ra0, ro0)
+        assert (m.stats().segments, m.stats().samples) == rs0[:2]
+        base = 2 if rng_mode != STREAM else 0
+        m.render(rci, acc, out, options=rtvk.make_options(rng_mode=rng_mode, accumulate=True, sample_base=base))
+        torch.cuda.synchronize()
+        assert_same(acc.cpu().numpy(), out.cpu().numpy(), ra1, ro1)
+
+
 @pytest.mark.parametrize("rng_mode", [STREAM, HASH])
 def test_multi_logical_rebalance(rtvk, torch, logical_refs, rng_mode):
     """The balancer's re-deals on 8 logical devices: device times fed every frame (device 0 and 3
