@@ -277,7 +277,10 @@ int balance_step(rt_multi* m) {
         weights.resize(measured.size());
         for (size_t i = 0; i < measured.size(); i++) {
             if (r.launch[i] == UINT64_MAX) continue;
-            if (int rc = rt::launch_ms_at(m->launches[i].ctx, r.launch[i], &ms[i])) return rc;
+            if (rt::launch_ms_at(m->launches[i].ctx, r.launch[i], &ms[i]) != RT_OK) {
+                rt::g_last_error.clear();   // a reading lost is no frame error: keep the partition
+                return RT_OK;
+            }
             // the launch's per-row work from its tile costs (none kept, e.g. brute force: the
             // device time alone rescales the rows' estimates)
             const std::string keep = rt::g_last_error;
