@@ -1547,6 +1547,7 @@ int rt_debug_kernel_times(rt_context* ctx, float* out_ms, uint32_t capacity, uin
 // frames queued behind it (the cross-device balancer of rt_multi / rtvk.dist).
 int rt_launch_row_weights(rt_context* ctx, uint32_t back, double* weights, uint32_t band_rows) {
     if (!ctx || (!weights && band_rows)) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
+    rt::keep_row_weights(ctx);   // from now on, even when this call finds nothing
     if (back >= ctx->kev_count) return fail(RT_ERR_INVALID_ARGUMENT, "no such launch recorded");
     std::vector<double> w;
     if (int rc = rt::launch_row_weights(ctx, ctx->kev_count - 1 - back, w)) return rc;

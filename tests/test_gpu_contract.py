@@ -258,6 +258,15 @@ def test_launch_time_and_row_weights(rtvk, torch, oracle):
         r.render_device(rci, acc, out, rows=rows, options=opt)
         with pytest.raises(rtvk.RtError):
             r.launch_row_weights(H, 0)   # records were not kept for it: this call switches them on
+        r2 = rtvk.Renderer(0)   # a context asked before its first launch keeps them from that launch on
+        try:
+            r2.set_scene(oracle.generate_scene())
+            with pytest.raises(rtvk.RtError):
+                r2.launch_row_weights(H, 0)
+            r2.render_device(rci, acc, out, rows=rows, options=opt)
+            assert r2.launch_row_weights(H, 0).sum() > 0
+        finally:
+            r2.close()
         for _ in range(3):
             r.render_device(rci, acc, out, rows=rows, options=opt)
         torch.cuda.synchronize()
