@@ -685,6 +685,28 @@ def test_multi_logical_rebalance(rtvk, torch, logical_refs, rng_mode):
         assert len(end[0]) < len(start[0]) and len(end[3]) < len(start[3])
 
 
+def test_multi_logical_balancer_measured(rtvk, torch, logical_refs):
+    """rt_multi's balancer on its own measurements (no fed times): 3 logical devices, 6 frames;
+    from the third frame on each reads every device's kernel time and tile-cost row weights of the
+    frame two before (rt_launch_ms / rt_launch_row_weights internally) and may re-deal. Every frame
+    equals the oracle bit for bit; the partition always holds every row once."""
+    sc, rci_np, refs = logical_refs
+    (ra0, ro0, _), _ = refs[HASH]
+    rci = rtvk.RenderCallInfo.from_buffer_copy(rci_np.tobytes())
+    with rtvk.MultiRenderer(3, logical=True) as m:
+        m.tune(tolerance=0.0)   # re-deal on any measured gain (times on a shared GPU are uneven)
+        m.set_scene(sc)
+        acc = torch.zeros((LOGICAL_H, LOGICAL_W, 4), dtype=torch.float32, device="cuda:0")
+        out = torch.zeros((LOGICAL_H, LOGICAL_W, 4), dtype=torch.uint8, device="cuda:0")
+        for _ in range(6):
+            m.render(rci, acc, out, options=rtvk.make_options(rng_mode=HASH))
+            torch.cuda.synchronize()
+            assert_same(acc.cpu().numpy(), out.cpu().numpy(), ra0, ro0)
+            parts = m.partition(LOGICAL_H)
+            assert sorted(np.concatenate(parts).tolist()) == list(range(LOGICAL_H))
+        assert m.balance_info()["frames"] == 6
+
+
 @pytest.mark.parametrize("rng_mode", [STREAM, HASH])
 def test_multi_zero_spp_matches_one_device(rtvk, torch, oracle, rng_mode):
     """samplesPerRenderCall = 0 renders the same bytes at every device count (the
