@@ -5,7 +5,8 @@ kernel's duration (HIP events on the launch stream) and the tail after the work 
 same image (checked against the first setting's, bit for bit).
 
 usage: python scripts/band_tune.py [N=8] [spp=10000] [--rank 0] [--rounds 3] [--full]
-       [--width W --height H --grid K] [--set name:key=v,key=v ...] (default sets below)"""
+       [--width W --height H --grid K] [--rng hash|stream] [--set name:key=v,key=v ...]
+       (default sets below)"""
 import argparse
 import ctypes
 import json
@@ -40,6 +41,7 @@ ap.add_argument("--full", action="store_true", help="the whole frame instead of 
 ap.add_argument("--width", type=int, default=1920)
 ap.add_argument("--height", type=int, default=1080)
 ap.add_argument("--grid", type=int, default=11)
+ap.add_argument("--rng", choices=["hash", "stream"], default="hash")
 ap.add_argument("--set", nargs="*", default=None)
 args = ap.parse_args()
 W, H = args.width, args.height
@@ -54,7 +56,7 @@ for spec in (args.set or DEFAULT_SETS):
 lib = abi.load_library()
 scene = rtvk.generateRandomScene(0.0, args.grid)
 rci = rtvk.canonical_render_call_info(args.spp, W, H)
-opt = rtvk.make_options(accel=abi.RT_ACCEL_LBVH, rng_mode=rtvk.HASH)
+opt = rtvk.make_options(accel=abi.RT_ACCEL_LBVH, rng_mode=rtvk.HASH if args.rng == "hash" else rtvk.STREAM)
 rows_np = None if args.full else rtvk.partition_strips(args.n, H)[args.rank].astype(np.int32)
 n = H if rows_np is None else len(rows_np)
 rows = None if rows_np is None else torch.from_numpy(rows_np).cuda()
@@ -89,4 +91,4 @@ for name, v in res.items():
     ms = float(np.median(v["ms"]))
     print(f"{name:18s} {ms:9.2f} ms ({(ms / base - 1) * 100:+5.1f} %)  tail after queue dry "
           f"{np.median(v['tail_ms']):6.2f} ms  chunks head/tail {v['chunks']}", flush=True)
-print(json.dumps({"n": args.n, "rank": args.rank, "spp": args.spp, "full": args.full, "rows": n, "results": res}))
+print(json.dumps({"n": args.n, "rank": args.rank, "spp": args.spp, "rng": args.rng, "full": args.full, "rows": n, "results": res}))

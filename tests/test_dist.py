@@ -1,4 +1,4 @@
-"""Multi-GPU path (rtvk.dist) on CPU: world size 2-3 over gloo, the oracle rendering each rank's
+"""Multi-GPU path (rtvk.dist) on CPU: world size 2, 3 and 8 (the driver's N = 8 topology) over gloo, the oracle rendering each rank's
 rows. Checks the row-exact strip partition (equal to rt_partition_strips, the C++ rt_multi's),
 that gather + reassembly reproduce the one-device image bit for bit (global seeds make the image
 independent of the split), and the cross-rank balancer:
@@ -82,7 +82,7 @@ def _worker(rank, world, port, out_path, rng_mode=0, resolve_on_root=True, gathe
 
 @pytest.mark.parametrize("world,rng_mode,resolve_on_root,gather_accum",
                          [(2, 0, True, True), (2, 2, True, True), (3, 2, True, True), (2, 2, False, True),
-                          (2, 2, True, False)])
+                          (2, 2, True, False), (8, 2, True, True)])
 def test_gather_reassembly(tmp_path, oracle, world, rng_mode, resolve_on_root, gather_accum):
     """Strips on `world` gloo ranks, gathered and reassembled on rank 0, equal the one-device
     frame bit for bit, for the reference stream (rng_mode 0) and the counter-based stream (2):
@@ -155,7 +155,7 @@ def _balance_worker(rank, world, port, out_path, frames):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_balancer_redeals_rows(tmp_path, oracle, world):
     """Cross-rank balancing (rtvk.dist, rt_partition_rebalance): with a synthetic per-row cost that
     makes the bottom rows 3x dearer, the ranks re-deal band-end rows between frames (every rank the
