@@ -1,5 +1,5 @@
-"""Multi-GPU path (rtvk.dist) on CPU: world size 2, 3 and 8 (the driver's N = 8 topology) over gloo, the oracle rendering each rank's
-rows. Checks the row-exact strip partition (equal to rt_partition_strips, the C++ rt_multi's),
+"""Multi-GPU path (rtvk.dist) on CPU: world size 2, 3 and 8 (the driver's N = 8 topology) over
+gloo, the oracle rendering each rank's rows. Checks the row-exact strip partition (equal to rt_partition_strips, the C++ rt_multi's),
 that gather + reassembly reproduce the one-device image bit for bit (global seeds make the image
 independent of the split), and the cross-rank balancer:
 every rank re-deals the same partition from a synthetic per-row cost, the image stays exact every
