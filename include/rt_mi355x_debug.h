@@ -115,9 +115,9 @@ int rt_debug_multi_create_logical(uint32_t n_devices, rt_multi** out);
 int rt_debug_multi_create_logical_rccl(uint32_t n_devices, rt_multi** out);
 /* The balancer of m's strip frames: "balance" (1 on, 0 off), "tolerance" (re-deal above
  * (1 + tolerance) x the mean device time, by exchanges that gain more than tolerance x the mean;
- * default 0.001), "blend" (weight of a new measurement in the per-row estimates; default 0.5),
- * "lag" (frames between the measured frame and the one it re-deals; default 2); -1 restores the
- * default. */
+ * default 0.001), "blend" (weight in (0, 1] of a new measurement in the per-row estimates, above 1
+ * taken as 1; default 0.5), "lag" (frames between the measured frame and the one it re-deals, 1 to
+ * 8; default 2); -1 restores the default. Other values: RT_ERR_INVALID_ARGUMENT. */
 int rt_debug_multi_tune(rt_multi* m, const char* key, double value);
 /* Feeds n device times (ms) as if measured on the current partition: the next rt_multi_render
  * re-deals from them instead of its own measurement (tests: forced re-deals). */

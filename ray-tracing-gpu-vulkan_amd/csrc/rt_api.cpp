@@ -1542,9 +1542,10 @@ int rt_debug_kernel_times(rt_context* ctx, float* out_ms, uint32_t capacity, uin
     return RT_OK;
 }
 
-// Trace-kernel duration of ctx's launch `back` launches before its most recent one: waits for
-// that launch's end event only, so a caller reading a launch two frames old does not drain the
-// frames queued behind it (the cross-device balancer of rt_multi / rtvk.dist).
+// Per-row work of ctx's launch `back` launches before its most recent one, from its tile-cost
+// record (copied to pinned memory after the kernel once a caller has asked for weights): waits for
+// that copy only. The cross-device balancer of rt_multi / rtvk.dist splits a band's measured time
+// over its rows with it.
 int rt_launch_row_weights(rt_context* ctx, uint32_t back, double* weights, uint32_t band_rows) {
     if (!ctx || (!weights && band_rows)) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     rt::keep_row_weights(ctx);   // from now on, even when this call finds nothing
@@ -1556,6 +1557,9 @@ int rt_launch_row_weights(rt_context* ctx, uint32_t back, double* weights, uint3
     return RT_OK;
 }
 
+// Trace-kernel duration of ctx's launch `back` launches before its most recent one: waits for
+// that launch's end event only, so a caller reading a launch two frames old does not drain the
+// frames queued behind it.
 int rt_launch_ms(rt_context* ctx, uint32_t back, float* ms) {
     if (!ctx || !ms) return fail(RT_ERR_INVALID_ARGUMENT, "NULL argument");
     if (back >= ctx->kev_count || back >= rt_context::kKernelEvents)

@@ -77,6 +77,8 @@ struct Launch {
     float* stage_acc = nullptr;          // dev != 0: the band's copy on device 0
 };
 
+constexpr uint32_t kMaxLag = 8;   // strip frames the balancer keeps (its largest lag)
+
 // A rendered strip frame, for the balancer: its partition and each part's launch index on its
 // context (UINT64_MAX: the part rendered nothing).
 struct FrameRecord {
@@ -612,7 +614,7 @@ int rt_multi_render(rt_multi* m, const RenderCallInfo* rci, const rt_options* op
         for (const Launch& l : m->launches)
             r.launch.push_back(l.rows.empty() ? UINT64_MAX : rt::launch_count(l.ctx) - 1);
         m->bal.history.push_back(std::move(r));
-        while (m->bal.history.size() > 8) m->bal.history.pop_front();
+        while (m->bal.history.size() > kMaxLag) m->bal.history.pop_front();
         m->bal.frames++;
     } catch (const std::exception& e) {
         return fail(RT_ERR_OUT_OF_MEMORY, e.what());
@@ -643,8 +645,13 @@ int rt_debug_multi_tune(rt_multi* m, const char* key, double value) {
     const std::string k = key;
     if (k == "balance") m->bal.enabled = value < 0 ? true : value != 0.0;
     else if (k == "tolerance") m->bal.tolerance = value < 0 ? 0.001 : value;
-    else if (k == "blend") m->bal.blend = value < 0 ? 0.5 : std::min(1.0, value);
-    else if (k == "lag") m->bal.lag = value < 0 ? 2u : std::max<uint32_t>(1, uint32_t(value));
+    else if (k == "blend") {
+        if (value == 0.0 || !(value == value)) return fail(RT_ERR_INVALID_ARGUMENT, "blend must be in (0, 1]");
+        m->bal.blend = value < 0 ? 0.5 : std::min(1.0, value);
+    } else if (k == "lag") {
+        if (value >= 0 && value > double(kMaxLag)) return fail(RT_ERR_INVALID_ARGUMENT, "lag above the kept frames");
+        m->bal.lag = value < 0 ? 2u : std::max<uint32_t>(1, uint32_t(value));
+    }
     else return fail(RT_ERR_INVALID_ARGUMENT, "unknown key " + k);
     return RT_OK;
 }

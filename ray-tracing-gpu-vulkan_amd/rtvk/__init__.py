@@ -409,7 +409,8 @@ class MultiRenderer:
         return _split(rows, counts)
 
     def tune(self, **kv) -> None:
-        """Balancer settings (rt_debug_multi_tune): balance=0/1, tolerance, lag; None restores."""
+        """Balancer settings (rt_debug_multi_tune): balance=0/1, tolerance, blend in (0, 1], lag 1-8;
+        None restores a default."""
         for k, v in kv.items():
             check(self._lib.rt_debug_multi_tune(self._m, k.encode(), -1.0 if v is None else float(v)))
 

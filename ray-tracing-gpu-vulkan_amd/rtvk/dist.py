@@ -127,6 +127,8 @@ class DistributedRenderer:
         self.staged = (self.world > 1 and getattr(device, "type", str(device)) != "cpu"
                        and dist.get_backend() == "gloo")
         self.timer = timer if self.multi else None   # (one rank + force_gather: the exchange path runs, no move)
+        if not (0.0 < blend <= 1.0):
+            raise ValueError("blend must be in (0, 1]")
         self.tolerance, self.lag, self.blend = tolerance, max(1, int(lag)), blend
         self.cost = np.zeros(height, np.float64)
         self.history = deque()      # per frame: (partition, launch index of this rank or None)

@@ -179,3 +179,13 @@ def test_balancer_redeals_rows(tmp_path, oracle, world):
     assert int(got["rebalances"]) >= 1 and int(got["moved"]) >= 1
     assert imb[-1] < imb[0] - 0.05, imb
     assert imb[-1] <= 1.0 + 3.0 / (sum(_row_cost(y) for y in range(BH)) / world), imb
+
+
+def test_blend_outside_unit_interval_refused():
+    """DistributedRenderer takes rt_multi's balancer settings: blend in (0, 1] (0 would freeze the
+    per-row estimates; rt_debug_multi_tune refuses it too)."""
+    from rtvk.dist import DistributedRenderer
+    for b in (0.0, -0.5, 1.5):
+        with pytest.raises(ValueError):
+            DistributedRenderer(8, 8, torch.device("cpu"), lambda *a: None, blend=b)
+    DistributedRenderer(8, 8, torch.device("cpu"), lambda *a: None, blend=1.0)

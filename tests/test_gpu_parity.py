@@ -707,6 +707,17 @@ def test_multi_logical_balancer_measured(rtvk, torch, logical_refs):
         assert m.balance_info()["frames"] == 6
 
 
+def test_multi_tune_rejects_bad_settings(rtvk):
+    """rt_debug_multi_tune: blend in (0, 1] (0 would freeze the per-row estimates), lag 1-8 (the
+    frames the balancer keeps), unknown keys refused; -1 (None) restores a default."""
+    with rtvk.MultiRenderer(2, logical=True) as m:
+        for kv in ({"blend": 0.0}, {"lag": 9}, {"nonsense": 1}):
+            with pytest.raises(RuntimeError):
+                m.tune(**kv)
+        m.tune(blend=0.25, lag=8, tolerance=0.01)
+        m.tune(blend=None, lag=None, tolerance=None, balance=None)
+
+
 @pytest.mark.parametrize("rng_mode", [STREAM, HASH])
 def test_multi_zero_spp_matches_one_device(rtvk, torch, oracle, rng_mode):
     """samplesPerRenderCall = 0 renders the same bytes at every device count (the
