@@ -1241,6 +1241,47 @@ __device__ __forceinline__ void grid_walk(const rt::TraceParams& P, const uint32
     float tz = bound_t(cz, sz, 2, r.o.z, r.inv.z);
     // linear cell index (a step adds the stepped axis's stride, dda_step)
     uint32_t cell = FLAT ? uint32_t(cz) * n0 + uint32_t(cx) : (uint32_t(cz) * n1 + uint32_t(cy)) * n0 + uint32_t(cx);
+    // One-layer grid walked from L2 (config 5): the DDA steps before the cell's references are
+    // tested (the step does not depend on them; the cull test still uses this cell's exit t and the
+    // limit they leave), so the next cell's two offsets are requested before this cell's records
+    // and arrive while they are tested: one dependent L2 round trip per cell instead of two, the
+    // same cells and references in the same order. Config 5 -0.3 % (1 000 spp) / -0.9 % (100 spp),
+    // no new spills.
+    if constexpr (FLAT && PAIRS) {
+        uint32_t b = cstart[cell], e = cstart[cell + 1];
+        for (;;) {
+            const float tm = fminf(fminf(tx, ty), tz);
+            uint32_t ncell = cell;   // unchanged when the step leaves the grid: a valid address
+            const bool more = dda_step_xz(tm, tx, ty, tz, cx, cz, sx, sz, ncell, r.o, r.inv);
+            const uint32_t nb = cstart[ncell], ne = cstart[ncell + 1];
+            if (COUNT) {
+                n_cell++;
+                n_empty += b == e ? 1u : 0u;
+            }
+            uint32_t j = b;
+            for (; j + 1 < e; j += 2) {
+                UTIL(1, true);
+                const float4 s0 = rec[j], s1 = rec[j + 1];
+                const uint32_t i0 = ids[j], i1 = ids[j + 1];
+                test1<true>(s0, [&] { return i0; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
+                test1<true>(s1, [&] { return i1; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
+                if (COUNT) n_sph += 2;
+            }
+            if (j < e) {
+                UTIL(1, true);
+                const float4 s0 = rec[j];
+                const uint32_t i0 = ids[j];
+                test1<true>(s0, [&] { return i0; }, r.o, r.d, r.inv, r.a, r.ia, r.best, r.bi, r.limit, P);
+                if (COUNT) n_sph++;
+            }
+            UTIL(0, true);
+            if (!(tm <= r.limit) || !more) break;
+            b = nb;
+            e = ne;
+            cell = ncell;
+        }
+        return;
+    }
     for (;;) {
         // the cell's reference run [b, e): from L2 through one address, so both offsets come in one
         // 8-byte load (config 5 -1.0 %); the LDS pair is one ds_read2 either way
